@@ -1,0 +1,368 @@
+/*
+ * uwvk.h — C ABI of the MI355X-native batched UKF engine (PoseUKF / VelocityUKF).
+ *
+ * This is the drop-in boundary for the predict / measurement-update hot path of
+ * tomcreutz/slam-uwv_kalman_filters.  The reference exposes single-instance C++
+ * classes (src/PoseUKF.hpp:89-255, src/VelocityUKF.hpp:231-266) that derive from
+ * pose_estimation::UnscentedKalmanFilter<State> [EXT].  Each entry point below
+ * names the reference member it replaces (file:line).  Every call works on a
+ * BATCH of independent filter instances held in device memory by the handle;
+ * batch = 1 is the reference's single-instance case.
+ *
+ * Conventions
+ *  - Plain C types only.  Host arrays passed in are borrowed for the duration
+ *    of the call (copied to the device before it returns).
+ *  - Arrays are instance-major: element [i][k] of a per-instance array of width
+ *    K lives at index i*K + k.  Matrices are row-major, n x n.
+ *  - Quaternions are stored (w, x, y, z).
+ *  - One handle owns one HIP stream and is NOT thread-safe (the reference is
+ *    not re-entrant either: PoseUKF.cpp:173, VelocityUKF.cpp:18).
+ *  - Errors are returned as uwvk_status codes; the C++ facade
+ *    (slam-uwv_kalman_filters_amd/include/uwv_kalman_filters_amd/PoseUKF.hpp)
+ *    maps them to std::runtime_error like the reference's checkMeasurment [EXT]
+ *    (PoseUKF.cpp:478) and the missing-model throw (VelocityUKF.cpp:117-118).
+ *  - There is NO CPU fallback: without a usable gfx950 device every create call
+ *    returns UWVK_EDEVICE.
+ */
+#ifndef UWVK_H_
+#define UWVK_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UWVK_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+typedef enum uwvk_status {
+  UWVK_OK = 0,
+  UWVK_EINVAL = 1,   /* bad argument (null handle, wrong size, unsupported layout) */
+  UWVK_ENAN = 2,     /* NaN/Inf in a measurement mean or covariance (checkMeasurment [EXT]) */
+  UWVK_ENOTPD = 3,   /* covariance not positive definite in at least one instance */
+  UWVK_ENOMODEL = 4, /* VelocityUKF predict without setupMotionModel (VelocityUKF.cpp:117-118) */
+  UWVK_EDEVICE = 5,  /* no gfx950 device / HIP runtime error */
+  UWVK_ENOMEM = 6,
+  UWVK_ENOTINIT = 7  /* state or process noise not initialised */
+} uwvk_status;
+
+/* per-instance status bits (uwvk_pose_get_status / uwvk_vel_get_status) */
+#define UWVK_ST_NOTPD 0x1u    /* Cholesky of Sigma failed (non-positive pivot) */
+#define UWVK_ST_NAN 0x2u      /* non-finite measurement skipped for this instance */
+#define UWVK_ST_NONFINITE 0x4u/* non-finite state after a step */
+
+/* ---- PoseState layout (src/PoseState.hpp:29-45) ------------------------ */
+/* Full layout: 53 DOF, 54 stored scalars (SO3 as a quaternion).           */
+/* Kinematic layout: the same without inertia / lin_damping / quad_damping */
+/* (26 DOF, 27 stored scalars) — the "~30-dim" config of BASELINE.json.     */
+#define UWVK_POSE_DOF_FULL 53
+#define UWVK_POSE_STORE_FULL 54
+#define UWVK_POSE_DOF_KIN 26
+#define UWVK_POSE_STORE_KIN 27
+/* storage offsets, full layout */
+#define UWVK_S_POS 0
+#define UWVK_S_QUAT 3
+#define UWVK_S_VEL 7
+#define UWVK_S_ACC 10
+#define UWVK_S_BIAS_GYRO 13
+#define UWVK_S_BIAS_ACC 16
+#define UWVK_S_GRAVITY 19
+#define UWVK_S_INERTIA 20      /* 3x3 column-major (PoseState.hpp:37) */
+#define UWVK_S_LIN_DAMPING 29  /* 3x3 column-major */
+#define UWVK_S_QUAD_DAMPING 38 /* 3x3 column-major */
+#define UWVK_S_WATER_VEL 47
+#define UWVK_S_WATER_VEL_BELOW 49
+#define UWVK_S_BIAS_ADCP 51
+#define UWVK_S_WATER_DENSITY 53
+
+/* ---- configuration PODs (Eigen-free mirrors of PoseUKFConfig.hpp) ------ */
+typedef struct uwvk_inertial_noise { /* InertialNoiseParameters, PoseUKFConfig.hpp:50-63 */
+  double randomwalk[3];
+  double bias_offset[3];
+  double bias_instability[3];
+  double bias_tau;
+} uwvk_inertial_noise;
+
+typedef struct uwvk_model_noise { /* DynamicModelNoiseParameters, PoseUKFConfig.hpp:65-97 */
+  double body_efforts_std[6];
+  double inertia_instability[9];
+  double lin_damping_instability[9];
+  double quad_damping_instability[9];
+  double inertia_tau;
+  double lin_damping_tau;
+  double quad_damping_tau;
+} uwvk_model_noise;
+
+typedef struct uwvk_water_velocity { /* WaterVelocityParameters, PoseUKFConfig.hpp:20-48 */
+  double tau;
+  double limits;
+  double measurement_std[3];
+  double scale;
+  double cell_size;
+  double first_cell_blank;
+  double minimum_correlation;
+  double adcp_bias_tau;
+  double adcp_bias_limits;
+} uwvk_water_velocity;
+
+typedef struct uwvk_location { /* LocationConfiguration, PoseUKFConfig.hpp:99-109 */
+  double latitude;  /* rad */
+  double longitude; /* rad */
+  double altitude;  /* m */
+} uwvk_location;
+
+typedef struct uwvk_hydrostatics { /* HydrostaticConfiguration, PoseUKFConfig.hpp:145-157 */
+  double water_density;
+  double water_density_limits;
+  double water_density_tau;
+  double atmospheric_pressure;
+  double pressure_std;
+} uwvk_hydrostatics;
+
+typedef struct uwvk_pose_config { /* PoseUKFConfig, PoseUKFConfig.hpp:159-194 (visual landmarks: out of scope) */
+  uwvk_inertial_noise acceleration;
+  uwvk_inertial_noise rotation_rate;
+  uwvk_model_noise model_noise_parameters;
+  uwvk_water_velocity water_velocity;
+  uwvk_location location;
+  uwvk_hydrostatics hydrostatics;
+  double max_jerk[3];
+  double max_effort[6];
+  double dynamic_model_min_depth;
+} uwvk_pose_config;
+
+/* [EXT] uwv_dynamic_model::UWVParameters, the subset the hot path reads
+ * (PoseUKF.cpp:159-171, VelocityUKF.cpp:60-74).  6x6 matrices row-major.
+ * Forces/torques follow M*nu_dot + C(nu)*nu + D_l*nu + D_q*|nu|*nu + g(q) = tau. */
+typedef struct uwvk_uwv_params {
+  double inertia_matrix[36];
+  double damping_matrices[2][36]; /* [0] linear, [1] quadratic */
+  double weight;
+  double buoyancy;
+  double distance_body2centerofgravity[3];
+  double distance_body2centerofbuoyancy[3];
+} uwvk_uwv_params;
+
+/* PoseUKF::PoseUKFParameter, PoseUKF.hpp:46-76 */
+typedef struct uwvk_pose_parameter {
+  double imu_in_body[3];
+  double gyro_bias_offset[3];
+  double gyro_bias_tau;
+  double acc_bias_offset[3];
+  double acc_bias_tau;
+  double inertia_tau;
+  double lin_damping_tau;
+  double quad_damping_tau;
+  double water_velocity_tau;
+  double water_velocity_limits;
+  double water_velocity_scale;
+  double adcp_bias_tau;
+  double atmospheric_pressure;
+  double water_density_tau;
+} uwvk_pose_parameter;
+
+/* ---- library ------------------------------------------------------------ */
+int uwvk_abi_version(void);
+/* 1 when a gfx950 device is visible and the kernels' code object loads. */
+int uwvk_device_available(int device);
+const char* uwvk_status_string(uwvk_status s);
+
+/* device memory helpers for device-resident logs (bench / run_log) */
+uwvk_status uwvk_device_malloc(int device, size_t bytes, void** out);
+uwvk_status uwvk_device_free(void* p);
+uwvk_status uwvk_memcpy_h2d(void* dst, const void* src, size_t bytes);
+uwvk_status uwvk_memcpy_d2h(void* dst, const void* src, size_t bytes);
+
+/* ======================================================================== */
+/* PoseUKF                                                                   */
+/* ======================================================================== */
+typedef struct uwvk_pose uwvk_pose;
+
+/* dof = 53 (PoseState) or 26 (kinematic subset).  Allocates device state. */
+uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out);
+void uwvk_pose_destroy(uwvk_pose* h);
+int64_t uwvk_pose_batch(const uwvk_pose* h);
+int uwvk_pose_dof(const uwvk_pose* h);
+/* hipStream_t of the handle (as void*), for event timing by the caller. */
+void* uwvk_pose_stream(const uwvk_pose* h);
+uwvk_status uwvk_pose_synchronize(uwvk_pose* h);
+
+/* PoseUKF::PoseUKF(pos, pos_cov, rot, rot_cov, cfg, uwv, imu_in_body)
+ * (PoseUKF.hpp:100-103, PoseUKF.cpp:288-372).  Per instance: pos[3],
+ * pos_cov[9], rot[4] (w,x,y,z), rot_cov[9].  imu_in_body = {tx,ty,tz,qw,qx,qy,qz}
+ * (NULL = identity), shared by the batch. */
+uwvk_status uwvk_pose_init_from_config(uwvk_pose* h, const double* pos, const double* pos_cov,
+                                       const double* rot, const double* rot_cov,
+                                       const uwvk_pose_config* cfg, const uwvk_uwv_params* uwv,
+                                       const double imu_in_body[7]);
+/* PoseUKF::PoseUKF(state, cov, location, uwv, param) (PoseUKF.hpp:113-115,
+ * PoseUKF.cpp:374-391).  x: batch*store, P: batch*dof*dof. */
+uwvk_status uwvk_pose_init_from_state(uwvk_pose* h, const double* x, const double* P,
+                                      const uwvk_location* location, const uwvk_uwv_params* uwv,
+                                      const uwvk_pose_parameter* param);
+/* setProcessNoiseFromConfig (PoseUKF.hpp:126-127, PoseUKF.cpp:393-439);
+ * q_imu_in_body (w,x,y,z) may be NULL (identity). */
+uwvk_status uwvk_pose_set_process_noise_from_config(uwvk_pose* h, const uwvk_pose_config* cfg,
+                                                    double imu_delta_t, const double q_imu_in_body[4]);
+/* setProcessNoiseCovariance [EXT base]: dof*dof, shared by the batch. */
+uwvk_status uwvk_pose_set_process_noise(uwvk_pose* h, const double* Q);
+
+/* integrateMeasurement(RotationRate) (PoseUKF.cpp:492-496): stores omega.
+ * w: batch*3, cov: batch*9 (checked for NaN only, may be NULL). */
+uwvk_status uwvk_pose_set_rotation_rate(uwvk_pose* h, const double* w, const double* cov);
+/* predictionStep(dt) -> predictionStepImpl (PoseUKF.cpp:446-474). */
+uwvk_status uwvk_pose_predict(uwvk_pose* h, double dt);
+
+/* Measurement updates.  mu: batch*m, cov: batch*m*m (NULL = shared_cov),
+ * shared_cov: m*m used when cov == NULL.  mask: batch bytes, 0 = skip this
+ * instance (NULL = all).  accepted (out, nullable): batch bytes, 1 when the
+ * innovation gate passed and the state was updated. */
+/* integrateMeasurement(Acceleration) (PoseUKF.cpp:484-490), m = 3 */
+uwvk_status uwvk_pose_update_acceleration(uwvk_pose* h, const double* mu, const double* cov,
+                                          const double* shared_cov, const uint8_t* mask, uint8_t* accepted);
+/* integrateMeasurement(Velocity) (PoseUKF.cpp:476-482), m = 3, DVL in IMU frame */
+uwvk_status uwvk_pose_update_velocity(uwvk_pose* h, const double* mu, const double* cov,
+                                      const double* shared_cov, const uint8_t* mask, uint8_t* accepted);
+/* integrateMeasurement(Pressure, sensor_in_imu) (PoseUKF.cpp:559-565), m = 1 */
+uwvk_status uwvk_pose_update_pressure(uwvk_pose* h, const double* mu, const double* cov,
+                                      const double* shared_cov, const double sensor_in_imu[3],
+                                      const uint8_t* mask, uint8_t* accepted);
+/* integrateMeasurement(WaterVelocityMeasurement, cell_weighting)
+ * (PoseUKF.cpp:604-611), m = 2, d2p95 gate.  cell_weighting: batch doubles. */
+uwvk_status uwvk_pose_update_water_velocity(uwvk_pose* h, const double* mu, const double* cov,
+                                            const double* shared_cov, const double* cell_weighting,
+                                            const uint8_t* mask, uint8_t* accepted);
+/* integrateMeasurement(BodyEffortsMeasurement, only_affect_velocity)
+ * (PoseUKF.cpp:581-602), m = 6. */
+uwvk_status uwvk_pose_update_efforts(uwvk_pose* h, const double* mu, const double* cov,
+                                     const double* shared_cov, int only_affect_velocity,
+                                     const uint8_t* mask, uint8_t* accepted);
+/* integrateMeasurement(XY_Position) (PoseUKF.cpp:506-512), m = 2 */
+uwvk_status uwvk_pose_update_xy(uwvk_pose* h, const double* mu, const double* cov,
+                                const double* shared_cov, const uint8_t* mask, uint8_t* accepted);
+/* integrateMeasurement(Z_Position) (PoseUKF.cpp:498-504), m = 1 */
+uwvk_status uwvk_pose_update_z(uwvk_pose* h, const double* mu, const double* cov,
+                               const double* shared_cov, const uint8_t* mask, uint8_t* accepted);
+/* integrateMeasurement(GeographicPosition, gps_in_body) (PoseUKF.cpp:567-579),
+ * m = 2 (lat, lon in rad), d2p95 gate. */
+uwvk_status uwvk_pose_update_geographic(uwvk_pose* h, const double* mu, const double* cov,
+                                        const double* shared_cov, const double gps_in_body[3],
+                                        const uint8_t* mask, uint8_t* accepted);
+/* integrateDelayedPositionMeasurement (PoseUKF.cpp:514-527): delayed_xy batch*2 */
+uwvk_status uwvk_pose_update_delayed_xy(uwvk_pose* h, const double* mu, const double* cov,
+                                        const double* shared_cov, const double* delayed_xy,
+                                        const uint8_t* mask, uint8_t* accepted);
+/* resetFilterWithExternalPose (PoseUKF.cpp:685-691): pose batch*7 {t, q(w,x,y,z)} */
+uwvk_status uwvk_pose_reset_with_external_pose(uwvk_pose* h, const double* pose);
+
+/* getCurrentState / ukf->mu(), ukf->sigma() [EXT]: x batch*store, P batch*dof*dof (nullable) */
+uwvk_status uwvk_pose_get_state(uwvk_pose* h, double* x, double* P);
+/* getRotationRate (PoseUKF.cpp:693-699): batch*3 */
+uwvk_status uwvk_pose_get_rotation_rate(uwvk_pose* h, double* out);
+/* per-instance status words (UWVK_ST_*), batch uint32; clear = 1 resets them */
+uwvk_status uwvk_pose_get_status(uwvk_pose* h, uint32_t* status, int clear);
+
+/* ---- device-resident measurement log (persistent multi-epoch path) ----- */
+/* Event flags per epoch (what the out-of-repo driver would call, §3 of SURVEY):
+ * every epoch: RotationRate -> predictionStep(dt) -> Acceleration update;
+ * then, when flagged: Velocity (DVL), Pressure, ADCP cells, BodyEfforts. */
+#define UWVK_EV_ACC 0x1u
+#define UWVK_EV_DVL 0x2u
+#define UWVK_EV_PRESSURE 0x4u
+#define UWVK_EV_ADCP 0x8u
+#define UWVK_EV_EFFORTS 0x10u
+#define UWVK_EV_EFFORTS_VELOCITY_ONLY 0x20u
+
+typedef struct uwvk_pose_log {
+  /* ALL pointers are DEVICE pointers (uwvk_device_malloc) unless noted. */
+  int64_t epochs;
+  double dt;                 /* predict step, seconds (host value) */
+  const uint32_t* flags;     /* [epochs] UWVK_EV_* */
+  const double* gyro;        /* [epochs][batch][3] */
+  const double* acc;         /* [epochs][batch][3] */
+  double acc_cov[9];         /* host value, shared */
+  const int32_t* dvl_index;  /* [epochs] row into dvl (valid when EV_DVL) */
+  const double* dvl;         /* [n_dvl][batch][3] */
+  double dvl_cov[9];
+  const int32_t* pressure_index;
+  const double* pressure;    /* [n_pressure][batch] */
+  double pressure_cov;
+  double pressure_sensor_in_imu[3];
+  const int32_t* adcp_index;
+  const double* adcp;        /* [n_adcp][cells][batch][2] */
+  int32_t adcp_cells;
+  double adcp_cell_weighting[8]; /* host values, per cell */
+  double adcp_cov[4];
+  const int32_t* efforts_index;
+  const double* efforts;     /* [n_efforts][batch][6] */
+  double efforts_cov[36];
+} uwvk_pose_log;
+
+/* Runs epochs [first, first+count) of the log; one fused kernel launch per
+ * epoch (predict + all flagged updates with Sigma resident in LDS).
+ * accept_counts (device, nullable): [batch][4] uint32 accepted DVL/pressure/ADCP/efforts. */
+uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t first, int64_t count,
+                              uint32_t* accept_counts);
+
+/* Ensemble statistics over the batch (for Monte-Carlo runs):
+ * out[0..store)        = sum_i x_i (orientation quaternion summed componentwise)
+ * out[store..2*store)  = sum_i x_i^2
+ * out[2*store..3*store)= sum_i (x_i - truth)^2 (orientation: rotation-vector error, 3 entries used)
+ * out[3*store]         = sum_i NEES_i over (position, orientation, velocity) (9 DOF)
+ * truth: host store-vector (nullable -> zeros).  out: host doubles, 3*store+1. */
+uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* out);
+
+/* Kernel-timing helper: HIP events recorded on the handle's stream. */
+uwvk_status uwvk_pose_timer_start(uwvk_pose* h);
+uwvk_status uwvk_pose_timer_stop(uwvk_pose* h, float* elapsed_ms);
+
+/* ======================================================================== */
+/* VelocityUKF (src/VelocityUKF.hpp:231-266)                                 */
+/* ======================================================================== */
+#define UWVK_VEL_DOF 4
+typedef struct uwvk_vel uwvk_vel;
+
+uwvk_status uwvk_vel_create(int64_t batch, int device, uwvk_vel** out);
+void uwvk_vel_destroy(uwvk_vel* h);
+void* uwvk_vel_stream(const uwvk_vel* h);
+/* VelocityUKF(state, cov) (VelocityUKF.cpp:49-56): x batch*4 {v, z}, P batch*16 */
+uwvk_status uwvk_vel_init(uwvk_vel* h, const double* x, const double* P);
+/* setupMotionModel (VelocityUKF.cpp:58-77) */
+uwvk_status uwvk_vel_setup_motion_model(uwvk_vel* h, const uwvk_uwv_params* uwv);
+/* GyroMeasurement (VelocityUKF.cpp:87-98): batch*3 */
+uwvk_status uwvk_vel_set_gyro(uwvk_vel* h, const double* w, const double* cov);
+/* BodyEffortsMeasurement (VelocityUKF.cpp:100-104): batch*6 */
+uwvk_status uwvk_vel_set_efforts(uwvk_vel* h, const double* tau, const double* cov);
+/* predictionStep -> predictionStepImpl (VelocityUKF.cpp:114-130) */
+uwvk_status uwvk_vel_predict(uwvk_vel* h, double dt);
+/* DVLMeasurement (VelocityUKF.cpp:79-85), m = 3 */
+uwvk_status uwvk_vel_update_dvl(uwvk_vel* h, const double* mu, const double* cov, const double* shared_cov,
+                                const uint8_t* mask);
+/* PressureMeasurement (z) (VelocityUKF.cpp:106-112), m = 1 */
+uwvk_status uwvk_vel_update_pressure(uwvk_vel* h, const double* mu, const double* cov, const double* shared_cov,
+                                     const uint8_t* mask);
+uwvk_status uwvk_vel_get_state(uwvk_vel* h, double* x, double* P);
+/* motion-model side state: batch*13 {p(3), q(4: w,x,y,z), v(3), w(3)} */
+uwvk_status uwvk_vel_get_model_state(uwvk_vel* h, double* out);
+
+typedef struct uwvk_vel_log {
+  int64_t epochs;
+  double dt;
+  const uint32_t* flags;    /* UWVK_EV_DVL / UWVK_EV_PRESSURE */
+  const double* gyro;       /* [epochs][batch][3] */
+  const double* efforts;    /* [epochs][batch][6] */
+  const int32_t* dvl_index;
+  const double* dvl;        /* [n_dvl][batch][3] */
+  double dvl_cov[9];
+  const int32_t* pressure_index;
+  const double* pressure;   /* [n_pressure][batch] (z position) */
+  double pressure_cov;
+} uwvk_vel_log;
+uwvk_status uwvk_vel_run_log(uwvk_vel* h, const uwvk_vel_log* log, int64_t first, int64_t count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UWVK_H_ */

@@ -1,0 +1,261 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — never by the product path.
+PARITY STATUS: unpinned against the reference binary (see uwvk_oracle.h).
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+from uwvk import abi  # noqa: E402
+
+_LIB = None
+DP = C.POINTER(C.c_double)
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.or_pose_sizeof.restype = C.c_size_t
+        L.or_vel_sizeof.restype = C.c_size_t
+        L.or_wgs84_gravity.restype = C.c_double
+        _LIB = L
+    return _LIB
+
+
+def dp(a):
+    if a is None:
+        return None
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a.ctypes.data_as(DP)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class RunArgs(C.Structure):
+    P = C.c_void_p
+    _fields_ = [("batch", C.c_int64), ("epochs", C.c_int64), ("dt", C.c_double), ("flags", P), ("gyro", P),
+                ("acc", P), ("acc_cov", C.c_double * 9), ("dvl_index", P), ("dvl", P), ("dvl_cov", C.c_double * 9),
+                ("pressure_index", P), ("pressure", P), ("pressure_cov", C.c_double),
+                ("pressure_sensor_in_imu", C.c_double * 3), ("adcp_index", P), ("adcp", P),
+                ("adcp_cells", C.c_int32), ("adcp_cell_weighting", C.c_double * 8), ("adcp_cov", C.c_double * 4),
+                ("efforts_index", P), ("efforts", P), ("efforts_cov", C.c_double * 36)]
+
+
+class OraclePoseBatch:
+    """`batch` independent oracle PoseUKF instances in one contiguous buffer."""
+
+    def __init__(self, batch, dof=53):
+        self.L = lib()
+        self.batch, self.dof = batch, dof
+        self.lay = abi.layout(dof)
+        self.sz = self.L.or_pose_sizeof()
+        self.buf = (C.c_char * (self.sz * batch))()
+        self._keep = []
+
+    def ptr(self, i):
+        return C.cast(C.addressof(self.buf) + i * self.sz, C.c_void_p)
+
+    def init_from_config(self, pos, pos_cov, rot, rot_cov, cfg, uwv, imu_in_body=None):
+        pos, pos_cov, rot, rot_cov = map(_f64, (pos, pos_cov, rot, rot_cov))
+        ib = dp(imu_in_body) if imu_in_body is not None else None
+        for i in range(self.batch):
+            e = self.L.or_pose_init_from_config(self.ptr(i), self.dof, dp(pos[i]), dp(pos_cov[i]), dp(rot[i]),
+                                                dp(rot_cov[i]), C.byref(cfg), C.byref(uwv), ib)
+            assert e == 0
+
+    def init_from_state(self, x, P, loc, uwv, param):
+        x, P = _f64(x), _f64(P)
+        for i in range(self.batch):
+            assert self.L.or_pose_init_from_state(self.ptr(i), self.dof, dp(x[i]), dp(P[i]), C.byref(loc),
+                                                  C.byref(uwv), C.byref(param)) == 0
+
+    def set_process_noise_from_config(self, cfg, dt, q_imu_in_body=None):
+        qb = dp(q_imu_in_body) if q_imu_in_body is not None else None
+        for i in range(self.batch):
+            self.L.or_pose_set_process_noise_from_config(self.ptr(i), C.byref(cfg), C.c_double(dt), qb)
+
+    def set_process_noise(self, Q):
+        for i in range(self.batch):
+            self.L.or_pose_set_process_noise(self.ptr(i), dp(Q))
+
+    def set_rotation_rate(self, w):
+        w = _f64(w)
+        for i in range(self.batch):
+            assert self.L.or_pose_set_rotation_rate(self.ptr(i), dp(w[i]), None) == 0
+
+    def predict(self, dt):
+        for i in range(self.batch):
+            e = self.L.or_pose_predict(self.ptr(i), C.c_double(dt))
+            if e:
+                raise RuntimeError("oracle predict failed: %s" % abi.STATUS.get(e, e))
+
+    def update(self, kind, mu, cov, extra=None, only_vel=0):
+        """kind in acceleration/velocity/pressure/water_velocity/efforts/xy/z/geographic/delayed_xy."""
+        mu = _f64(mu)
+        cov = _f64(cov)
+        acc = np.zeros(self.batch, np.uint8)
+        a = C.c_int(0)
+        fn = getattr(self.L, "or_pose_update_" + kind)
+        for i in range(self.batch):
+            c = cov[i] if cov.ndim == mu.ndim + 1 else cov
+            args = [self.ptr(i), dp(mu[i]), dp(c)]
+            if kind == "pressure":
+                args.append(dp(extra if extra is not None else np.zeros(3)))
+            elif kind == "water_velocity":
+                args.append(C.c_double(float(np.broadcast_to(extra, (self.batch,))[i])))
+            elif kind == "efforts":
+                args.append(C.c_int(only_vel))
+            elif kind == "geographic":
+                args.append(dp(extra if extra is not None else np.zeros(3)))
+            elif kind == "delayed_xy":
+                args.append(dp(_f64(extra)[i]))
+            args.append(C.byref(a))
+            e = fn(*args)
+            if e:
+                raise RuntimeError("oracle update %s failed: %s" % (kind, abi.STATUS.get(e, e)))
+            acc[i] = a.value
+        return acc
+
+    def reset_with_external_pose(self, pose):
+        pose = _f64(pose)
+        for i in range(self.batch):
+            self.L.or_pose_reset_with_external_pose(self.ptr(i), dp(pose[i]))
+
+    def get_state(self):
+        n, s = self.dof, self.lay["store"]
+        x = np.empty((self.batch, s))
+        P = np.empty((self.batch, n, n))
+        for i in range(self.batch):
+            self.L.or_pose_get_state(self.ptr(i), x[i].ctypes.data_as(DP),
+                                     P[i].ctypes.data_as(DP))
+        return x, P
+
+    def get_rotation_rate(self):
+        out = np.empty((self.batch, 3))
+        for i in range(self.batch):
+            self.L.or_pose_get_rotation_rate(self.ptr(i), dp(out[i]))
+        return out
+
+    def run_log(self, log, first=0, count=None, nthreads=1):
+        count = log["epochs"] - first if count is None else count
+        a = RunArgs()
+        a.batch, a.epochs, a.dt = self.batch, log["epochs"], log["dt"]
+        keep = {}
+
+        def put(name, arr, dtype):
+            arr = np.ascontiguousarray(arr, dtype=dtype)
+            keep[name] = arr
+            return arr.ctypes.data
+
+        a.flags = put("flags", log["flags"], np.uint32)
+        a.gyro = put("gyro", log["gyro"], np.float64)
+        a.acc = put("acc", log["acc"], np.float64)
+        abi.fill(a.acc_cov, np.asarray(log["acc_cov"]).ravel())
+        a.dvl_index = put("dvl_index", log["dvl_index"], np.int32)
+        a.dvl = put("dvl", log["dvl"] if log["dvl"].size else np.zeros(3), np.float64)
+        abi.fill(a.dvl_cov, np.asarray(log["dvl_cov"]).ravel())
+        a.pressure_index = put("pressure_index", log["pressure_index"], np.int32)
+        a.pressure = put("pressure", log["pressure"] if log["pressure"].size else np.zeros(1), np.float64)
+        a.pressure_cov = float(log["pressure_cov"])
+        abi.fill(a.pressure_sensor_in_imu, log["pressure_sensor_in_imu"])
+        a.adcp_index = put("adcp_index", log["adcp_index"], np.int32)
+        a.adcp = put("adcp", log["adcp"] if log["adcp"].size else np.zeros(2), np.float64)
+        a.adcp_cells = int(log["adcp_cells"])
+        abi.fill(a.adcp_cell_weighting, log["adcp_cell_weighting"])
+        abi.fill(a.adcp_cov, np.asarray(log["adcp_cov"]).ravel())
+        a.efforts_index = put("efforts_index", log["efforts_index"], np.int32)
+        a.efforts = put("efforts", log["efforts"] if log["efforts"].size else np.zeros(6), np.float64)
+        abi.fill(a.efforts_cov, np.asarray(log["efforts_cov"]).ravel())
+        counts = np.zeros((self.batch, 4), np.uint32)
+        e = self.L.or_pose_run_log(C.cast(C.addressof(self.buf), C.c_void_p), C.byref(a), C.c_int64(first),
+                                   C.c_int64(count), C.c_int(nthreads), counts.ctypes.data_as(C.c_void_p))
+        if e:
+            raise RuntimeError("oracle run_log failed: %s" % abi.STATUS.get(e, e))
+        return counts
+
+
+class OracleVelBatch:
+    def __init__(self, batch):
+        self.L = lib()
+        self.batch = batch
+        self.sz = self.L.or_vel_sizeof()
+        self.buf = (C.c_char * (self.sz * batch))()
+
+    def ptr(self, i):
+        return C.cast(C.addressof(self.buf) + i * self.sz, C.c_void_p)
+
+    def init(self, x, P):
+        x, P = _f64(x), _f64(P)
+        for i in range(self.batch):
+            self.L.or_vel_init(self.ptr(i), dp(x[i]), dp(P[i]))
+
+    def setup_motion_model(self, uwv):
+        for i in range(self.batch):
+            self.L.or_vel_setup_motion_model(self.ptr(i), C.byref(uwv))
+
+    def set_gyro(self, w):
+        w = _f64(w)
+        for i in range(self.batch):
+            assert self.L.or_vel_set_gyro(self.ptr(i), dp(w[i]), None) == 0
+
+    def set_efforts(self, t):
+        t = _f64(t)
+        for i in range(self.batch):
+            assert self.L.or_vel_set_efforts(self.ptr(i), dp(t[i]), None) == 0
+
+    def predict(self, dt):
+        for i in range(self.batch):
+            e = self.L.or_vel_predict(self.ptr(i), C.c_double(dt))
+            if e:
+                raise RuntimeError("oracle vel predict failed: %s" % abi.STATUS.get(e, e))
+
+    def update_dvl(self, mu, cov):
+        mu = _f64(mu)
+        for i in range(self.batch):
+            assert self.L.or_vel_update_dvl(self.ptr(i), dp(mu[i]), dp(cov)) == 0
+
+    def update_pressure(self, mu, cov):
+        mu = _f64(mu)
+        for i in range(self.batch):
+            assert self.L.or_vel_update_pressure(self.ptr(i), dp(mu[i:i + 1]), dp(np.array([cov]))) == 0
+
+    def get_state(self, model=False):
+        x = np.empty((self.batch, 4))
+        P = np.empty((self.batch, 4, 4))
+        ms = np.empty((self.batch, 13))
+        for i in range(self.batch):
+            self.L.or_vel_get_state(self.ptr(i), x[i].ctypes.data_as(DP), P[i].ctypes.data_as(DP),
+                                    ms[i].ctypes.data_as(DP))
+        return (x, P, ms) if model else (x, P)
+
+    def run_log(self, log, first=0, count=None):
+        count = log["epochs"] - first if count is None else count
+        B = self.batch
+        for e in range(first, first + count):
+            self.set_gyro(log["gyro"][e])
+            self.set_efforts(log["efforts"][e])
+            self.predict(log["dt"])
+            f = log["flags"][e]
+            if f & abi.EV_DVL:
+                self.update_dvl(log["dvl"][log["dvl_index"][e]], log["dvl_cov"])
+            if f & abi.EV_PRESSURE:
+                self.update_pressure(log["pressure"][log["pressure_index"][e]], log["pressure_cov"])
+        return B

@@ -1,0 +1,414 @@
+// uwvk_pose.hip — PoseUKF kernels (gfx950) and the uwvk_pose_* C ABI.
+//
+// Grid: one 64-thread workgroup (= one wavefront) per filter instance.
+// Every kernel loads (mu, Sigma) of its instance into LDS once, runs one or
+// more predict / update steps on it and writes it back.  The fused epoch
+// kernel (k_pose_epoch) is the hot path of uwvk_pose_run_log:
+//   RotationRate -> predictionStep(dt) -> Acceleration update
+//   [-> Velocity (DVL) -> Pressure -> ADCP cells -> BodyEfforts]
+// with Sigma resident in LDS across all steps of the epoch.
+#include "uwvk_pose_kernels.hpp"
+#include "uwvk_host.hpp"
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+using namespace uwvk;
+
+
+// ===========================================================================
+// host side
+// ===========================================================================
+struct uwvk_pose {
+  int64_t batch = 0;
+  int dof = 53, store = 54, device = 0;
+  hipStream_t stream = nullptr;
+  double *d_mu = nullptr, *d_sigma = nullptr, *d_Q = nullptr, *d_rot = nullptr, *d_off = nullptr,
+         *d_model = nullptr, *d_uwv = nullptr;
+  uint32_t* d_status = nullptr;
+  double* d_meas = nullptr;  // staging: batch*36 (mu) + batch*36 (cov) + batch*2 (extra)
+  uint8_t* d_mask = nullptr;
+  uint8_t* d_accepted = nullptr;
+  double* d_scratch = nullptr;  // ensemble stats / rotation rate outputs
+  PoseShared sh{};
+  uwvk_location loc{};
+  uwvk_uwv_params uwv{};
+  bool has_state = false, has_Q = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+static PoseBufs bufs(const uwvk_pose* h) {
+  PoseBufs b;
+  b.batch = h->batch; b.mu = h->d_mu; b.sigma = h->d_sigma; b.Q = h->d_Q; b.rot = h->d_rot; b.off = h->d_off;
+  b.model = h->d_model; b.uwv = h->d_uwv; b.status = h->d_status;
+  return b;
+}
+
+static void set_shared(uwvk_pose* h, const uwvk_pose_parameter& p, const uwvk_location& loc,
+                       const uwvk_uwv_params& uwv) {
+  h->loc = loc;
+  h->uwv = uwv;
+  h->sh.p = p;
+  double rm, rn;
+  host::wgs84_radii(loc.latitude, &rm, &rn);
+  h->sh.lat0 = loc.latitude;
+  h->sh.lon0 = loc.longitude;
+  h->sh.rm = rm;
+  h->sh.inv_rm = 1.0 / rm;
+  h->sh.rn_cos = rn * std::cos(loc.latitude);
+  h->sh.uwv_weight = uwv.weight;
+  h->sh.uwv_buoyancy = uwv.buoyancy;
+  for (int k = 0; k < 3; k++) {
+    h->sh.cog[k] = uwv.distance_body2centerofgravity[k];
+    h->sh.cob[k] = uwv.distance_body2centerofbuoyancy[k];
+  }
+}
+
+#define HIPCHK(x)                              \
+  do {                                         \
+    if ((x) != hipSuccess) return UWVK_EDEVICE; \
+  } while (0)
+
+
+static bool finite_all(const double* a, size_t n) {
+  for (size_t k = 0; k < n; k++)
+    if (!std::isfinite(a[k])) return false;
+  return true;
+}
+
+extern "C" {
+
+uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out) {
+  if (!out || batch <= 0 || (dof != 53 && dof != 26)) return UWVK_EINVAL;
+  *out = nullptr;
+  if (!uwvk_device_available(device)) return UWVK_EDEVICE;
+  uwvk_pose* h = new uwvk_pose();
+  h->batch = batch;
+  h->dof = dof;
+  h->store = dof == 53 ? 54 : 27;
+  h->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return UWVK_EDEVICE;
+  }
+  const size_t B = (size_t)batch, n = (size_t)dof;
+  bool ok = hipMalloc(&h->d_mu, B * h->store * 8) == hipSuccess && hipMalloc(&h->d_sigma, B * n * n * 8) == hipSuccess &&
+            hipMalloc(&h->d_Q, n * n * 8) == hipSuccess && hipMalloc(&h->d_rot, B * 3 * 8) == hipSuccess &&
+            hipMalloc(&h->d_off, B * 28 * 8) == hipSuccess && hipMalloc(&h->d_model, B * 27 * 8) == hipSuccess &&
+            hipMalloc(&h->d_uwv, 108 * 8) == hipSuccess && hipMalloc(&h->d_status, B * 4) == hipSuccess &&
+            hipMalloc(&h->d_meas, B * 74 * 8) == hipSuccess && hipMalloc(&h->d_mask, B) == hipSuccess &&
+            hipMalloc(&h->d_accepted, B) == hipSuccess && hipMalloc(&h->d_scratch, (B * 3 + 256) * 8) == hipSuccess &&
+            hipEventCreate(&h->ev0) == hipSuccess && hipEventCreate(&h->ev1) == hipSuccess;
+  if (!ok) {
+    uwvk_pose_destroy(h);
+    return UWVK_ENOMEM;
+  }
+  (void)hipMemsetAsync(h->d_status, 0, B * 4, h->stream);
+  (void)hipMemsetAsync(h->d_rot, 0, B * 3 * 8, h->stream);
+  (void)hipMemsetAsync(h->d_Q, 0, n * n * 8, h->stream);
+  if (hipStreamSynchronize(h->stream) != hipSuccess) {
+    uwvk_pose_destroy(h);
+    return UWVK_EDEVICE;
+  }
+  *out = h;
+  return UWVK_OK;
+}
+
+void uwvk_pose_destroy(uwvk_pose* h) {
+  if (!h) return;
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_Q, (void*)h->d_rot, (void*)h->d_off,
+                  (void*)h->d_model, (void*)h->d_uwv, (void*)h->d_status, (void*)h->d_meas, (void*)h->d_mask,
+                  (void*)h->d_accepted, (void*)h->d_scratch})
+    if (p) (void)hipFree(p);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int64_t uwvk_pose_batch(const uwvk_pose* h) { return h ? h->batch : 0; }
+int uwvk_pose_dof(const uwvk_pose* h) { return h ? h->dof : 0; }
+void* uwvk_pose_stream(const uwvk_pose* h) { return h ? (void*)h->stream : nullptr; }
+uwvk_status uwvk_pose_synchronize(uwvk_pose* h) {
+  if (!h) return UWVK_EINVAL;
+  return hipStreamSynchronize(h->stream) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
+}
+
+static uwvk_status upload_state(uwvk_pose* h, const std::vector<double>& x, const std::vector<double>& P,
+                                const std::vector<double>& off, const std::vector<double>& model) {
+  HIPCHK(hipMemcpyAsync(h->d_mu, x.data(), x.size() * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d_sigma, P.data(), P.size() * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d_model, model.data(), model.size() * 8, hipMemcpyHostToDevice, h->stream));
+  double uw[108];
+  std::memcpy(uw, h->uwv.inertia_matrix, 36 * 8);
+  std::memcpy(uw + 36, h->uwv.damping_matrices[0], 36 * 8);
+  std::memcpy(uw + 72, h->uwv.damping_matrices[1], 36 * 8);
+  HIPCHK(hipMemcpyAsync(h->d_uwv, uw, sizeof(uw), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemsetAsync(h->d_status, 0, (size_t)h->batch * 4, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->has_state = true;
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_pose_init_from_config(uwvk_pose* h, const double* pos, const double* pos_cov, const double* rot,
+                                       const double* rot_cov, const uwvk_pose_config* cfg, const uwvk_uwv_params* uwv,
+                                       const double imu_in_body[7]) {
+  if (!h || !pos || !pos_cov || !rot || !rot_cov || !cfg || !uwv) return UWVK_EINVAL;
+  const int64_t B = h->batch;
+  const int n = h->dof, s = h->store;
+  std::vector<double> x(B * s), P(B * n * n), off(B * 28), model(B * 27);
+  uwvk_pose_parameter par{};
+  for (int64_t i = 0; i < B; i++) {
+    host::pose_initial_state(n, pos + 3 * i, pos_cov + 9 * i, rot + 4 * i, rot_cov + 9 * i, *cfg, *uwv, imu_in_body,
+                             &x[i * s], &P[i * n * n], &par);
+    host::pose_offsets(n, &x[i * s], &off[i * 28]);
+    host::model_blocks(*uwv, &model[i * 27]);
+  }
+  set_shared(h, par, cfg->location, *uwv);
+  return upload_state(h, x, P, off, model);
+}
+
+uwvk_status uwvk_pose_init_from_state(uwvk_pose* h, const double* x, const double* P, const uwvk_location* loc,
+                                      const uwvk_uwv_params* uwv, const uwvk_pose_parameter* param) {
+  if (!h || !x || !P || !loc || !uwv || !param) return UWVK_EINVAL;
+  const int64_t B = h->batch;
+  const int n = h->dof, s = h->store;
+  std::vector<double> xs(x, x + B * s), Ps(P, P + B * n * n), off(B * 28), model(B * 27);
+  for (int64_t i = 0; i < B; i++) {
+    host::pose_offsets(n, &xs[i * s], &off[i * 28]);
+    host::model_blocks(*uwv, &model[i * 27]);
+  }
+  set_shared(h, *param, *loc, *uwv);
+  return upload_state(h, xs, Ps, off, model);
+}
+
+uwvk_status uwvk_pose_set_process_noise_from_config(uwvk_pose* h, const uwvk_pose_config* cfg, double imu_delta_t,
+                                                    const double q_imu_in_body[4]) {
+  if (!h || !cfg || !(imu_delta_t > 0)) return UWVK_EINVAL;
+  std::vector<double> Q(h->dof * h->dof);
+  host::pose_process_noise(h->dof, *cfg, imu_delta_t, q_imu_in_body, Q.data());
+  return uwvk_pose_set_process_noise(h, Q.data());
+}
+
+uwvk_status uwvk_pose_set_process_noise(uwvk_pose* h, const double* Q) {
+  if (!h || !Q) return UWVK_EINVAL;
+  HIPCHK(hipMemcpyAsync(h->d_Q, Q, (size_t)h->dof * h->dof * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->has_Q = true;
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_pose_set_rotation_rate(uwvk_pose* h, const double* w, const double* cov) {
+  if (!h || !w) return UWVK_EINVAL;
+  if (!finite_all(w, (size_t)h->batch * 3) || (cov && !finite_all(cov, (size_t)h->batch * 9))) return UWVK_ENAN;
+  HIPCHK(hipMemcpyAsync(h->d_rot, w, (size_t)h->batch * 3 * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_pose_predict(uwvk_pose* h, double dt) {
+  if (!h) return UWVK_EINVAL;
+  if (!h->has_state) return UWVK_ENOTINIT;
+  PoseBufs b = bufs(h);
+  PoseShared sh = h->sh;
+  HIPCHK(launch_pose_predict(h->dof, h->stream, b, sh, dt));
+  return UWVK_OK;
+}
+
+}  // extern "C"
+
+template <int K>
+static uwvk_status launch_update(uwvk_pose* h, int m, const double* mu, const double* cov, const double* shared_cov,
+                                 const uint8_t* mask, uint8_t* accepted, const double* extra, int extra_w,
+                                 const double* v3, int only_vel) {
+  if (!h || !mu || (!cov && !shared_cov)) return UWVK_EINVAL;
+  if (!h->has_state) return UWVK_ENOTINIT;
+  const int64_t B = h->batch;
+  // checkMeasurment [EXT] (PoseUKF.cpp:478): NaN -> error, nothing applied
+  for (int64_t i = 0; i < B; i++) {
+    if (mask && !mask[i]) continue;
+    if (!finite_all(mu + i * m, m) || (cov && !finite_all(cov + i * m * m, (size_t)m * m))) return UWVK_ENAN;
+  }
+  if (!cov && !finite_all(shared_cov, (size_t)m * m)) return UWVK_ENAN;
+  MeasArgs ma{};
+  double* dmu = h->d_meas;
+  double* dcov = h->d_meas + B * 36;
+  double* dext = h->d_meas + B * 72;
+  HIPCHK(hipMemcpyAsync(dmu, mu, (size_t)B * m * 8, hipMemcpyHostToDevice, h->stream));
+  ma.mu = dmu;
+  if (cov) {
+    HIPCHK(hipMemcpyAsync(dcov, cov, (size_t)B * m * m * 8, hipMemcpyHostToDevice, h->stream));
+    ma.cov = dcov;
+  } else {
+    std::memcpy(ma.shared_cov, shared_cov, (size_t)m * m * 8);
+  }
+  if (mask) {
+    HIPCHK(hipMemcpyAsync(h->d_mask, mask, (size_t)B, hipMemcpyHostToDevice, h->stream));
+    ma.mask = h->d_mask;
+  }
+  if (extra) {
+    HIPCHK(hipMemcpyAsync(dext, extra, (size_t)B * extra_w * 8, hipMemcpyHostToDevice, h->stream));
+    ma.extra = dext;
+  }
+  if (v3)
+    for (int k = 0; k < 3; k++) ma.v3[k] = v3[k];
+  ma.only_vel = only_vel;
+  ma.accepted = h->d_accepted;
+  PoseBufs b = bufs(h);
+  PoseShared sh = h->sh;
+  HIPCHK(launch_pose_update(h->dof, K, h->stream, b, sh, ma, m));
+  if (accepted) HIPCHK(hipMemcpyAsync(accepted, h->d_accepted, (size_t)B, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+extern "C" {
+
+uwvk_status uwvk_pose_update_acceleration(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
+                                          const uint8_t* mask, uint8_t* acc) {
+  return launch_update<MK_ACC>(h, 3, mu, cov, sc, mask, acc, nullptr, 0, nullptr, 0);
+}
+uwvk_status uwvk_pose_update_velocity(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
+                                      const uint8_t* mask, uint8_t* acc) {
+  return launch_update<MK_VEL>(h, 3, mu, cov, sc, mask, acc, nullptr, 0, nullptr, 0);
+}
+uwvk_status uwvk_pose_update_pressure(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
+                                      const double sensor_in_imu[3], const uint8_t* mask, uint8_t* acc) {
+  const double zero[3] = {0, 0, 0};
+  return launch_update<MK_PRESSURE>(h, 1, mu, cov, sc, mask, acc, nullptr, 0, sensor_in_imu ? sensor_in_imu : zero, 0);
+}
+uwvk_status uwvk_pose_update_water_velocity(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
+                                            const double* cw, const uint8_t* mask, uint8_t* acc) {
+  if (!cw) return UWVK_EINVAL;
+  return launch_update<MK_WATER>(h, 2, mu, cov, sc, mask, acc, cw, 1, nullptr, 0);
+}
+uwvk_status uwvk_pose_update_efforts(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
+                                     int only_affect_velocity, const uint8_t* mask, uint8_t* acc) {
+  return launch_update<MK_EFFORTS>(h, 6, mu, cov, sc, mask, acc, nullptr, 0, nullptr, only_affect_velocity ? 1 : 0);
+}
+uwvk_status uwvk_pose_update_xy(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
+                                const uint8_t* mask, uint8_t* acc) {
+  return launch_update<MK_XY>(h, 2, mu, cov, sc, mask, acc, nullptr, 0, nullptr, 0);
+}
+uwvk_status uwvk_pose_update_z(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
+                               const uint8_t* mask, uint8_t* acc) {
+  return launch_update<MK_Z>(h, 1, mu, cov, sc, mask, acc, nullptr, 0, nullptr, 0);
+}
+uwvk_status uwvk_pose_update_geographic(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
+                                        const double gps_in_body[3], const uint8_t* mask, uint8_t* acc) {
+  const double zero[3] = {0, 0, 0};
+  return launch_update<MK_GEO>(h, 2, mu, cov, sc, mask, acc, nullptr, 0, gps_in_body ? gps_in_body : zero, 0);
+}
+uwvk_status uwvk_pose_update_delayed_xy(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
+                                        const double* delayed_xy, const uint8_t* mask, uint8_t* acc) {
+  if (!delayed_xy) return UWVK_EINVAL;
+  return launch_update<MK_DELAYED>(h, 2, mu, cov, sc, mask, acc, delayed_xy, 2, nullptr, 0);
+}
+
+uwvk_status uwvk_pose_reset_with_external_pose(uwvk_pose* h, const double* pose) {
+  if (!h || !pose) return UWVK_EINVAL;
+  if (!h->has_state) return UWVK_ENOTINIT;
+  const int64_t B = h->batch;
+  std::vector<double> x(B * h->store);
+  HIPCHK(hipMemcpyAsync(x.data(), h->d_mu, x.size() * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (int64_t i = 0; i < B; i++) std::memcpy(&x[i * h->store], pose + 7 * i, 7 * 8);  // PoseUKF.cpp:687-690
+  HIPCHK(hipMemcpyAsync(h->d_mu, x.data(), x.size() * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_pose_get_state(uwvk_pose* h, double* x, double* P) {
+  if (!h || !x) return UWVK_EINVAL;
+  HIPCHK(hipMemcpyAsync(x, h->d_mu, (size_t)h->batch * h->store * 8, hipMemcpyDeviceToHost, h->stream));
+  if (P)
+    HIPCHK(hipMemcpyAsync(P, h->d_sigma, (size_t)h->batch * h->dof * h->dof * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_pose_get_rotation_rate(uwvk_pose* h, double* out) {
+  if (!h || !out) return UWVK_EINVAL;
+  PoseBufs b = bufs(h);
+  PoseShared sh = h->sh;
+  double* d = h->d_scratch;
+  HIPCHK(launch_pose_rotation_rate(h->dof, h->stream, b, sh, d));
+  HIPCHK(hipMemcpyAsync(out, d, (size_t)h->batch * 3 * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_pose_get_status(uwvk_pose* h, uint32_t* status, int clear) {
+  if (!h || !status) return UWVK_EINVAL;
+  HIPCHK(hipMemcpyAsync(status, h->d_status, (size_t)h->batch * 4, hipMemcpyDeviceToHost, h->stream));
+  if (clear) HIPCHK(hipMemsetAsync(h->d_status, 0, (size_t)h->batch * 4, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t first, int64_t count,
+                              uint32_t* accept_counts) {
+  if (!h || !log || first < 0 || count < 0 || first + count > log->epochs || log->adcp_cells > 8) return UWVK_EINVAL;
+  if (!h->has_state) return UWVK_ENOTINIT;
+  EpochArgs ea{};
+  ea.flags = log->flags; ea.gyro = log->gyro; ea.acc = log->acc;
+  std::memcpy(ea.acc_cov, log->acc_cov, sizeof(ea.acc_cov));
+  ea.dvl_index = log->dvl_index; ea.dvl = log->dvl;
+  std::memcpy(ea.dvl_cov, log->dvl_cov, sizeof(ea.dvl_cov));
+  ea.p_index = log->pressure_index; ea.pressure = log->pressure; ea.p_cov = log->pressure_cov;
+  std::memcpy(ea.p_sens, log->pressure_sensor_in_imu, sizeof(ea.p_sens));
+  ea.a_index = log->adcp_index; ea.adcp = log->adcp; ea.cells = log->adcp_cells;
+  std::memcpy(ea.cw, log->adcp_cell_weighting, sizeof(ea.cw));
+  std::memcpy(ea.adcp_cov, log->adcp_cov, sizeof(ea.adcp_cov));
+  ea.e_index = log->efforts_index; ea.efforts = log->efforts;
+  std::memcpy(ea.e_cov, log->efforts_cov, sizeof(ea.e_cov));
+  ea.dt = log->dt;
+  ea.accept_counts = accept_counts;
+  PoseBufs b = bufs(h);
+  PoseShared sh = h->sh;
+  // one launch per epoch: the driver's "step" granularity
+  for (int64_t e = first; e < first + count; e++) {
+    ea.first = e;
+    ea.count = 1;
+    HIPCHK(launch_pose_epoch(h->dof, h->stream, b, sh, ea));
+  }
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* out) {
+  if (!h || !out) return UWVK_EINVAL;
+  const int s = h->store;
+  const int nout = 3 * s + 1;
+  double* d_out = h->d_scratch;
+  double* d_truth = h->d_scratch + 192;
+  std::vector<double> t(s, 0.0);
+  if (truth) std::memcpy(t.data(), truth, s * 8);
+  else t[3] = 1.0;
+  HIPCHK(hipMemsetAsync(d_out, 0, nout * 8, h->stream));
+  HIPCHK(hipMemcpyAsync(d_truth, t.data(), s * 8, hipMemcpyHostToDevice, h->stream));
+  PoseBufs b = bufs(h);
+  const unsigned nb = (unsigned)((h->batch + 63) / 64);
+  (void)nb;
+  HIPCHK(launch_pose_stats(h->dof, h->stream, b, d_truth, d_out));
+  HIPCHK(hipMemcpyAsync(out, d_out, nout * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_pose_timer_start(uwvk_pose* h) {
+  if (!h) return UWVK_EINVAL;
+  HIPCHK(hipEventRecord(h->ev0, h->stream));
+  return UWVK_OK;
+}
+uwvk_status uwvk_pose_timer_stop(uwvk_pose* h, float* ms) {
+  if (!h || !ms) return UWVK_EINVAL;
+  HIPCHK(hipEventRecord(h->ev1, h->stream));
+  HIPCHK(hipEventSynchronize(h->ev1));
+  HIPCHK(hipEventElapsedTime(ms, h->ev0, h->ev1));
+  return UWVK_OK;
+}
+
+}  // extern "C"

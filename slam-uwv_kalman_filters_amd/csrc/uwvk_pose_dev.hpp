@@ -1,0 +1,950 @@
+// uwvk_pose_dev.hpp — PoseUKF predict / update as workgroup-per-filter device
+// code for gfx950.
+//
+// Work split inside the workgroup of T = 64*NW threads (NW wavefronts, one
+// PoseUKF instance; NW = 2 for the 53-DOF state, 1 for the 26-DOF subset):
+//   * Sigma (n x n fp64) lives in LDS for the whole call.
+//   * Cholesky: wavefront 0, lane r owns row r in VGPRs, right-looking, column
+//     k broadcast through a 64-double LDS buffer.
+//   * Sigma points: thread p owns sigma point p (N = 2n+1 <= T); process and
+//     measurement models run per thread in VGPRs (one 54-double state each).
+//   * Means and small reductions: shuffle folds + LDS transpose sums.
+//   * Covariance reconstruction Sigma = 1/2 D D^T (+Q'): v_mfma_f64_16x16x4_f64
+//     over the n x N deviation matrix D, staged through LDS in 32-point chunks;
+//     the upper 16x16 tiles are dealt round-robin over the wavefronts and
+//     accumulate in registers.
+//
+// The arithmetic follows the reference and the frozen [EXT] spec exactly like
+// the CPU oracle (oracle/uwvk_oracle.c, citations there); only summation order
+// and FMA contraction differ (parity tolerance in tests/test_gpu_parity.py).
+#pragma once
+#include "uwvk_dev.hpp"
+#include "../../include/uwvk.h"
+
+namespace uwvk {
+
+// ---------------------------------------------------------------------------
+// per-handle (batch-shared) parameters, passed by value to every kernel
+// ---------------------------------------------------------------------------
+struct PoseShared {
+  uwvk_pose_parameter p;
+  double lat0, lon0, rm, rn_cos, inv_rm;  // GeographicProjection [EXT]: lat = lat0 + x/rm, lon = lon0 - y/rn_cos
+  double uwv_weight, uwv_buoyancy, cog[3], cob[3];
+};
+
+struct PoseBufs {
+  int64_t batch;
+  double* mu;         // [batch][store]
+  double* sigma;      // [batch][dof*dof]
+  const double* Q;    // [dof*dof] process_noise_cov (shared)
+  double* rot;        // [batch][3] stored RotationRate (PoseUKF.cpp:492-496)
+  double* off;        // [batch][28] inertia/lin/quad offsets (9 each, col-major) + density offset
+  double* model;      // [batch][27] the shared DynamicModel's (surge,sway,yaw) blocks (PoseUKF.cpp:173)
+  const double* uwv;  // [108] base M, D_l, D_q (row-major 6x6)
+  uint32_t* status;   // [batch]
+};
+
+template <int DOF>
+struct NWaves {
+  static constexpr int value = (2 * DOF + 1 + 63) / 64;
+};
+
+// geometry of the LDS staging for the MFMA covariance GEMM
+template <int DOF>
+struct Geo {
+  static constexpr int NW = NWaves<DOF>::value;
+  static constexpr int T = 64 * NW;                    // threads per filter
+  static constexpr int N = 2 * DOF + 1;                // sigma points (<= T)
+  static constexpr int NT = (DOF + 15) / 16;           // 16-row tiles per dimension
+  static constexpr int NTILE = NT * (NT + 1) / 2;      // upper tiles
+  static constexpr int TPW = (NTILE + NW - 1) / NW;    // tiles per wave
+  static constexpr int STR = 16 * NT + 1;              // staging row stride (odd: conflict-free writes)
+  static constexpr int NCHUNK = (N + 31) / 32;         // 32-point chunks
+  static constexpr int RS = DOF | 1;                   // transpose-sum row stride
+  static constexpr int RROWS = 16 * NW;                // rows after folding each wave 64 -> 16
+  static constexpr int A = DOF * DOF, B = 32 * STR, C = RROWS * RS;
+  static constexpr int SZ = (A > B ? (A > C ? A : C) : (B > C ? B : C));
+  static constexpr int LP = DOF * (DOF + 1) / 2, LC = 16 * (DOF | 1);
+  static constexpr int LPSZ = LP > LC ? LP : LC;       // packed L / update staging
+  static_assert(N <= T, "one sigma point per thread");
+};
+
+template <int NT>
+struct TileIJ {  // t -> (i, j) over the upper tiles, row-major
+  UWVK_DEV static constexpr int i(int t) {
+    int r = 0, k = t;
+    while (k >= NT - r) { k -= NT - r; r++; }
+    return r;
+  }
+  UWVK_DEV static constexpr int j(int t) {
+    int r = 0, k = t;
+    while (k >= NT - r) { k -= NT - r; r++; }
+    return r + k;
+  }
+};
+
+template <int DOF>
+struct alignas(16) Smem {
+  double S[Geo<DOF>::SZ];  // Sigma (row-major, stride DOF) / D staging / reduction scratch
+  double Lp[Geo<DOF>::LPSZ];  // Cholesky factor, packed lower triangle (row r at r(r+1)/2) / dx staging
+  double mu[56];           // current mean (store layout)
+  double ref[56];          // scratch state (X0 / mean under construction)
+  double col[2][64];       // Cholesky column broadcast (double-buffered)
+  double vec[64];          // broadcast vectors (sums, delta)
+  double red[4][32];       // cross-wave partial sums
+  double kb[DOF * 6];      // Kalman gain rows
+  double dz[32 * 8];       // staged measurement deviations
+  double qori[9];          // R Q_ori R^T for the predict
+};
+
+UWVK_DEV int tid() { return threadIdx.x; }
+UWVK_DEV int wid() { return threadIdx.x >> 6; }
+
+// intra-wavefront ordering point for LDS exchanges done by one wave
+UWVK_DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// sum of K values over all threads of the workgroup; result in every thread
+template <int DOF, int K>
+UWVK_DEV void block_sum(Smem<DOF>& sm, double (&v)[K]) {
+  constexpr int NW = Geo<DOF>::NW;
+#pragma unroll
+  for (int k = 0; k < K; k++) v[k] = wave_sum(v[k]);
+  if constexpr (NW > 1) {
+    static_assert(K <= 32, "block_sum width");
+    if (lane_id() == 0) {
+#pragma unroll
+      for (int k = 0; k < K; k++) sm.red[wid()][k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      double s = sm.red[0][k];
+#pragma unroll
+      for (int w = 1; w < NW; w++) s += sm.red[w][k];
+      v[k] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Cholesky of S into the packed factor sm.Lp by wavefront 0 (S is kept).  Returns false (uniform) if a
+// pivot is not > 0.
+// ---------------------------------------------------------------------------
+// one right-looking column step; template recursion keeps every register index
+// a compile-time constant (a runtime-indexed row would live in scratch)
+template <int DOF, int K>
+UWVK_DEV void chol_step(double (&a)[DOF], Smem<DOF>& sm, int r, bool& ok) {
+  if constexpr (K < DOF) {
+    const double akk = readlane_d(a[K], K);
+    ok = ok && (akk > 0.0);
+    const double d = sqrt(akk);
+    const double inv = 1.0 / d;
+    a[K] = (r == K) ? d : a[K] * inv;
+    sm.col[K & 1][r] = a[K];
+    wave_sync();
+#pragma unroll
+    for (int c = K + 1; c < DOF; c++) a[c] -= a[K] * sm.col[K & 1][c];
+    // keep the update eager: without this the compiler sinks every a[c]
+    // update to its first use and keeps O(n^2) column values live (spills)
+#pragma unroll
+    for (int c = K + 1; c < DOF; c++) asm volatile("" : "+v"(a[c]));
+    chol_step<DOF, K + 1>(a, sm, r, ok);
+  }
+}
+
+template <int DOF>
+UWVK_DEV bool chol_lds(Smem<DOF>& sm) {
+  if (wid() == 0) {
+    const int r = lane_id();
+    double a[DOF];
+#pragma unroll
+    for (int c = 0; c < DOF; c++) a[c] = (r < DOF) ? sm.S[r * DOF + c] : 0.0;
+    bool ok = true;
+    chol_step<DOF, 0>(a, sm, r, ok);
+    if (r < DOF) {
+      const int base = r * (r + 1) / 2;
+#pragma unroll
+      for (int c = 0; c < DOF; c++)
+        if (c <= r) sm.Lp[base + c] = a[c];
+    }
+    if (r == 0) sm.vec[63] = ok ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  const bool ok = sm.vec[63] != 0.0;
+  __syncthreads();
+  return ok;
+}
+
+// sigma point p (0..N-1) of (mu, L) into x (store layout):
+// X0 = mu, X_{2j+1} = mu [+] L_j, X_{2j+2} = mu [+] -L_j
+template <int DOF>
+UWVK_DEV void gen_point(const Smem<DOF>& sm, int p, double x[Lay<DOF>::store]) {
+  using L = Lay<DOF>;
+#pragma unroll
+  for (int s = 0; s < L::store; s++) x[s] = sm.mu[s];
+  if (p <= 0 || p >= Geo<DOF>::N) return;
+  const int j = (p - 1) >> 1;
+  const double sg = (p & 1) ? 1.0 : -1.0;
+#pragma unroll
+  for (int d = 0; d < DOF; d++) {
+    if (d >= 3 && d < 6) continue;
+    const double l = (d >= j) ? sm.Lp[d * (d + 1) / 2 + j] : 0.0;
+    x[d2s(d)] = sm.mu[d2s(d)] + sg * l;
+  }
+  if (j <= 5) {  // columns j > 5 of a lower-triangular L have no orientation entries
+    double v[3], e[4];
+#pragma unroll
+    for (int i = 0; i < 3; i++) v[i] = sg * ((3 + i >= j) ? sm.Lp[(3 + i) * (4 + i) / 2 + j] : 0.0);
+    so3_exp(v, e);
+    qmul(e, sm.mu + L::s_quat, x + L::s_quat);
+  }
+}
+
+// x [-] m (store -> tangent), m read from LDS
+template <int DOF>
+UWVK_DEV void boxminus_lds(const double x[Lay<DOF>::store], const double* m, double d[DOF]) {
+#pragma unroll
+  for (int k = 0; k < DOF; k++) {
+    if (k >= 3 && k < 6) continue;
+    d[k] = x[d2s(k)] - m[d2s(k)];
+  }
+  const double q[4] = {m[3], m[4], m[5], m[6]};
+  qboxminus(x + 3, q, d + 3);
+}
+
+// x [+] delta (delta uniform, from LDS)
+template <int DOF>
+UWVK_DEV void boxplus_vec(double x[Lay<DOF>::store], const double* delta) {
+#pragma unroll
+  for (int k = 0; k < DOF; k++) {
+    if (k >= 3 && k < 6) continue;
+    x[d2s(k)] = x[d2s(k)] + 1.0 * delta[k];
+  }
+  double e[4], q[4];
+  const double dv[3] = {delta[3], delta[4], delta[5]};
+  so3_exp(dv, e);
+  qmul(e, x + 3, q);
+#pragma unroll
+  for (int i = 0; i < 4; i++) x[3 + i] = q[i];
+}
+
+// ---------------------------------------------------------------------------
+// Sum over all threads of a per-thread vector v[DOF], result into sm.vec.
+// Fold each wave 64 -> 16 with two shuffles, LDS transpose, thread c sums
+// column c.  Uses sm.S as scratch (must be free).
+// ---------------------------------------------------------------------------
+template <int DOF>
+UWVK_DEV void lane_sum_vec(Smem<DOF>& sm, double (&v)[DOF]) {
+  using G = Geo<DOF>;
+  const int l = lane_id(), w = wid();
+#pragma unroll
+  for (int k = 0; k < DOF; k++) {
+    double a = v[k] + shfl_xor_d(v[k], 32);
+    a = a + shfl_xor_d(a, 16);
+    if (l < 16) sm.S[(16 * w + l) * G::RS + k] = a;
+  }
+  __syncthreads();
+  const int t = tid();
+  if (t < DOF) {
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int r = 0; r < G::RROWS; r += 4) {
+      s0 += sm.S[r * G::RS + t];
+      s1 += sm.S[(r + 1) * G::RS + t];
+      s2 += sm.S[(r + 2) * G::RS + t];
+      s3 += sm.S[(r + 3) * G::RS + t];
+    }
+    sm.vec[t] = (s0 + s1) + (s2 + s3);
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Sigma = 0.5 * D D^T over the per-thread deviations d (point = thread), via
+// v_mfma_f64_16x16x4_f64.  Upper tile t is owned by wave t % NW.
+// ---------------------------------------------------------------------------
+template <int DOF>
+UWVK_DEV void cov_gemm(Smem<DOF>& sm, const double (&d)[DOF], d4_t (&acc)[Geo<DOF>::TPW]) {
+  using G = Geo<DOF>;
+  const int l = lane_id(), w = wid(), t = tid();
+#pragma unroll
+  for (int u = 0; u < G::TPW; u++) acc[u] = d4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < G::NCHUNK; c++) {
+    if ((t >> 5) == c) {  // threads 32c .. 32c+31 stage their points
+      const int row = t & 31;
+      const bool valid = t < G::N;
+#pragma unroll
+      for (int k = 0; k < 16 * G::NT; k++) sm.S[row * G::STR + k] = (k < DOF && valid) ? d[k] : 0.0;
+    }
+    __syncthreads();
+    const int npts = (G::N - 32 * c) < 32 ? (G::N - 32 * c) : 32;
+    const int ks = (npts + 3) / 4;
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      if (s < ks) {
+        double f[G::NT];
+#pragma unroll
+        for (int i = 0; i < G::NT; i++) f[i] = sm.S[(4 * s + (l >> 4)) * G::STR + 16 * i + (l & 15)];
+#pragma unroll
+        for (int u = 0; u < G::TPW; u++) {
+#pragma unroll
+          for (int ww = 0; ww < G::NW; ww++) {
+            const int tt = ww + G::NW * u;
+            if (tt < G::NTILE && ww == w)
+              acc[u] = mfma_f64(f[TileIJ<G::NT>::i(tt)], f[TileIJ<G::NT>::j(tt)], acc[u]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// write 0.5*acc + qfun(r, c) into sm.S (full symmetric)
+template <int DOF, class QF>
+UWVK_DEV void store_cov(Smem<DOF>& sm, const d4_t (&acc)[Geo<DOF>::TPW], QF qfun) {
+  using G = Geo<DOF>;
+  const int l = lane_id(), w = wid();
+#pragma unroll
+  for (int u = 0; u < G::TPW; u++) {
+#pragma unroll
+    for (int ww = 0; ww < G::NW; ww++) {
+      const int tt = ww + G::NW * u;
+      if (tt < G::NTILE && ww == w) {
+        const int i = TileIJ<G::NT>::i(tt), j = TileIJ<G::NT>::j(tt);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int r = 16 * i + (l >> 4) + 4 * q, c = 16 * j + (l & 15);
+          if (r < DOF && c < DOF) {
+            const double v = 0.5 * acc[u][q] + qfun(r, c);
+            sm.S[r * DOF + c] = v;
+            if (i != j) sm.S[c * DOF + r] = v;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// process model, PoseUKF.cpp:12-84 (per sigma point, in registers)
+// ---------------------------------------------------------------------------
+struct ProcCtx {
+  double w[3];        // stored rotation rate
+  double dt;
+  const double* off;  // per-instance offsets (global, uniform address)
+};
+
+template <int DOF>
+UWVK_DEV void process_point(double x[Lay<DOF>::store], const PoseShared& sh, const ProcCtx& c) {
+  using L = Lay<DOF>;
+  const double dt = c.dt;
+  const uwvk_pose_parameter& P = sh.p;
+  // orientation first (reads pre-step position / bias / orientation)
+  const double lat = sh.lat0 + x[L::s_pos] * sh.inv_rm;  // navToWorld [EXT]
+  double sl, cl;
+  sincos(lat, &sl, &cl);
+  const double er[3] = {kEarthW * cl, 0.0, kEarthW * sl};
+  double wb[3], wn[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) wb[i] = c.w[i] - x[L::s_bg + i];
+  qrot(x + L::s_quat, wb, wn);
+#pragma unroll
+  for (int i = 0; i < 3; i++) wn[i] = (wn[i] - er[i]) * dt;
+  double e[4], q[4];
+  so3_exp(wn, e);
+  qmul(e, x + L::s_quat, q);
+#pragma unroll
+  for (int i = 0; i < 4; i++) x[L::s_quat + i] = q[i];
+  // vector parts: every update reads only pre-step values of other blocks
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    x[L::s_pos + i] = x[L::s_pos + i] + dt * x[L::s_vel + i];
+    x[L::s_vel + i] = x[L::s_vel + i] + dt * x[L::s_acc + i];
+    const double dg = (-1.0 / P.gyro_bias_tau) * (x[L::s_bg + i] - P.gyro_bias_offset[i]);
+    x[L::s_bg + i] = x[L::s_bg + i] + dt * dg;
+    const double da = (-1.0 / P.acc_bias_tau) * (x[L::s_ba + i] - P.acc_bias_offset[i]);
+    x[L::s_ba + i] = x[L::s_ba + i] + dt * da;
+  }
+  if constexpr (L::has_params) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const double di = (-1.0 / P.inertia_tau) * (x[L::s_inertia + k] - c.off[k]);
+      x[L::s_inertia + k] = x[L::s_inertia + k] + dt * di;
+      const double dl = (-1.0 / P.lin_damping_tau) * (x[L::s_lin + k] - c.off[9 + k]);
+      x[L::s_lin + k] = x[L::s_lin + k] + dt * dl;
+      const double dq = (-1.0 / P.quad_damping_tau) * (x[L::s_quad + k] - c.off[18 + k]);
+      x[L::s_quad + k] = x[L::s_quad + k] + dt * dq;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const double dw = (-1.0 / P.water_velocity_tau) * x[L::s_wv + k];
+    x[L::s_wv + k] = x[L::s_wv + k] + dt * dw;
+    const double db = (-1.0 / P.water_velocity_tau) * x[L::s_wvb + k];
+    x[L::s_wvb + k] = x[L::s_wvb + k] + dt * db;
+    const double dad = (-1.0 / P.adcp_bias_tau) * x[L::s_badcp + k];
+    x[L::s_badcp + k] = x[L::s_badcp + k] + dt * dad;
+  }
+  const double dr = (-1.0 / P.water_density_tau) * (x[L::s_rho] - c.off[27]);
+  x[L::s_rho] = x[L::s_rho] + dt * dr;
+}
+
+// ---------------------------------------------------------------------------
+// predictionStepImpl (PoseUKF.cpp:446-465) + ukf::predict [EXT]
+// ---------------------------------------------------------------------------
+template <int DOF>
+UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q) {
+  using L = Lay<DOF>;
+  using G = Geo<DOF>;
+  const int t = tid();
+  const double dt = pc.dt;
+  const bool mine = t < G::N;
+  // --- process noise shaping with the PRE-predict mean (PoseUKF.cpp:448-460)
+  if (t < 9) {
+    double R[9];
+    qmatrix(sm.mu + L::s_quat, R);
+    const int r = t / 3, c = t % 3, o = L::d_ori;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      double u = 0.0;
+#pragma unroll
+      for (int m = 0; m < 3; m++) u += R[r * 3 + m] * Q[(o + m) * DOF + o + k];
+      s += u * R[c * 3 + k];
+    }
+    sm.qori[t] = s;
+  }
+  const double vs0 = sm.mu[L::s_vel], vs1 = sm.mu[L::s_vel + 1], vs2 = 10 * sm.mu[L::s_vel + 2];
+  const double wv_add = sh.p.water_velocity_scale * (vs0 * vs0 + vs1 * vs1 + vs2 * vs2) * dt;
+  const double dt2 = dt * dt;
+  // --- sigma points through the process model
+  const bool ok = chol_lds<DOF>(sm);
+  double x[L::store];
+  gen_point<DOF>(sm, t, x);
+  process_point<DOF>(x, sh, pc);
+  // X0 (thread 0's point) as the first reference of the manifold mean
+  if (t == 0) {
+#pragma unroll
+    for (int s = 0; s < L::store; s++) sm.ref[s] = x[s];
+  }
+  __syncthreads();  // L dead from here on; ref visible
+  // --- manifold mean (Gauss-Newton, |delta| <= 1e-6, max 1e4 iterations)
+  double nrm2 = 0.0;
+  double dori[3];
+  {
+    double d[DOF];
+    boxminus_lds<DOF>(x, sm.ref, d);
+    if (!mine) {
+#pragma unroll
+      for (int k = 0; k < DOF; k++) d[k] = 0.0;
+    }
+    lane_sum_vec<DOF>(sm, d);
+  }
+  if (t < DOF) {
+    const double dd = sm.vec[t] / (double)G::N;
+    if (t < 3 || t >= 6) sm.ref[d2s(t)] = sm.ref[d2s(t)] + 1.0 * dd;
+  }
+#pragma unroll
+  for (int k = 0; k < DOF; k++) {
+    const double dd = sm.vec[k] / (double)G::N;
+    nrm2 += dd * dd;
+    if (k >= 3 && k < 6) dori[k - 3] = dd;
+  }
+  double mq[4];
+  {
+    double e[4];
+    const double q0[4] = {sm.ref[3], sm.ref[4], sm.ref[5], sm.ref[6]};
+    so3_exp(dori, e);
+    qmul(e, q0, mq);
+  }
+  int it = 0;
+  while (sqrt(nrm2) > 1e-6 && ++it < 10000) {
+    // orientation-only refinement: the vect parts are already the exact mean
+    double la[3];
+    qboxminus(x + L::s_quat, mq, la);
+    if (!mine) la[0] = la[1] = la[2] = 0.0;
+    block_sum<DOF, 3>(sm, la);
+    nrm2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      la[i] = la[i] / (double)G::N;
+      nrm2 += la[i] * la[i];
+    }
+    double e[4], q[4];
+    so3_exp(la, e);
+    qmul(e, mq, q);
+#pragma unroll
+    for (int i = 0; i < 4; i++) mq[i] = q[i];
+  }
+  __syncthreads();
+  if (t < 4) sm.ref[3 + t] = mq[t];
+  __syncthreads();
+  // --- deviations and covariance reconstruction
+  d4_t acc[G::TPW];
+  {
+    double d[DOF];
+    boxminus_lds<DOF>(x, sm.ref, d);
+    cov_gemm<DOF>(sm, d, acc);
+  }
+  auto qf = [&](int r, int c) -> double {
+    double q = Q[r * DOF + c];
+    if (r >= L::d_ori && r < L::d_ori + 3 && c >= L::d_ori && c < L::d_ori + 3)
+      q = sm.qori[(r - L::d_ori) * 3 + (c - L::d_ori)];
+    if (r == c && ((r >= L::d_wv && r < L::d_wv + 2) || (r >= L::d_wvb && r < L::d_wvb + 2))) q = q + wv_add;
+    return dt2 * q;
+  };
+  store_cov<DOF>(sm, acc, qf);
+  if (t < L::store) sm.mu[t] = sm.ref[t];
+  __syncthreads();
+  return ok;
+}
+
+// ---------------------------------------------------------------------------
+// small m x m inverse (m <= 6), identical formulas to the oracle
+// ---------------------------------------------------------------------------
+template <int M>
+UWVK_DEV void small_inv(const double* A, double* X) {
+  if constexpr (M == 1) {
+    X[0] = 1.0 / A[0];
+  } else if constexpr (M == 2) {
+    const double det = A[0] * A[3] - A[1] * A[2];
+    const double id = 1.0 / det;
+    X[0] = A[3] * id; X[1] = -A[1] * id; X[2] = -A[2] * id; X[3] = A[0] * id;
+  } else if constexpr (M == 3) {
+    const double c00 = A[4] * A[8] - A[5] * A[7];
+    const double c01 = A[5] * A[6] - A[3] * A[8];
+    const double c02 = A[3] * A[7] - A[4] * A[6];
+    const double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+    const double id = 1.0 / det;
+    X[0] = c00 * id;
+    X[1] = (A[2] * A[7] - A[1] * A[8]) * id;
+    X[2] = (A[1] * A[5] - A[2] * A[4]) * id;
+    X[3] = c01 * id;
+    X[4] = (A[0] * A[8] - A[2] * A[6]) * id;
+    X[5] = (A[2] * A[3] - A[0] * A[5]) * id;
+    X[6] = c02 * id;
+    X[7] = (A[1] * A[6] - A[0] * A[7]) * id;
+    X[8] = (A[0] * A[4] - A[1] * A[3]) * id;
+  } else {
+    double Mx[M][2 * M];
+#pragma unroll
+    for (int i = 0; i < M; i++)
+#pragma unroll
+      for (int j = 0; j < 2 * M; j++) Mx[i][j] = j < M ? A[i * M + j] : (j - M == i ? 1.0 : 0.0);
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+      int p = c;
+      double best = fabs(Mx[c][c]);
+#pragma unroll
+      for (int r = c + 1; r < M; r++) {
+        const double v = fabs(Mx[r][c]);
+        if (v > best) { best = v; p = r; }
+      }
+#pragma unroll
+      for (int r = c + 1; r < M; r++) {
+        if (r == p) {
+#pragma unroll
+          for (int j = 0; j < 2 * M; j++) { double tt = Mx[c][j]; Mx[c][j] = Mx[r][j]; Mx[r][j] = tt; }
+        }
+      }
+      const double ip = 1.0 / Mx[c][c];
+#pragma unroll
+      for (int j = 0; j < 2 * M; j++) Mx[c][j] *= ip;
+#pragma unroll
+      for (int r = 0; r < M; r++) {
+        if (r == c) continue;
+        const double f = Mx[r][c];
+        if (f == 0.0) continue;
+#pragma unroll
+        for (int j = 0; j < 2 * M; j++) Mx[r][j] -= f * Mx[c][j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < M; i++)
+#pragma unroll
+      for (int j = 0; j < M; j++) X[i * M + j] = Mx[i][M + j];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// apply_delta [EXT ukfom]: re-spread (mu, Sigma), shift every point and the
+// mean by delta, Sigma = 1/2 sum (X'_p [-] mu')(X'_p [-] mu')^T.
+// delta (tangent) is in sm.vec.
+// ---------------------------------------------------------------------------
+template <int DOF>
+UWVK_DEV bool apply_delta(Smem<DOF>& sm) {
+  using L = Lay<DOF>;
+  const int t = tid();
+  const bool ok = chol_lds<DOF>(sm);
+  double x[L::store];
+  gen_point<DOF>(sm, t, x);
+  boxplus_vec<DOF>(x, sm.vec);
+  if (t == 0) {
+    double m[L::store];
+#pragma unroll
+    for (int s = 0; s < L::store; s++) m[s] = sm.mu[s];
+    boxplus_vec<DOF>(m, sm.vec);
+#pragma unroll
+    for (int s = 0; s < L::store; s++) sm.ref[s] = m[s];
+  }
+  __syncthreads();
+  d4_t acc[Geo<DOF>::TPW];
+  {
+    double d[DOF];
+    boxminus_lds<DOF>(x, sm.ref, d);
+    cov_gemm<DOF>(sm, d, acc);
+  }
+  store_cov<DOF>(sm, acc, [](int, int) { return 0.0; });
+  if (t < L::store) sm.mu[t] = sm.ref[t];
+  __syncthreads();
+  return ok;
+}
+
+// ---------------------------------------------------------------------------
+// ukf::update [EXT] with measurement functor h (per sigma point, registers).
+//   zmode 0: Eigen-vector measurement (plain average)
+//   zmode 1: vect-manifold measurement (iterative mean, |d| <= 1e-6)
+//   gate 0: accept_any_mahalanobis_distance; 1: d2p95 (PoseUKF.cpp:275-286)
+// Returns the gate decision; *ok = false on a Cholesky failure.
+// ---------------------------------------------------------------------------
+template <int DOF, int M, class H>
+UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)[M * M], int zmode, int gate, H h,
+                          bool* ok) {
+  using L = Lay<DOF>;
+  using G = Geo<DOF>;
+  const int t = tid();
+  const bool mine = t < G::N;
+  const bool cok = chol_lds<DOF>(sm);
+  double x[L::store];
+  gen_point<DOF>(sm, t, x);
+  __syncthreads();  // L dead from here on
+  double zp[M], zm[M];
+  h(x, zp);
+  if (zmode == 0) {
+#pragma unroll
+    for (int a = 0; a < M; a++) zm[a] = mine ? zp[a] : 0.0;
+    block_sum<DOF, M>(sm, zm);
+#pragma unroll
+    for (int a = 0; a < M; a++) zm[a] = zm[a] / (double)G::N;
+  } else {
+    if (t == 0) {
+#pragma unroll
+      for (int a = 0; a < M; a++) sm.vec[a] = zp[a];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < M; a++) zm[a] = sm.vec[a];
+    __syncthreads();
+    int it = 0;
+    double nrm;
+    do {
+      double d[M];
+#pragma unroll
+      for (int a = 0; a < M; a++) d[a] = mine ? (zp[a] - zm[a]) : 0.0;
+      block_sum<DOF, M>(sm, d);
+      nrm = 0.0;
+#pragma unroll
+      for (int a = 0; a < M; a++) {
+        d[a] = d[a] / (double)G::N;
+        nrm += d[a] * d[a];
+      }
+#pragma unroll
+      for (int a = 0; a < M; a++) zm[a] = zm[a] + d[a];
+      nrm = sqrt(nrm);
+    } while (nrm > 1e-6 && ++it < 10000);
+  }
+  double dz[M];
+#pragma unroll
+  for (int a = 0; a < M; a++) dz[a] = mine ? (zp[a] - zm[a]) : 0.0;
+  double S[M * M], Si[M * M];
+  {
+    constexpr int NS = M * (M + 1) / 2;
+    double sp[NS];
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < M; a++)
+#pragma unroll
+      for (int b = a; b < M; b++) sp[k++] = dz[a] * dz[b];
+    block_sum<DOF, NS>(sm, sp);
+    k = 0;
+#pragma unroll
+    for (int a = 0; a < M; a++)
+#pragma unroll
+      for (int b = a; b < M; b++) {
+        const double s = 0.5 * sp[k++];
+        S[a * M + b] = s + R[a * M + b];
+        S[b * M + a] = s + R[b * M + a];
+      }
+  }
+  // cross covariance C = 1/2 sum dx dz^T; thread r (< DOF) accumulates row r.
+  // dx is staged through the (dead) Cholesky-factor region in 16-point chunks;
+  // Sigma in sm.S stays intact for the covariance update below.
+  double C[M];
+#pragma unroll
+  for (int a = 0; a < M; a++) C[a] = 0.0;
+  {
+    constexpr int CS = DOF | 1;
+    double dx[DOF];
+    boxminus_lds<DOF>(x, sm.mu, dx);
+#pragma unroll
+    for (int c = 0; c < (G::N + 15) / 16; c++) {
+      if ((t >> 4) == c) {
+        const int row = t & 15;
+#pragma unroll
+        for (int k = 0; k < DOF; k++) sm.Lp[row * CS + k] = mine ? dx[k] : 0.0;
+#pragma unroll
+        for (int a = 0; a < M; a++) sm.dz[row * 8 + a] = dz[a];
+      }
+      __syncthreads();
+      const int npts = (G::N - 16 * c) < 16 ? (G::N - 16 * c) : 16;
+      if (t < DOF) {
+        for (int q = 0; q < npts; q++) {
+          const double v = sm.Lp[q * CS + t];
+#pragma unroll
+          for (int a = 0; a < M; a++) C[a] += v * sm.dz[q * 8 + a];
+        }
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < M; a++) C[a] = 0.5 * C[a];
+  small_inv<M>(S, Si);
+  double K[M];
+#pragma unroll
+  for (int a = 0; a < M; a++) {
+    double s = 0.0;
+#pragma unroll
+    for (int b = 0; b < M; b++) s += C[b] * Si[b * M + a];
+    K[a] = s;
+  }
+  double nu[M];
+#pragma unroll
+  for (int a = 0; a < M; a++) nu[a] = z[a] - zm[a];
+  double d2 = 0.0;
+#pragma unroll
+  for (int b = 0; b < M; b++) {
+    double u = 0.0;
+#pragma unroll
+    for (int a = 0; a < M; a++) u += nu[a] * Si[a * M + b];
+    d2 += u * nu[b];
+  }
+  const bool accept = gate == 0 ? true : !(d2 > kD2P95);
+  if (!accept) {
+    *ok = cok;
+    return false;
+  }
+  // Sigma -= C K^T ; delta = K nu
+  if (t < DOF) {
+#pragma unroll
+    for (int a = 0; a < M; a++) sm.kb[t * M + a] = K[a];
+  }
+  __syncthreads();
+  if (t < DOF) {
+    for (int c = 0; c < DOF; c++) {
+      double s = 0.0;
+#pragma unroll
+      for (int a = 0; a < M; a++) s += C[a] * sm.kb[c * M + a];
+      sm.S[t * DOF + c] -= s;
+    }
+    double dl = 0.0;
+#pragma unroll
+    for (int a = 0; a < M; a++) dl += K[a] * nu[a];
+    sm.vec[t] = dl;
+  }
+  __syncthreads();
+  const bool aok = apply_delta<DOF>(sm);
+  *ok = cok && aok;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// measurement models (PoseUKF.cpp:87-219)
+// ---------------------------------------------------------------------------
+template <int DOF>
+struct HAcc {  // measurementAcceleration, PoseUKF.cpp:125-131
+  UWVK_DEV void operator()(const double* x, double (&z)[3]) const {
+    using L = Lay<DOF>;
+    const double a[3] = {x[L::s_acc], x[L::s_acc + 1], x[L::s_acc + 2] + x[L::s_grav]};
+    double r[3];
+    qrot_inv(x + L::s_quat, a, r);
+#pragma unroll
+    for (int i = 0; i < 3; i++) z[i] = r[i] + x[L::s_ba + i];
+  }
+};
+template <int DOF>
+struct HVel {  // measurementVelocity, PoseUKF.cpp:117-123
+  UWVK_DEV void operator()(const double* x, double (&z)[3]) const {
+    using L = Lay<DOF>;
+    qrot_inv(x + L::s_quat, x + L::s_vel, z);
+  }
+};
+template <int DOF>
+struct HPressure {  // measurementPressureSensor, PoseUKF.cpp:107-115
+  double s[3], patm;
+  UWVK_DEV void operator()(const double* x, double (&z)[1]) const {
+    using L = Lay<DOF>;
+    double r[3];
+    qrot(x + L::s_quat, s, r);
+    const double pz = x[L::s_pos + 2] + r[2];
+    z[0] = patm - pz * x[L::s_grav] * x[L::s_rho];
+  }
+};
+template <int DOF>
+struct HWater {  // measurementWaterCurrents, PoseUKF.cpp:133-151
+  double cw;
+  UWVK_DEV void operator()(const double* x, double (&z)[2]) const {
+    using L = Lay<DOF>;
+    const double vb[3] = {x[L::s_vel] - x[L::s_wvb], x[L::s_vel + 1] - x[L::s_wvb + 1], x[L::s_vel + 2] - 0.0};
+    const double vw[3] = {x[L::s_vel] - x[L::s_wv], x[L::s_vel + 1] - x[L::s_wv + 1], x[L::s_vel + 2] - 0.0};
+    double rb[3], rw[3];
+    qrot_inv(x + L::s_quat, vb, rb);
+    qrot_inv(x + L::s_quat, vw, rw);
+#pragma unroll
+    for (int i = 0; i < 2; i++) z[i] = cw * rb[i] + (1 - cw) * rw[i] + x[L::s_badcp + i];
+  }
+};
+template <int DOF>
+struct HXY {  // measurementXYPosition, PoseUKF.cpp:87-92
+  UWVK_DEV void operator()(const double* x, double (&z)[2]) const { z[0] = x[0]; z[1] = x[1]; }
+};
+template <int DOF>
+struct HZ {  // measurementZPosition, PoseUKF.cpp:100-105
+  UWVK_DEV void operator()(const double* x, double (&z)[1]) const { z[0] = x[2]; }
+};
+
+// [EXT] DynamicModel::calcEfforts: tau = M a + C(nu) nu + D_l nu + D_q |nu| nu + g(q)
+// M/Dl/Dq: base 6x6 (row-major, global) with the (0,1,5) blocks overridden by blk
+struct Efforts6 {
+  const double* base;  // M[36], Dl[36], Dq[36]
+  double weight, buoyancy, cog[3], cob[3];
+  UWVK_DEV static constexpr int blk_index(int r, int c) {  // -> a + 3b of the 3x3 block or -1
+    const int a = r == 0 ? 0 : r == 1 ? 1 : r == 5 ? 2 : -1;
+    const int b = c == 0 ? 0 : c == 1 ? 1 : c == 5 ? 2 : -1;
+    return (a < 0 || b < 0) ? -1 : a + 3 * b;
+  }
+  template <class BLK>
+  UWVK_DEV double m(int which, int r, int c, const BLK& blk) const {
+    const int k = blk_index(r, c);
+    if (k >= 0 && blk.has) return blk.v[which * 9 + k];
+    return base[which * 36 + r * 6 + c];
+  }
+  template <class BLK>
+  UWVK_DEV void eval(const double acc6[6], const double nu[6], const double q[4], const BLK& blk, double tau[6]) const {
+    double a[3], b[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      double sa = 0, sb = 0;
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        sa += m(0, i, j, blk) * nu[j];
+        sb += m(0, 3 + i, j, blk) * nu[j];
+      }
+      a[i] = sa; b[i] = sb;
+    }
+    double t0[3], t1[3], t2[3], cor[6];
+    cross3(nu + 3, a, t0);
+    cross3(nu, a, t1);
+    cross3(nu + 3, b, t2);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { cor[i] = t0[i]; cor[3 + i] = t1[i] + t2[i]; }
+    const double fw[3] = {0, 0, -weight}, fb[3] = {0, 0, buoyancy};
+    double fg[3], fbb[3], mg[3], mb[3], g[6];
+    qrot_inv(q, fw, fg);
+    qrot_inv(q, fb, fbb);
+    cross3(cog, fg, mg);
+    cross3(cob, fbb, mb);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { g[i] = -(fg[i] + fbb[i]); g[3 + i] = -(mg[i] + mb[i]); }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      double sl = 0, sq = 0, mm = 0;
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        sl += m(1, i, j, blk) * nu[j];
+        sq += m(2, i, j, blk) * (fabs(nu[j]) * nu[j]);
+        mm += m(0, i, j, blk) * acc6[j];
+      }
+      tau[i] = mm + cor[i] + (sl + sq) + g[i];
+    }
+  }
+};
+
+struct BlkPtr { bool has; const double* v; };
+
+template <int DOF>
+struct HEfforts {  // measurementEfforts, PoseUKF.cpp:153-196
+  Efforts6 ef;
+  double wb[3], imu[3];
+  UWVK_DEV void operator()(const double* x, double (&z)[6]) const {
+    using L = Lay<DOF>;
+    struct BlkState { bool has; double v[27]; } blk;
+    blk.has = L::has_params != 0;
+    if constexpr (L::has_params) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        blk.v[k] = x[L::s_inertia + k];
+        blk.v[9 + k] = x[L::s_lin + k];
+        blk.v[18 + k] = x[L::s_quad + k];
+      }
+    }
+    const double wv[3] = {x[L::s_wv], x[L::s_wv + 1], 0.0};
+    double vb[3], cr[3], rw[3], vel6[6], acc6[6], ab[3], cc[3];
+    qrot_inv(x + L::s_quat, x + L::s_vel, vb);
+    cross3(wb, imu, cr);
+#pragma unroll
+    for (int i = 0; i < 3; i++) vb[i] = vb[i] - cr[i];
+    qrot_inv(x + L::s_quat, wv, rw);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { vel6[i] = vb[i] - rw[i]; vel6[3 + i] = wb[i]; }
+    qrot_inv(x + L::s_quat, x + L::s_acc, ab);
+    cross3(wb, cr, cc);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { acc6[i] = ab[i] - cc[i]; acc6[3 + i] = 0.0; }
+    ef.eval(acc6, vel6, x + L::s_quat, blk, z);
+  }
+};
+
+template <int DOF>
+struct HConstrain {  // constrainVelocity, PoseUKF.cpp:199-219
+  Efforts6 ef;
+  BlkPtr blk;  // the shared model's current (surge,sway,yaw) blocks
+  double wb[3], imu[3], w3[3], q[4], ab[3];
+  UWVK_DEV void operator()(const double* x, double (&z)[6]) const {
+    using L = Lay<DOF>;
+    double vb[3], cr[3], rw[3], vel6[6], acc6[6];
+    qrot_inv(q, x + L::s_vel, vb);
+    cross3(wb, imu, cr);
+#pragma unroll
+    for (int i = 0; i < 3; i++) vb[i] = vb[i] - cr[i];
+    qrot_inv(q, w3, rw);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { vel6[i] = vb[i] - rw[i]; vel6[3 + i] = wb[i]; acc6[i] = ab[i]; acc6[3 + i] = 0.0; }
+    ef.eval(acc6, vel6, q, blk, z);
+  }
+};
+
+// getRotationRate (PoseUKF.cpp:693-699) at the current mean
+template <int DOF>
+UWVK_DEV void rotation_rate_body(const Smem<DOF>& sm, const PoseShared& sh, const double w[3], double out[3]) {
+  using L = Lay<DOF>;
+  const double lat = sh.lat0 + sm.mu[L::s_pos] * sh.inv_rm;
+  double sl, cl;
+  sincos(lat, &sl, &cl);
+  const double er[3] = {kEarthW * cl, 0.0, kEarthW * sl};
+  const double q[4] = {sm.mu[L::s_quat], sm.mu[L::s_quat + 1], sm.mu[L::s_quat + 2], sm.mu[L::s_quat + 3]};
+  double r[3];
+  qrot_inv(q, er, r);
+#pragma unroll
+  for (int i = 0; i < 3; i++) out[i] = (w[i] - sm.mu[L::s_bg + i]) - r[i];
+}
+
+}  // namespace uwvk

@@ -1,0 +1,15 @@
+// PoseUKF fused epoch kernel (predict + flagged updates, Sigma LDS-resident).
+#define UWVK_POSE_KERNEL_BODIES
+#include "uwvk_pose_kernels.hpp"
+
+namespace uwvk {
+
+hipError_t launch_pose_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea) {
+  if (dof == 53)
+    hipLaunchKernelGGL(k_pose_epoch<53>, dim3((unsigned)b.batch), dim3(Geo<53>::T), 0, st, b, sh, ea);
+  else
+    hipLaunchKernelGGL(k_pose_epoch<26>, dim3((unsigned)b.batch), dim3(Geo<26>::T), 0, st, b, sh, ea);
+  return hipGetLastError();
+}
+
+}  // namespace uwvk

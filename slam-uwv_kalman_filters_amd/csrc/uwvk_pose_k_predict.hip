@@ -1,0 +1,32 @@
+// PoseUKF predict / rotation-rate / ensemble-statistics kernels (gfx950).
+#define UWVK_POSE_KERNEL_BODIES
+#include "uwvk_pose_kernels.hpp"
+
+namespace uwvk {
+
+hipError_t launch_pose_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt) {
+  if (dof == 53)
+    hipLaunchKernelGGL(k_pose_predict<53>, dim3((unsigned)b.batch), dim3(Geo<53>::T), 0, st, b, sh, dt);
+  else
+    hipLaunchKernelGGL(k_pose_predict<26>, dim3((unsigned)b.batch), dim3(Geo<26>::T), 0, st, b, sh, dt);
+  return hipGetLastError();
+}
+
+hipError_t launch_pose_rotation_rate(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double* out) {
+  if (dof == 53)
+    hipLaunchKernelGGL(k_pose_rotation_rate<53>, dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, out);
+  else
+    hipLaunchKernelGGL(k_pose_rotation_rate<26>, dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const double* truth, double* out) {
+  const unsigned nb = (unsigned)((b.batch + 63) / 64);
+  if (dof == 53)
+    hipLaunchKernelGGL(k_pose_stats<53>, dim3(nb), dim3(64), 0, st, b, truth, out);
+  else
+    hipLaunchKernelGGL(k_pose_stats<26>, dim3(nb), dim3(64), 0, st, b, truth, out);
+  return hipGetLastError();
+}
+
+}  // namespace uwvk

@@ -1,0 +1,23 @@
+// PoseUKF single-measurement update kernels, group b (MK_WATER MK_EFFORTS).
+#define UWVK_POSE_KERNEL_BODIES
+#include "uwvk_pose_kernels.hpp"
+
+namespace uwvk {
+
+hipError_t launch_pose_update_b(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                                 const MeasArgs& ma, int m) {
+  const dim3 g((unsigned)b.batch);
+  switch (kind) {
+    case MK_WATER:
+      if (dof == 53) hipLaunchKernelGGL((k_pose_update<53, MK_WATER>), g, dim3(Geo<53>::T), 0, st, b, sh, ma, m);
+      else hipLaunchKernelGGL((k_pose_update<26, MK_WATER>), g, dim3(Geo<26>::T), 0, st, b, sh, ma, m);
+      return hipGetLastError();
+    case MK_EFFORTS:
+      if (dof == 53) hipLaunchKernelGGL((k_pose_update<53, MK_EFFORTS>), g, dim3(Geo<53>::T), 0, st, b, sh, ma, m);
+      else hipLaunchKernelGGL((k_pose_update<26, MK_EFFORTS>), g, dim3(Geo<26>::T), 0, st, b, sh, ma, m);
+      return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace uwvk

@@ -1,0 +1,361 @@
+// uwvk_pose_kernels.hpp — PoseUKF kernel templates (one workgroup of
+// Geo<DOF>::T threads per filter instance) and their launch declarations.
+// Explicit instantiations live in the uwvk_pose_k_*.hip translation units so
+// the build parallelises; the C ABI (uwvk_pose.hip) only sees the launchers.
+#pragma once
+#include "uwvk_pose_dev.hpp"
+
+namespace uwvk {
+
+enum MeasKind { MK_ACC = 0, MK_VEL, MK_PRESSURE, MK_WATER, MK_EFFORTS, MK_XY, MK_Z, MK_GEO, MK_DELAYED };
+
+struct MeasArgs {
+  const double* mu;    // [batch][m]
+  const double* cov;   // [batch][m*m] or null -> shared_cov
+  double shared_cov[36];
+  const uint8_t* mask; // nullable
+  uint8_t* accepted;   // nullable
+  const double* extra; // cell_weighting [batch] / delayed_xy [batch][2]
+  double v3[3];        // sensor_in_imu / gps_in_body
+  int only_vel;
+};
+
+struct EpochArgs {
+  const uint32_t* flags;
+  const double* gyro;
+  const double* acc;
+  double acc_cov[9];
+  const int32_t* dvl_index;
+  const double* dvl;
+  double dvl_cov[9];
+  const int32_t* p_index;
+  const double* pressure;
+  double p_cov;
+  double p_sens[3];
+  const int32_t* a_index;
+  const double* adcp;
+  int cells;
+  double cw[8];
+  double adcp_cov[4];
+  const int32_t* e_index;
+  const double* efforts;
+  double e_cov[36];
+  double dt;
+  int64_t first, count;
+  uint32_t* accept_counts;  // [batch][4] nullable
+};
+
+// host-callable launchers (grid = one workgroup per instance)
+hipError_t launch_pose_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt);
+hipError_t launch_pose_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                              const MeasArgs& ma, int m);
+hipError_t launch_pose_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea);
+hipError_t launch_pose_rotation_rate(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double* out);
+hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const double* truth, double* out);
+
+#ifdef UWVK_POSE_KERNEL_BODIES
+
+
+
+
+
+template <int DOF>
+UWVK_DEV void load_instance(Smem<DOF>& sm, const PoseBufs& b, int64_t i) {
+  const int l = tid();
+  const double* gs = b.sigma + i * (int64_t)(DOF * DOF);
+  for (int k = l; k < DOF * DOF; k += Geo<DOF>::T) sm.S[k] = gs[k];
+  if (l < Lay<DOF>::store) sm.mu[l] = b.mu[i * Lay<DOF>::store + l];
+  __syncthreads();
+}
+
+template <int DOF>
+UWVK_DEV void store_instance(const Smem<DOF>& sm, const PoseBufs& b, int64_t i) {
+  const int l = tid();
+  double* gs = b.sigma + i * (int64_t)(DOF * DOF);
+  for (int k = l; k < DOF * DOF; k += Geo<DOF>::T) gs[k] = sm.S[k];
+  if (l < Lay<DOF>::store) b.mu[i * Lay<DOF>::store + l] = sm.mu[l];
+}
+
+UWVK_DEV bool all_finite(const double* a, int n) {
+  bool f = true;
+  for (int k = 0; k < n; k++) f = f && isfinite(a[k]);
+  return f;
+}
+
+// one measurement update of kind K on instance i (Sigma in LDS)
+template <int DOF, int K>
+UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, int64_t i, const double* zin,
+                        const double* Rin, const MeasArgs& ma, double wrot[3], bool* ok) {
+  using L = Lay<DOF>;
+  if constexpr (K == MK_ACC) {
+    double z[3], R[9];
+    for (int k = 0; k < 3; k++) z[k] = zin[k];
+    for (int k = 0; k < 9; k++) R[k] = Rin[k];
+    return pose_update<DOF, 3>(sm, z, R, 1, 0, HAcc<DOF>{}, ok);
+  } else if constexpr (K == MK_VEL) {
+    double z[3], R[9];
+    for (int k = 0; k < 3; k++) z[k] = zin[k];
+    for (int k = 0; k < 9; k++) R[k] = Rin[k];
+    return pose_update<DOF, 3>(sm, z, R, 1, 0, HVel<DOF>{}, ok);
+  } else if constexpr (K == MK_PRESSURE) {
+    double z[1] = {zin[0]}, R[1] = {Rin[0]};
+    HPressure<DOF> h;
+    h.s[0] = ma.v3[0]; h.s[1] = ma.v3[1]; h.s[2] = ma.v3[2];
+    h.patm = sh.p.atmospheric_pressure;
+    return pose_update<DOF, 1>(sm, z, R, 0, 0, h, ok);
+  } else if constexpr (K == MK_WATER) {
+    double z[2] = {zin[0], zin[1]}, R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
+    HWater<DOF> h;
+    h.cw = ma.extra ? ma.extra[i] : 0.0;
+    return pose_update<DOF, 2>(sm, z, R, 1, 1, h, ok);
+  } else if constexpr (K == MK_XY || K == MK_GEO || K == MK_DELAYED) {
+    double z[2] = {zin[0], zin[1]}, R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
+    int gate = 0;
+    if constexpr (K == MK_GEO) {  // PoseUKF.cpp:571-578
+      double r[3];
+      const double x = (zin[0] - sh.lat0) * sh.rm;
+      const double y = -(zin[1] - sh.lon0) * sh.rn_cos;
+      qrot(sm.mu + L::s_quat, ma.v3, r);
+      z[0] = x - r[0];
+      z[1] = y - r[1];
+      gate = 1;
+    }
+    if constexpr (K == MK_DELAYED) {  // PoseUKF.cpp:516-521
+      z[0] = zin[0] + (sm.mu[L::s_pos] - ma.extra[2 * i]);
+      z[1] = zin[1] + (sm.mu[L::s_pos + 1] - ma.extra[2 * i + 1]);
+    }
+    return pose_update<DOF, 2>(sm, z, R, 0, gate, HXY<DOF>{}, ok);
+  } else if constexpr (K == MK_Z) {
+    double z[1] = {zin[0]}, R[1] = {Rin[0]};
+    return pose_update<DOF, 1>(sm, z, R, 0, 0, HZ<DOF>{}, ok);
+  } else {  // MK_EFFORTS, PoseUKF.cpp:581-602
+    double z[6], R[36];
+    for (int k = 0; k < 6; k++) z[k] = zin[k];
+    for (int k = 0; k < 36; k++) R[k] = Rin[k];
+    Efforts6 ef;
+    ef.base = b.uwv;
+    ef.weight = sh.uwv_weight;
+    ef.buoyancy = sh.uwv_buoyancy;
+    for (int k = 0; k < 3; k++) { ef.cog[k] = sh.cog[k]; ef.cob[k] = sh.cob[k]; }
+    double wb[3];
+    rotation_rate_body<DOF>(sm, sh, wrot, wb);
+    double* model = b.model + i * 27;
+    if (ma.only_vel) {
+      HConstrain<DOF> h;
+      h.ef = ef;
+      h.blk.has = true;
+      h.blk.v = model;
+      for (int k = 0; k < 3; k++) { h.wb[k] = wb[k]; h.imu[k] = sh.p.imu_in_body[k]; }
+      h.w3[0] = sm.mu[L::s_wv]; h.w3[1] = sm.mu[L::s_wv + 1]; h.w3[2] = 0.0;
+      for (int k = 0; k < 4; k++) h.q[k] = sm.mu[L::s_quat + k];
+      double ra[3], cr[3], cc[3];
+      qrot_inv(h.q, sm.mu + L::s_acc, ra);
+      cross3(wb, h.imu, cr);
+      cross3(wb, cr, cc);
+      for (int k = 0; k < 3; k++) h.ab[k] = ra[k] - cc[k];
+      return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok);
+    }
+    HEfforts<DOF> h;
+    h.ef = ef;
+    for (int k = 0; k < 3; k++) { h.wb[k] = wb[k]; h.imu[k] = sh.p.imu_in_body[k]; }
+    // side effect of PoseUKF.cpp:173: the shared model ends with the last sigma
+    // point's blocks, X_2n = mu [+] -L_{:,n-1}, i.e. the pre-update mean's.
+    if constexpr (L::has_params) {
+      const int l = tid();
+      if (l < 9) {
+        model[l] = sm.mu[L::s_inertia + l];
+        model[9 + l] = sm.mu[L::s_lin + l];
+        model[18 + l] = sm.mu[L::s_quad + l];
+      }
+    }
+    return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok);
+  }
+}
+
+template <int DOF>
+__global__ __launch_bounds__(Geo<DOF>::T) void k_pose_predict(PoseBufs b, PoseShared sh, double dt) {
+  __shared__ Smem<DOF> sm;
+  const int64_t i = blockIdx.x;
+  load_instance<DOF>(sm, b, i);
+  ProcCtx pc;
+  for (int k = 0; k < 3; k++) pc.w[k] = b.rot[i * 3 + k];
+  pc.dt = dt;
+  pc.off = b.off + i * 28;
+  const bool ok = pose_predict<DOF>(sm, sh, pc, b.Q);
+  if (!ok && tid() == 0) b.status[i] |= UWVK_ST_NOTPD;
+  store_instance<DOF>(sm, b, i);
+}
+
+template <int DOF, int K>
+__global__ __launch_bounds__(Geo<DOF>::T) void k_pose_update(PoseBufs b, PoseShared sh, MeasArgs ma, int m) {
+  __shared__ Smem<DOF> sm;
+  const int64_t i = blockIdx.x;
+  if (ma.mask && !ma.mask[i]) {
+    if (ma.accepted && tid() == 0) ma.accepted[i] = 0;
+    return;
+  }
+  const double* z = ma.mu + i * m;
+  const double* R = ma.cov ? ma.cov + i * m * m : ma.shared_cov;
+  if (!all_finite(z, m) || !all_finite(R, m * m)) {  // checkMeasurment [EXT]
+    if (tid() == 0) {
+      b.status[i] |= UWVK_ST_NAN;
+      if (ma.accepted) ma.accepted[i] = 0;
+    }
+    return;
+  }
+  load_instance<DOF>(sm, b, i);
+  double w[3] = {b.rot[i * 3], b.rot[i * 3 + 1], b.rot[i * 3 + 2]};
+  bool ok = true;
+  const bool acc = do_update<DOF, K>(sm, sh, b, i, z, R, ma, w, &ok);
+  if (tid() == 0) {
+    if (!ok) b.status[i] |= UWVK_ST_NOTPD;
+    if (ma.accepted) ma.accepted[i] = acc ? 1 : 0;
+  }
+  store_instance<DOF>(sm, b, i);
+}
+
+template <int DOF>
+__global__ __launch_bounds__(Geo<DOF>::T) void k_pose_epoch(PoseBufs b, PoseShared sh, EpochArgs ea) {
+  __shared__ Smem<DOF> sm;
+  const int64_t i = blockIdx.x, B = b.batch;
+  load_instance<DOF>(sm, b, i);
+  bool ok = true, nan = false;
+  uint32_t cnt[4] = {0, 0, 0, 0};
+  MeasArgs ma;
+  ma.mask = nullptr; ma.accepted = nullptr; ma.cov = nullptr; ma.only_vel = 0;
+  ma.v3[0] = ea.p_sens[0]; ma.v3[1] = ea.p_sens[1]; ma.v3[2] = ea.p_sens[2];
+  double w[3] = {b.rot[i * 3], b.rot[i * 3 + 1], b.rot[i * 3 + 2]};
+  ProcCtx pc;
+  for (int k = 0; k < 3; k++) pc.w[k] = w[k];
+  pc.dt = ea.dt;
+  pc.off = b.off + i * 28;
+  for (int64_t e = ea.first; e < ea.first + ea.count; e++) {
+    const uint32_t fl = ea.flags[e];
+    const double* g = ea.gyro + (e * B + i) * 3;
+    if (all_finite(g, 3)) {  // integrateMeasurement(RotationRate): checkMeasurment, then store
+      for (int k = 0; k < 3; k++) { w[k] = g[k]; pc.w[k] = g[k]; }
+    } else {
+      nan = true;
+    }
+    bool sok = pose_predict<DOF>(sm, sh, pc, b.Q);
+    ok = ok && sok;
+    if (fl & UWVK_EV_ACC) {
+      const double* z = ea.acc + (e * B + i) * 3;
+      if (all_finite(z, 3)) {
+        do_update<DOF, MK_ACC>(sm, sh, b, i, z, ea.acc_cov, ma, w, &sok);
+        ok = ok && sok;
+      } else {
+        nan = true;
+      }
+    }
+    if (fl & UWVK_EV_DVL) {
+      const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + i) * 3;
+      if (all_finite(z, 3)) {
+        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, b, i, z, ea.dvl_cov, ma, w, &sok);
+        ok = ok && sok;
+      } else {
+        nan = true;
+      }
+    }
+    if (fl & UWVK_EV_PRESSURE) {
+      const double* z = ea.pressure + (int64_t)ea.p_index[e] * B + i;
+      if (all_finite(z, 1)) {
+        cnt[1] += do_update<DOF, MK_PRESSURE>(sm, sh, b, i, z, &ea.p_cov, ma, w, &sok);
+        ok = ok && sok;
+      } else {
+        nan = true;
+      }
+    }
+    if (fl & UWVK_EV_ADCP) {
+      for (int c = 0; c < ea.cells; c++) {
+        const double* z = ea.adcp + (((int64_t)ea.a_index[e] * ea.cells + c) * B + i) * 2;
+        if (!all_finite(z, 2)) { nan = true; continue; }
+        double zz[2] = {z[0], z[1]}, R[4] = {ea.adcp_cov[0], ea.adcp_cov[1], ea.adcp_cov[2], ea.adcp_cov[3]};
+        HWater<DOF> h;
+        h.cw = ea.cw[c];
+        cnt[2] += pose_update<DOF, 2>(sm, zz, R, 1, 1, h, &sok);
+        ok = ok && sok;
+      }
+    }
+    if (fl & UWVK_EV_EFFORTS) {
+      MeasArgs me = ma;
+      me.only_vel = (fl & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0;
+      const double* z = ea.efforts + ((int64_t)ea.e_index[e] * B + i) * 6;
+      if (all_finite(z, 6)) {
+        cnt[3] += do_update<DOF, MK_EFFORTS>(sm, sh, b, i, z, ea.e_cov, me, w, &sok);
+        ok = ok && sok;
+      } else {
+        nan = true;
+      }
+    }
+  }
+  if (tid() == 0) {
+    if (!ok) b.status[i] |= UWVK_ST_NOTPD;
+    if (nan) b.status[i] |= UWVK_ST_NAN;
+    if (ea.count > 0) {
+      b.rot[i * 3] = w[0]; b.rot[i * 3 + 1] = w[1]; b.rot[i * 3 + 2] = w[2];
+    }
+    if (ea.accept_counts)
+      for (int k = 0; k < 4; k++) ea.accept_counts[i * 4 + k] += cnt[k];
+  }
+  store_instance<DOF>(sm, b, i);
+}
+
+template <int DOF>
+__global__ __launch_bounds__(64) void k_pose_rotation_rate(PoseBufs b, PoseShared sh, double* out) {
+  __shared__ Smem<DOF> sm;
+  const int64_t i = blockIdx.x;
+  if (lane_id() < Lay<DOF>::store) sm.mu[lane_id()] = b.mu[i * Lay<DOF>::store + lane_id()];
+  __syncthreads();
+  double w[3] = {b.rot[i * 3], b.rot[i * 3 + 1], b.rot[i * 3 + 2]}, o[3];
+  rotation_rate_body<DOF>(sm, sh, w, o);
+  if (lane_id() < 3) out[i * 3 + lane_id()] = o[lane_id()];
+}
+
+// ensemble statistics: one block per 64 instances, atomics into out
+template <int DOF>
+__global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, const double* truth, double* out) {
+  using L = Lay<DOF>;
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= b.batch) return;
+  const double* x = b.mu + i * L::store;
+  const double* P = b.sigma + i * (int64_t)(DOF * DOF);
+  double err[9];
+  for (int s = 0; s < L::store; s++) {
+    atomicAdd(&out[s], x[s]);
+    atomicAdd(&out[L::store + s], x[s] * x[s]);
+  }
+  for (int s = 0; s < L::store; s++) {
+    double e = x[s] - truth[s];
+    if (s >= 3 && s < 7) continue;
+    atomicAdd(&out[2 * L::store + s], e * e);
+  }
+  double r[3];
+  qboxminus(x + 3, truth + 3, r);
+  for (int k = 0; k < 3; k++) atomicAdd(&out[2 * L::store + 3 + k], r[k] * r[k]);
+  // NEES over (position, orientation, velocity): e^T P_sub^-1 e via a 9x9 Cholesky solve
+  for (int k = 0; k < 3; k++) { err[k] = x[k] - truth[k]; err[3 + k] = r[k]; err[6 + k] = x[7 + k] - truth[7 + k]; }
+  double A[81];
+  for (int a = 0; a < 9; a++)
+    for (int c = 0; c < 9; c++) A[a * 9 + c] = P[a * DOF + c];
+  for (int a = 0; a < 9; a++) {
+    for (int c = 0; c <= a; c++) {
+      double s = A[a * 9 + c];
+      for (int k = 0; k < c; k++) s -= A[a * 9 + k] * A[c * 9 + k];
+      A[a * 9 + c] = (a == c) ? sqrt(s) : s / A[c * 9 + c];
+    }
+  }
+  double y[9], nees = 0;
+  for (int a = 0; a < 9; a++) {
+    double s = err[a];
+    for (int k = 0; k < a; k++) s -= A[a * 9 + k] * y[k];
+    y[a] = s / A[a * 9 + a];
+    nees += y[a] * y[a];
+  }
+  atomicAdd(&out[3 * L::store], nees);
+}
+
+
+#endif  // UWVK_POSE_KERNEL_BODIES
+
+}  // namespace uwvk

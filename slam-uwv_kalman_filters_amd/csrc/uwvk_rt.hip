@@ -1,0 +1,62 @@
+// uwvk_rt.hip — library-level entry points of the C ABI (device probe, memory
+// helpers, status strings).  There is deliberately no CPU fallback anywhere in
+// libuwvk.so: without a gfx950 device every handle creation fails loudly.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "../../include/uwvk.h"
+
+__global__ void uwvk_probe_kernel(int* out) {
+  if (threadIdx.x == 0) out[0] = 0x5a5a;
+}
+
+extern "C" {
+
+int uwvk_abi_version(void) { return UWVK_ABI_VERSION; }
+
+int uwvk_device_available(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return 0;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, device) != hipSuccess) return 0;
+  if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0) return 0;
+  if (hipSetDevice(device) != hipSuccess) return 0;
+  // make sure this library's gfx950 code object actually loads and runs
+  int* d = nullptr;
+  int h = 0;
+  if (hipMalloc(&d, sizeof(int)) != hipSuccess) return 0;
+  hipLaunchKernelGGL(uwvk_probe_kernel, dim3(1), dim3(64), 0, 0, d);
+  bool ok = hipGetLastError() == hipSuccess && hipMemcpy(&h, d, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess;
+  hipFree(d);
+  return ok && h == 0x5a5a;
+}
+
+const char* uwvk_status_string(uwvk_status s) {
+  switch (s) {
+    case UWVK_OK: return "UWVK_OK";
+    case UWVK_EINVAL: return "UWVK_EINVAL: invalid argument";
+    case UWVK_ENAN: return "UWVK_ENAN: measurement contains NaN/Inf";
+    case UWVK_ENOTPD: return "UWVK_ENOTPD: covariance not positive definite";
+    case UWVK_ENOMODEL: return "UWVK_ENOMODEL: Motion model is not initialized!";
+    case UWVK_EDEVICE: return "UWVK_EDEVICE: no usable gfx950 device / HIP error";
+    case UWVK_ENOMEM: return "UWVK_ENOMEM: device allocation failed";
+    case UWVK_ENOTINIT: return "UWVK_ENOTINIT: filter state not initialised";
+  }
+  return "UWVK_?";
+}
+
+uwvk_status uwvk_device_malloc(int device, size_t bytes, void** out) {
+  if (!out) return UWVK_EINVAL;
+  if (hipSetDevice(device) != hipSuccess) return UWVK_EDEVICE;
+  return hipMalloc(out, bytes ? bytes : 16) == hipSuccess ? UWVK_OK : UWVK_ENOMEM;
+}
+uwvk_status uwvk_device_free(void* p) { return hipFree(p) == hipSuccess ? UWVK_OK : UWVK_EDEVICE; }
+uwvk_status uwvk_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
+}
+uwvk_status uwvk_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
+}
+
+}  // extern "C"

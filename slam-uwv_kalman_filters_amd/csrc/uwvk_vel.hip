@@ -1,0 +1,665 @@
+// uwvk_vel.hip — VelocityUKF (src/VelocityUKF.hpp:231-266, VelocityUKF.cpp) on
+// gfx950: one filter instance per LANE.  The state is 4 DOF (body velocity +
+// z position) with 9 sigma points, so Sigma, the sigma points and the RK4
+// integration of the [EXT] uwv_dynamic_model ModelSimulation all live in
+// VGPRs; the kernel is bound by the fp64 model evaluation (9 x RK4 per predict).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "uwvk_dev.hpp"
+#include "uwvk_host.hpp"
+
+using namespace uwvk;
+
+namespace {
+
+struct VelShared {  // batch-shared model parameters (by value)
+  double M[36], Dl[36], Dq[36], Minv[36];
+  double weight, buoyancy, cog[3], cob[3];
+  double Q0[16];  // process_noise_cov (VelocityUKF.cpp:54-55)
+};
+
+struct VelBufs {
+  int64_t batch;
+  double* mu;       // [batch][4]
+  double* sigma;    // [batch][16]
+  double* gyro;     // [batch][3]  stored GyroMeasurement
+  double* efforts;  // [batch][6]  stored BodyEffortsMeasurement
+  double* model;    // [batch][13] motion_model pose p(3) q(4) v(3) w(3)
+  uint32_t* status;
+};
+
+struct VelEpochArgs {
+  const uint32_t* flags;
+  const double* gyro;     // [epochs][batch][3]
+  const double* efforts;  // [epochs][batch][6]
+  const int32_t* dvl_index;
+  const double* dvl;
+  double dvl_cov[9];
+  const int32_t* p_index;
+  const double* pressure;
+  double p_cov;
+  double dt;
+  int64_t first, count;
+};
+
+// ---- [EXT] ModelSimulation: M nu_dot + C(nu) nu + D(nu) nu + g(q) = tau, RK4 --
+UWVK_DEV void v_coriolis(const VelShared& P, const double nu[6], double c[6]) {
+  double a[3], b[3], t0[3], t1[3], t2[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    double sa = 0, sb = 0;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      sa += P.M[i * 6 + j] * nu[j];
+      sb += P.M[(3 + i) * 6 + j] * nu[j];
+    }
+    a[i] = sa; b[i] = sb;
+  }
+  cross3(nu + 3, a, t0);
+  cross3(nu, a, t1);
+  cross3(nu + 3, b, t2);
+#pragma unroll
+  for (int i = 0; i < 3; i++) { c[i] = t0[i]; c[3 + i] = t1[i] + t2[i]; }
+}
+
+UWVK_DEV void v_deriv(const VelShared& P, const double tau[6], const double s[13], double ds[13]) {
+  const double q[4] = {s[3], s[4], s[5], s[6]};
+  const double nu[6] = {s[7], s[8], s[9], s[10], s[11], s[12]};
+  const double v[3] = {s[7], s[8], s[9]};
+  qrot(q, v, ds);
+  const double wq[4] = {0, s[10], s[11], s[12]};
+  double qd[4];
+  qmul(q, wq, qd);
+#pragma unroll
+  for (int i = 0; i < 4; i++) ds[3 + i] = 0.5 * qd[i];
+  double c[6], d[6], g[6], r[6];
+  v_coriolis(P, nu, c);
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    double sl = 0, sq = 0;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      sl += P.Dl[i * 6 + j] * nu[j];
+      sq += P.Dq[i * 6 + j] * (fabs(nu[j]) * nu[j]);
+    }
+    d[i] = sl + sq;
+  }
+  const double fw[3] = {0, 0, -P.weight}, fb[3] = {0, 0, P.buoyancy};
+  double fg[3], fbb[3], mg[3], mb[3];
+  qrot_inv(q, fw, fg);
+  qrot_inv(q, fb, fbb);
+  cross3(P.cog, fg, mg);
+  cross3(P.cob, fbb, mb);
+#pragma unroll
+  for (int i = 0; i < 3; i++) { g[i] = -(fg[i] + fbb[i]); g[3 + i] = -(mg[i] + mb[i]); }
+#pragma unroll
+  for (int i = 0; i < 6; i++) r[i] = tau[i] - c[i] - d[i] - g[i];
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    double a = 0;
+#pragma unroll
+    for (int j = 0; j < 6; j++) a += P.Minv[i * 6 + j] * r[j];
+    ds[7 + i] = a;
+  }
+}
+
+UWVK_DEV void v_rk4(const VelShared& P, const double tau[6], double dt, const double s[13], double o[13]) {
+  double k1[13], k2[13], k3[13], k4[13], t[13];
+  v_deriv(P, tau, s, k1);
+#pragma unroll
+  for (int i = 0; i < 13; i++) t[i] = s[i] + 0.5 * dt * k1[i];
+  v_deriv(P, tau, t, k2);
+#pragma unroll
+  for (int i = 0; i < 13; i++) t[i] = s[i] + 0.5 * dt * k2[i];
+  v_deriv(P, tau, t, k3);
+#pragma unroll
+  for (int i = 0; i < 13; i++) t[i] = s[i] + dt * k3[i];
+  v_deriv(P, tau, t, k4);
+#pragma unroll
+  for (int i = 0; i < 13; i++) o[i] = s[i] + (dt / 6.0) * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
+  const double n = sqrt(o[3] * o[3] + o[4] * o[4] + o[5] * o[5] + o[6] * o[6]);
+#pragma unroll
+  for (int i = 3; i < 7; i++) o[i] /= n;
+}
+
+// ---- 4-DOF vector-manifold UKF core in registers [EXT ukfom] -----------------
+UWVK_DEV bool v_chol(const double A[16], double L[16]) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 16; i++) L[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+#pragma unroll
+    for (int j = 0; j <= i; j++) {
+      double s = A[i * 4 + j];
+#pragma unroll
+      for (int k = 0; k < j; k++) s -= L[i * 4 + k] * L[j * 4 + k];
+      if (i == j) {
+        ok = ok && (s > 0.0);
+        L[i * 4 + i] = sqrt(s);
+      } else {
+        L[i * 4 + j] = s / L[j * 4 + j];
+      }
+    }
+  }
+  return ok;
+}
+
+UWVK_DEV void v_points(const double mu[4], const double L[16], double X[9][4]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) X[0][k] = mu[k];
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      X[2 * j + 1][k] = mu[k] + 1.0 * L[k * 4 + j];
+      X[2 * j + 2][k] = mu[k] + -1.0 * L[k * 4 + j];
+    }
+}
+
+// manifold mean (all-vector here): ref = X0, delta = mean(X - ref), |delta| <= 1e-6
+template <int M, int N>
+UWVK_DEV void v_mean(const double (&X)[N][M], double ref[M]) {
+#pragma unroll
+  for (int k = 0; k < M; k++) ref[k] = X[0][k];
+  int it = 0;
+  double nrm;
+  do {
+    double d[M];
+#pragma unroll
+    for (int k = 0; k < M; k++) d[k] = 0.0;
+#pragma unroll
+    for (int p = 0; p < N; p++)
+#pragma unroll
+      for (int k = 0; k < M; k++) d[k] += X[p][k] - ref[k];
+    nrm = 0.0;
+#pragma unroll
+    for (int k = 0; k < M; k++) {
+      d[k] /= (double)N;
+      nrm += d[k] * d[k];
+    }
+#pragma unroll
+    for (int k = 0; k < M; k++) ref[k] = ref[k] + 1.0 * d[k];
+    nrm = sqrt(nrm);
+  } while (nrm > 1e-6 && ++it < 10000);
+}
+
+UWVK_DEV void v_cov(const double (&X)[9][4], const double mean[4], double S[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) S[i] = 0.0;
+#pragma unroll
+  for (int p = 0; p < 9; p++) {
+    double d[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[k] = X[p][k] - mean[k];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) S[i * 4 + j] += d[i] * d[j];
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) S[i] = 0.5 * S[i];
+}
+
+// processMotionModel, VelocityUKF.cpp:6-33
+UWVK_DEV void v_process(const VelShared& P, const double q[4], const double w[3], const double tau[6], double dt,
+                        double x[4]) {
+  double s[13], n[13], r[3], t[3];
+  s[0] = s[1] = s[2] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) s[3 + k] = q[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { s[7 + k] = x[k]; s[10 + k] = w[k]; }
+  v_rk4(P, tau, dt, s, n);
+#pragma unroll
+  for (int i = 0; i < 3; i++) t[i] = x[i] + (n[7 + i] - x[i]);
+  qrot(q, t, r);
+  x[3] = x[3] + dt * r[2];
+  x[0] = t[0]; x[1] = t[1]; x[2] = t[2];
+}
+
+UWVK_DEV bool v_predict(const VelShared& P, double mu[4], double S[16], const double model[13], const double w[3],
+                        const double tau[6], double dt) {
+  double L[16], X[9][4];
+  const bool ok = v_chol(S, L);
+  v_points(mu, L, X);
+  const double q[4] = {model[3], model[4], model[5], model[6]};
+#pragma unroll
+  for (int p = 0; p < 9; p++) v_process(P, q, w, tau, dt, X[p]);
+  v_mean<4, 9>(X, mu);
+  v_cov(X, mu, S);
+#pragma unroll
+  for (int i = 0; i < 16; i++) S[i] += dt * P.Q0[i];
+  return ok;
+}
+
+// update with h = a sub-vector of the state (DVL: v, m = 3; pressure: z, m = 1),
+// vect-manifold measurement (iterative mean), accept any
+template <int M, int OFF>
+UWVK_DEV bool v_update(double mu[4], double S[16], const double z[M], const double R[M * M]) {
+  double L[16], X[9][4], Z[9][M];
+  bool ok = v_chol(S, L);
+  v_points(mu, L, X);
+#pragma unroll
+  for (int p = 0; p < 9; p++)
+#pragma unroll
+    for (int a = 0; a < M; a++) Z[p][a] = X[p][OFF + a];
+  double zm[M];
+  v_mean<M, 9>(Z, zm);
+  double Sz[M * M], C[4 * M], Si[M * M], K[4 * M], nu[M];
+#pragma unroll
+  for (int i = 0; i < M * M; i++) Sz[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4 * M; i++) C[i] = 0.0;
+#pragma unroll
+  for (int p = 0; p < 9; p++) {
+    double dz[M], dx[4];
+#pragma unroll
+    for (int a = 0; a < M; a++) dz[a] = Z[p][a] - zm[a];
+#pragma unroll
+    for (int k = 0; k < 4; k++) dx[k] = X[p][k] - mu[k];
+#pragma unroll
+    for (int a = 0; a < M; a++)
+#pragma unroll
+      for (int b = 0; b < M; b++) Sz[a * M + b] += dz[a] * dz[b];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int a = 0; a < M; a++) C[i * M + a] += dx[i] * dz[a];
+  }
+#pragma unroll
+  for (int i = 0; i < M * M; i++) Sz[i] = 0.5 * Sz[i] + R[i];
+#pragma unroll
+  for (int i = 0; i < 4 * M; i++) C[i] = 0.5 * C[i];
+  if constexpr (M == 1) {
+    Si[0] = 1.0 / Sz[0];
+  } else {
+    const double* A = Sz;
+    const double c00 = A[4] * A[8] - A[5] * A[7];
+    const double c01 = A[5] * A[6] - A[3] * A[8];
+    const double c02 = A[3] * A[7] - A[4] * A[6];
+    const double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+    const double id = 1.0 / det;
+    Si[0] = c00 * id;
+    Si[1] = (A[2] * A[7] - A[1] * A[8]) * id;
+    Si[2] = (A[1] * A[5] - A[2] * A[4]) * id;
+    Si[3] = c01 * id;
+    Si[4] = (A[0] * A[8] - A[2] * A[6]) * id;
+    Si[5] = (A[2] * A[3] - A[0] * A[5]) * id;
+    Si[6] = c02 * id;
+    Si[7] = (A[1] * A[6] - A[0] * A[7]) * id;
+    Si[8] = (A[0] * A[4] - A[1] * A[3]) * id;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int a = 0; a < M; a++) {
+      double s = 0.0;
+#pragma unroll
+      for (int b = 0; b < M; b++) s += C[i * M + b] * Si[b * M + a];
+      K[i * M + a] = s;
+    }
+#pragma unroll
+  for (int a = 0; a < M; a++) nu[a] = z[a] - zm[a];
+  // accept_any_mahalanobis_distance: Sigma -= C K^T, apply_delta(K nu)
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      double s = 0.0;
+#pragma unroll
+      for (int a = 0; a < M; a++) s += C[i * M + a] * K[j * M + a];
+      S[i * 4 + j] -= s;
+    }
+  double delta[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    double s = 0.0;
+#pragma unroll
+    for (int a = 0; a < M; a++) s += K[i * M + a] * nu[a];
+    delta[i] = s;
+  }
+  ok = v_chol(S, L) && ok;
+  v_points(mu, L, X);
+#pragma unroll
+  for (int k = 0; k < 4; k++) mu[k] = mu[k] + 1.0 * delta[k];
+#pragma unroll
+  for (int p = 0; p < 9; p++)
+#pragma unroll
+    for (int k = 0; k < 4; k++) X[p][k] = X[p][k] + 1.0 * delta[k];
+  v_cov(X, mu, S);
+  return ok;
+}
+
+UWVK_DEV void v_load(const VelBufs& b, int64_t i, double mu[4], double S[16]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) mu[k] = b.mu[i * 4 + k];
+#pragma unroll
+  for (int k = 0; k < 16; k++) S[k] = b.sigma[i * 16 + k];
+}
+UWVK_DEV void v_store(const VelBufs& b, int64_t i, const double mu[4], const double S[16]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) b.mu[i * 4 + k] = mu[k];
+#pragma unroll
+  for (int k = 0; k < 16; k++) b.sigma[i * 16 + k] = S[k];
+}
+
+__global__ __launch_bounds__(64) void k_vel_predict(VelBufs b, VelShared P, double dt) {
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= b.batch) return;
+  double mu[4], S[16], m[13], w[3], tau[6];
+  v_load(b, i, mu, S);
+#pragma unroll
+  for (int k = 0; k < 13; k++) m[k] = b.model[i * 13 + k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) w[k] = b.gyro[i * 3 + k];
+#pragma unroll
+  for (int k = 0; k < 6; k++) tau[k] = b.efforts[i * 6 + k];
+  const bool ok = v_predict(P, mu, S, m, w, tau, dt);
+  double n[13];
+  v_rk4(P, tau, dt, m, n);  // motion_model->sendEffort(tau) (VelocityUKF.cpp:126-127)
+#pragma unroll
+  for (int k = 0; k < 13; k++) b.model[i * 13 + k] = n[k];
+  if (!ok) b.status[i] |= UWVK_ST_NOTPD;
+  v_store(b, i, mu, S);
+}
+
+template <int M, int OFF>
+__global__ __launch_bounds__(64) void k_vel_update(VelBufs b, const double* z, const double* cov, VelShared P,
+                                                   double shared_cov0, const double* shared_cov, const uint8_t* mask) {
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= b.batch || (mask && !mask[i])) return;
+  double mu[4], S[16], zz[M], R[M * M];
+  v_load(b, i, mu, S);
+#pragma unroll
+  for (int a = 0; a < M; a++) zz[a] = z[i * M + a];
+#pragma unroll
+  for (int a = 0; a < M * M; a++) R[a] = cov ? cov[i * M * M + a] : shared_cov[a];
+  const bool ok = v_update<M, OFF>(mu, S, zz, R);
+  if (!ok) b.status[i] |= UWVK_ST_NOTPD;
+  v_store(b, i, mu, S);
+  (void)P;
+  (void)shared_cov0;
+}
+
+__global__ __launch_bounds__(64) void k_vel_epoch(VelBufs b, VelShared P, VelEpochArgs ea) {
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= b.batch) return;
+  const int64_t B = b.batch;
+  double mu[4], S[16], m[13], w[3], tau[6];
+  v_load(b, i, mu, S);
+#pragma unroll
+  for (int k = 0; k < 13; k++) m[k] = b.model[i * 13 + k];
+  bool ok = true;
+  for (int64_t e = ea.first; e < ea.first + ea.count; e++) {
+    // GyroMeasurement: stored + copied into the motion model (VelocityUKF.cpp:87-98)
+#pragma unroll
+    for (int k = 0; k < 3; k++) { w[k] = ea.gyro[(e * B + i) * 3 + k]; m[10 + k] = w[k]; }
+#pragma unroll
+    for (int k = 0; k < 6; k++) tau[k] = ea.efforts[(e * B + i) * 6 + k];
+    ok = v_predict(P, mu, S, m, w, tau, ea.dt) && ok;
+    double n[13];
+    v_rk4(P, tau, ea.dt, m, n);
+#pragma unroll
+    for (int k = 0; k < 13; k++) m[k] = n[k];
+    const uint32_t fl = ea.flags[e];
+    if (fl & UWVK_EV_DVL) {
+      const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + i) * 3;
+      const double zz[3] = {z[0], z[1], z[2]};
+      ok = v_update<3, 0>(mu, S, zz, ea.dvl_cov) && ok;
+    }
+    if (fl & UWVK_EV_PRESSURE) {
+      const double zz[1] = {ea.pressure[(int64_t)ea.p_index[e] * B + i]};
+      const double R[1] = {ea.p_cov};
+      ok = v_update<1, 3>(mu, S, zz, R) && ok;
+    }
+  }
+  if (ea.count > 0) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) b.gyro[i * 3 + k] = w[k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) b.efforts[i * 6 + k] = tau[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 13; k++) b.model[i * 13 + k] = m[k];
+  if (!ok) b.status[i] |= UWVK_ST_NOTPD;
+  v_store(b, i, mu, S);
+}
+
+__global__ void k_vel_setup(VelBufs b) {  // setupMotionModel pose (VelocityUKF.cpp:65-74)
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= b.batch) return;
+  double* m = b.model + i * 13;
+  m[0] = m[1] = m[2] = 0.0;
+  m[3] = 1.0; m[4] = m[5] = m[6] = 0.0;
+  for (int k = 0; k < 3; k++) { m[7 + k] = b.mu[i * 4 + k]; m[10 + k] = b.gyro[i * 3 + k]; }
+}
+
+__global__ void k_vel_gyro_to_model(VelBufs b) {
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= b.batch) return;
+  for (int k = 0; k < 3; k++) b.model[i * 13 + 10 + k] = b.gyro[i * 3 + k];
+}
+
+}  // namespace
+
+struct uwvk_vel {
+  int64_t batch = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  double *d_mu = nullptr, *d_sigma = nullptr, *d_gyro = nullptr, *d_eff = nullptr, *d_model = nullptr,
+         *d_meas = nullptr;
+  uint8_t* d_mask = nullptr;
+  uint32_t* d_status = nullptr;
+  VelShared P{};
+  bool has_state = false, has_model = false;
+};
+
+static VelBufs vbufs(const uwvk_vel* h) {
+  VelBufs b;
+  b.batch = h->batch; b.mu = h->d_mu; b.sigma = h->d_sigma; b.gyro = h->d_gyro; b.efforts = h->d_eff;
+  b.model = h->d_model; b.status = h->d_status;
+  return b;
+}
+
+#define HIPCHK(x)                              \
+  do {                                         \
+    if ((x) != hipSuccess) return UWVK_EDEVICE; \
+  } while (0)
+
+static unsigned vgrid(int64_t B) { return (unsigned)((B + 63) / 64); }
+
+static bool vfinite(const double* a, size_t n) {
+  for (size_t k = 0; k < n; k++)
+    if (!std::isfinite(a[k])) return false;
+  return true;
+}
+
+extern "C" {
+
+uwvk_status uwvk_vel_create(int64_t batch, int device, uwvk_vel** out) {
+  if (!out || batch <= 0) return UWVK_EINVAL;
+  *out = nullptr;
+  if (!uwvk_device_available(device)) return UWVK_EDEVICE;
+  uwvk_vel* h = new uwvk_vel();
+  h->batch = batch;
+  h->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return UWVK_EDEVICE;
+  }
+  const size_t B = (size_t)batch;
+  const bool ok = hipMalloc(&h->d_mu, B * 4 * 8) == hipSuccess && hipMalloc(&h->d_sigma, B * 16 * 8) == hipSuccess &&
+                  hipMalloc(&h->d_gyro, B * 3 * 8) == hipSuccess && hipMalloc(&h->d_eff, B * 6 * 8) == hipSuccess &&
+                  hipMalloc(&h->d_model, B * 13 * 8) == hipSuccess && hipMalloc(&h->d_meas, B * 12 * 8) == hipSuccess &&
+                  hipMalloc(&h->d_mask, B) == hipSuccess && hipMalloc(&h->d_status, B * 4) == hipSuccess;
+  if (!ok) {
+    uwvk_vel_destroy(h);
+    return UWVK_ENOMEM;
+  }
+  (void)hipMemsetAsync(h->d_gyro, 0, B * 3 * 8, h->stream);
+  (void)hipMemsetAsync(h->d_eff, 0, B * 6 * 8, h->stream);
+  (void)hipMemsetAsync(h->d_model, 0, B * 13 * 8, h->stream);
+  (void)hipMemsetAsync(h->d_status, 0, B * 4, h->stream);
+  // process_noise_cov = 0 except velocity diag 1e-4 (VelocityUKF.cpp:54-55)
+  for (int k = 0; k < 3; k++) h->P.Q0[k * 4 + k] = 0.0001;
+  if (hipStreamSynchronize(h->stream) != hipSuccess) {
+    uwvk_vel_destroy(h);
+    return UWVK_EDEVICE;
+  }
+  *out = h;
+  return UWVK_OK;
+}
+
+void uwvk_vel_destroy(uwvk_vel* h) {
+  if (!h) return;
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_gyro, (void*)h->d_eff, (void*)h->d_model,
+                  (void*)h->d_meas, (void*)h->d_mask, (void*)h->d_status})
+    if (p) (void)hipFree(p);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+void* uwvk_vel_stream(const uwvk_vel* h) { return h ? (void*)h->stream : nullptr; }
+
+uwvk_status uwvk_vel_init(uwvk_vel* h, const double* x, const double* P) {
+  if (!h || !x || !P) return UWVK_EINVAL;
+  HIPCHK(hipMemcpyAsync(h->d_mu, x, (size_t)h->batch * 4 * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d_sigma, P, (size_t)h->batch * 16 * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->has_state = true;
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_vel_setup_motion_model(uwvk_vel* h, const uwvk_uwv_params* u) {
+  if (!h || !u) return UWVK_EINVAL;
+  if (!h->has_state) return UWVK_ENOTINIT;
+  std::memcpy(h->P.M, u->inertia_matrix, 36 * 8);
+  std::memcpy(h->P.Dl, u->damping_matrices[0], 36 * 8);
+  std::memcpy(h->P.Dq, u->damping_matrices[1], 36 * 8);
+  if (!host::invert6(u->inertia_matrix, h->P.Minv)) return UWVK_EINVAL;
+  h->P.weight = u->weight;
+  h->P.buoyancy = u->buoyancy;
+  for (int k = 0; k < 3; k++) {
+    h->P.cog[k] = u->distance_body2centerofgravity[k];
+    h->P.cob[k] = u->distance_body2centerofbuoyancy[k];
+  }
+  hipLaunchKernelGGL(k_vel_setup, dim3(vgrid(h->batch)), dim3(64), 0, h->stream, vbufs(h));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->has_model = true;
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_vel_set_gyro(uwvk_vel* h, const double* w, const double* cov) {
+  if (!h || !w) return UWVK_EINVAL;
+  if (!vfinite(w, (size_t)h->batch * 3) || (cov && !vfinite(cov, (size_t)h->batch * 9))) return UWVK_ENAN;
+  HIPCHK(hipMemcpyAsync(h->d_gyro, w, (size_t)h->batch * 3 * 8, hipMemcpyHostToDevice, h->stream));
+  if (h->has_model) {
+    hipLaunchKernelGGL(k_vel_gyro_to_model, dim3(vgrid(h->batch)), dim3(64), 0, h->stream, vbufs(h));
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_vel_set_efforts(uwvk_vel* h, const double* tau, const double* cov) {
+  if (!h || !tau) return UWVK_EINVAL;
+  if (!vfinite(tau, (size_t)h->batch * 6) || (cov && !vfinite(cov, (size_t)h->batch * 36))) return UWVK_ENAN;
+  HIPCHK(hipMemcpyAsync(h->d_eff, tau, (size_t)h->batch * 6 * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_vel_predict(uwvk_vel* h, double dt) {
+  if (!h) return UWVK_EINVAL;
+  if (!h->has_model) return UWVK_ENOMODEL;  // VelocityUKF.cpp:117-118
+  hipLaunchKernelGGL(k_vel_predict, dim3(vgrid(h->batch)), dim3(64), 0, h->stream, vbufs(h), h->P, dt);
+  HIPCHK(hipGetLastError());
+  return UWVK_OK;
+}
+
+static uwvk_status vel_update(uwvk_vel* h, int m, const double* mu, const double* cov, const double* shared_cov,
+                              const uint8_t* mask) {
+  if (!h || !mu || (!cov && !shared_cov)) return UWVK_EINVAL;
+  if (!h->has_state) return UWVK_ENOTINIT;
+  const int64_t B = h->batch;
+  for (int64_t i = 0; i < B; i++) {
+    if (mask && !mask[i]) continue;
+    if (!vfinite(mu + i * m, m) || (cov && !vfinite(cov + i * m * m, (size_t)m * m))) return UWVK_ENAN;
+  }
+  if (!cov && !vfinite(shared_cov, (size_t)m * m)) return UWVK_ENAN;
+  double* dz = h->d_meas;
+  double* dc = h->d_meas + B * 3;
+  HIPCHK(hipMemcpyAsync(dz, mu, (size_t)B * m * 8, hipMemcpyHostToDevice, h->stream));
+  const double* dcov = nullptr;
+  if (cov) {
+    HIPCHK(hipMemcpyAsync(dc, cov, (size_t)B * m * m * 8, hipMemcpyHostToDevice, h->stream));
+    dcov = dc;
+  }
+  double* dshared = h->d_meas + B * 12 - 9;
+  if (!cov) HIPCHK(hipMemcpyAsync(dshared, shared_cov, (size_t)m * m * 8, hipMemcpyHostToDevice, h->stream));
+  const uint8_t* dmask = nullptr;
+  if (mask) {
+    HIPCHK(hipMemcpyAsync(h->d_mask, mask, (size_t)B, hipMemcpyHostToDevice, h->stream));
+    dmask = h->d_mask;
+  }
+  if (m == 3)
+    hipLaunchKernelGGL((k_vel_update<3, 0>), dim3(vgrid(B)), dim3(64), 0, h->stream, vbufs(h), dz, dcov, h->P, 0.0,
+                       dshared, dmask);
+  else
+    hipLaunchKernelGGL((k_vel_update<1, 3>), dim3(vgrid(B)), dim3(64), 0, h->stream, vbufs(h), dz, dcov, h->P, 0.0,
+                       dshared, dmask);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_vel_update_dvl(uwvk_vel* h, const double* mu, const double* cov, const double* sc,
+                                const uint8_t* mask) {
+  return vel_update(h, 3, mu, cov, sc, mask);
+}
+uwvk_status uwvk_vel_update_pressure(uwvk_vel* h, const double* mu, const double* cov, const double* sc,
+                                     const uint8_t* mask) {
+  return vel_update(h, 1, mu, cov, sc, mask);
+}
+
+uwvk_status uwvk_vel_get_state(uwvk_vel* h, double* x, double* P) {
+  if (!h || !x) return UWVK_EINVAL;
+  HIPCHK(hipMemcpyAsync(x, h->d_mu, (size_t)h->batch * 4 * 8, hipMemcpyDeviceToHost, h->stream));
+  if (P) HIPCHK(hipMemcpyAsync(P, h->d_sigma, (size_t)h->batch * 16 * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_vel_get_model_state(uwvk_vel* h, double* out) {
+  if (!h || !out) return UWVK_EINVAL;
+  HIPCHK(hipMemcpyAsync(out, h->d_model, (size_t)h->batch * 13 * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_vel_run_log(uwvk_vel* h, const uwvk_vel_log* log, int64_t first, int64_t count) {
+  if (!h || !log || first < 0 || count < 0 || first + count > log->epochs) return UWVK_EINVAL;
+  if (!h->has_model) return UWVK_ENOMODEL;
+  VelEpochArgs ea{};
+  ea.flags = log->flags; ea.gyro = log->gyro; ea.efforts = log->efforts;
+  ea.dvl_index = log->dvl_index; ea.dvl = log->dvl;
+  std::memcpy(ea.dvl_cov, log->dvl_cov, sizeof(ea.dvl_cov));
+  ea.p_index = log->pressure_index; ea.pressure = log->pressure; ea.p_cov = log->pressure_cov;
+  ea.dt = log->dt;
+  for (int64_t e = first; e < first + count; e++) {
+    ea.first = e;
+    ea.count = 1;
+    hipLaunchKernelGGL(k_vel_epoch, dim3(vgrid(h->batch)), dim3(64), 0, h->stream, vbufs(h), h->P, ea);
+    HIPCHK(hipGetLastError());
+  }
+  return UWVK_OK;
+}
+
+}  // extern "C"

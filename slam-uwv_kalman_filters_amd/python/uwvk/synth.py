@@ -1,0 +1,308 @@
+"""Synthetic AUV scenario and measurement logs for the batched UKF engine.
+
+The reference ships no driver and no data: the event
+order and sensor rates of a mission come from an out-of-repo orogen task.  This
+module is that driver for benches and parity tests.  It builds
+
+* the builder-chosen common settings of SURVEY.md §8(d) (location, IMU noise,
+  hydrodynamic model, water currents, sensor noise), as the reference's config
+  structs (`abi.PoseConfig`, PoseUKFConfig.hpp:159-194),
+* a truth trajectory (lawnmower-like: 1 m/s surge, 10 m depth,
+  yaw rate 0.1*sin(0.05 t) rad/s),
+* per-instance noisy IMU / DVL / pressure / ADCP / body-effort logs, seeded with
+  numpy's counter-based Philox generator (instance i, stream id) so a sub-batch
+  reproduces exactly the rows of the full batch.
+
+Epoch e (0-based) is: RotationRate(gyro[e]) -> predictionStep(dt) ->
+Acceleration(acc[e]) -> (DVL | Pressure | ADCP cells | BodyEfforts when flagged),
+all measurements taken at t = (e + 1) * dt.
+"""
+import numpy as np
+
+from . import abi
+
+EARTHW = 7.292115e-5
+LAT0, LON0 = 0.925, 0.154
+SEED = 20250218
+
+
+def default_pose_config():
+    c = abi.PoseConfig()
+    abi.fill(c.acceleration.randomwalk, [1e-3] * 3)
+    abi.fill(c.acceleration.bias_offset, [0.0] * 3)
+    abi.fill(c.acceleration.bias_instability, [1e-4] * 3)
+    c.acceleration.bias_tau = 600.0
+    abi.fill(c.rotation_rate.randomwalk, [1e-4] * 3)
+    abi.fill(c.rotation_rate.bias_offset, [0.0] * 3)
+    abi.fill(c.rotation_rate.bias_instability, [1e-5] * 3)
+    c.rotation_rate.bias_tau = 600.0
+    m = c.model_noise_parameters
+    abi.fill(m.body_efforts_std, [5.0, 5.0, 5.0, 1.0, 1.0, 1.0])
+    abi.fill(m.inertia_instability, [10.0] * 9)
+    abi.fill(m.lin_damping_instability, [5.0] * 9)
+    abi.fill(m.quad_damping_instability, [5.0] * 9)
+    m.inertia_tau = m.lin_damping_tau = m.quad_damping_tau = 3600.0
+    w = c.water_velocity
+    w.tau, w.limits, w.scale = 900.0, 0.1, 1e-3
+    abi.fill(w.measurement_std, [0.05] * 3)
+    w.cell_size, w.first_cell_blank, w.minimum_correlation = 1.0, 0.5, 0.5
+    w.adcp_bias_tau, w.adcp_bias_limits = 900.0, 0.05
+    c.location.latitude, c.location.longitude, c.location.altitude = LAT0, LON0, 0.0
+    h = c.hydrostatics
+    h.water_density, h.water_density_limits, h.water_density_tau = 1025.0, 2.0, 3600.0
+    h.atmospheric_pressure, h.pressure_std = 101325.0, 100.0
+    abi.fill(c.max_jerk, [0.5] * 3)
+    abi.fill(c.max_effort, [100.0] * 6)
+    c.dynamic_model_min_depth = 1.0
+    return c
+
+
+def default_uwv():
+    u = abi.UWVParams()
+    M = np.diag([200.0, 250.0, 300.0, 20.0, 30.0, 30.0])
+    Dl = np.diag([20.0, 30.0, 40.0, 5.0, 5.0, 5.0])
+    Dq = np.diag([50.0, 80.0, 100.0, 10.0, 10.0, 10.0])
+    abi.fill(u.inertia_matrix, M.ravel())
+    abi.fill(u.damping_matrices[0], Dl.ravel())
+    abi.fill(u.damping_matrices[1], Dq.ravel())
+    u.weight = u.buoyancy = 2000.0
+    abi.fill(u.distance_body2centerofgravity, [0.0, 0.0, 0.0])
+    abi.fill(u.distance_body2centerofbuoyancy, [0.0, 0.0, 0.05])
+    return u
+
+
+def uwv_arrays(u):
+    M = np.array(u.inertia_matrix[:]).reshape(6, 6)
+    Dl = np.array(u.damping_matrices[0][:]).reshape(6, 6)
+    Dq = np.array(u.damping_matrices[1][:]).reshape(6, 6)
+    return M, Dl, Dq
+
+
+def wgs84_gravity(lat, alt):
+    s2 = np.sin(lat) ** 2
+    return 9.7803253359 * (1.0 + 0.00193185265241 * s2) / np.sqrt(1.0 - 0.00669437999013 * s2) - 3.086e-6 * alt
+
+
+def _rotz_T(psi, v):
+    """R_z(psi)^T v for arrays: psi [...], v [..., 3]."""
+    c, s = np.cos(psi), np.sin(psi)
+    return np.stack([c * v[..., 0] + s * v[..., 1], -s * v[..., 0] + c * v[..., 1], v[..., 2]], axis=-1)
+
+
+def calc_efforts_np(M, Dl, Dq, acc6, vel6, weight=2000.0, buoyancy=2000.0, cob=(0, 0, 0.05), psi=None):
+    """Numpy restatement of the [EXT] calcEfforts convention (truth generation only)."""
+    v, w = vel6[..., :3], vel6[..., 3:]
+    a = vel6 @ M[:3].T
+    b = vel6 @ M[3:].T
+    cor = np.concatenate([np.cross(w, a), np.cross(v, a) + np.cross(w, b)], axis=-1)
+    damp = vel6 @ Dl.T + (np.abs(vel6) * vel6) @ Dq.T
+    # level vehicle (roll = pitch = 0): body z is nav z, restoring forces cancel for W = B,
+    # moment r_b x f_b with f_b = (0,0,B) vanishes for r_b on the z axis.
+    fg = np.array([0, 0, -weight])
+    fb = np.array([0, 0, buoyancy])
+    g = -np.concatenate([fg + fb, np.cross(np.array(cob), fb)])
+    return acc6 @ M.T + cor + damp + g
+
+
+class Truth:
+    """Truth trajectory sampled at t_k = k * dt, k = 0..epochs."""
+
+    def __init__(self, epochs, dt=1e-3, speed=1.0, depth=10.0, gravity=None):
+        self.dt, self.epochs = dt, epochs
+        t = np.arange(epochs + 1) * dt
+        self.t = t
+        self.psi = 2.0 * (1.0 - np.cos(0.05 * t))
+        self.r = 0.1 * np.sin(0.05 * t)
+        vx, vy = speed * np.cos(self.psi), speed * np.sin(self.psi)
+        self.v_nav = np.stack([vx, vy, np.zeros_like(t)], -1)
+        self.a_nav = np.stack([-speed * self.r * np.sin(self.psi), speed * self.r * np.cos(self.psi),
+                               np.zeros_like(t)], -1)
+        pos = np.zeros((epochs + 1, 3))
+        pos[:, 2] = -depth
+        inc = 0.5 * (self.v_nav[1:] + self.v_nav[:-1]) * dt
+        pos[1:, :2] = np.cumsum(inc[:, :2], axis=0)
+        self.pos = pos
+        self.q = np.stack([np.cos(self.psi / 2), np.zeros_like(t), np.zeros_like(t), np.sin(self.psi / 2)], -1)
+        self.g = wgs84_gravity(LAT0, 0.0) if gravity is None else gravity
+        self.speed = speed
+        self.wv = np.array([0.08, -0.04])
+        self.wvb = np.array([0.03, 0.02])
+        self.rho = 1025.0
+        er = EARTHW * np.array([np.cos(LAT0), 0.0, np.sin(LAT0)])
+        w_nav = np.zeros((epochs + 1, 3))
+        w_nav[:, 2] = self.r
+        self.gyro = _rotz_T(self.psi, w_nav + er)
+        self.acc = _rotz_T(self.psi, self.a_nav + np.array([0, 0, self.g]))
+        self.dvl = _rotz_T(self.psi, self.v_nav)
+        self.pressure = 101325.0 - self.pos[:, 2] * self.g * self.rho
+
+    def state(self, k, dof=53, uwv=None):
+        L = abi.layout(dof)
+        x = np.zeros(L["store"])
+        x[0:3] = self.pos[k]
+        x[3:7] = self.q[k]
+        x[7:10] = self.v_nav[k]
+        x[10:13] = self.a_nav[k]
+        x[L["s_grav"]] = self.g
+        x[L["s_wv"]:L["s_wv"] + 2] = self.wv
+        x[L["s_wvb"]:L["s_wvb"] + 2] = self.wvb
+        x[L["s_rho"]] = self.rho
+        if dof == 53:
+            M, Dl, Dq = uwv_arrays(uwv or default_uwv())
+            idx = [0, 1, 5]
+            x[20:29] = M[np.ix_(idx, idx)].ravel(order="F")
+            x[29:38] = Dl[np.ix_(idx, idx)].ravel(order="F")
+            x[38:47] = Dq[np.ix_(idx, idx)].ravel(order="F")
+        return x
+
+
+MODES = ("C1", "C3", "C4")
+
+
+def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_instance=0, cfg=None):
+    """Per-instance noisy measurement log.  Returns a dict of numpy arrays.
+
+    mode C1/C3: 1 kHz IMU + 5 Hz DVL.
+    mode C4: C3 + 10 Hz pressure + 1 Hz ADCP x 4 cells (weights 0, 1/3, 2/3, 1,
+             d2p95 gate) + DVL drop-outs (30 s on / 10 s off) with 10 Hz
+             BodyEfforts updates during the drop-out.
+    """
+    cfg = cfg or default_pose_config()
+    uwv = default_uwv()
+    tr = Truth(epochs, dt)
+    k = np.arange(1, epochs + 1)  # measurement sample index (t = k dt)
+    flags = np.full(epochs, abi.EV_ACC, np.uint32)
+    t_meas = k * dt
+    dropout = np.zeros(epochs, bool)
+    if mode == "C4":
+        dropout = np.mod(t_meas, 40.0) >= 30.0 - 1e-12
+    dvl_due = (k % 200 == 0) & ~dropout
+    flags[dvl_due] |= abi.EV_DVL
+    if mode == "C4":
+        flags[k % 100 == 0] |= abi.EV_PRESSURE
+        flags[k % 1000 == 0] |= abi.EV_ADCP
+        flags[(k % 100 == 0) & dropout] |= abi.EV_EFFORTS
+
+    def idx_of(bit):
+        sel = (flags & bit) != 0
+        ix = np.full(epochs, -1, np.int32)
+        ix[sel] = np.arange(sel.sum(), dtype=np.int32)
+        return ix, k[sel]
+
+    dvl_index, dvl_k = idx_of(abi.EV_DVL)
+    p_index, p_k = idx_of(abi.EV_PRESSURE)
+    a_index, a_k = idx_of(abi.EV_ADCP)
+    e_index, e_k = idx_of(abi.EV_EFFORTS)
+
+    inst = np.arange(first_instance, first_instance + batch)
+
+    def normal(stream, shape_tail):
+        # counter-based: one Philox stream per (instance, measurement kind)
+        out = np.empty((batch,) + shape_tail)
+        for j, i in enumerate(inst):
+            g = np.random.Generator(np.random.Philox(key=[seed, int(i) * 16 + stream]))
+            out[j] = g.standard_normal(shape_tail)
+        return out
+
+    sg = 1e-4 / np.sqrt(dt)
+    sa = 1e-3 / np.sqrt(dt)
+    gyro = tr.gyro[k][None] + sg * normal(0, (epochs, 3))
+    acc = tr.acc[k][None] + sa * normal(1, (epochs, 3))
+    gyro = np.ascontiguousarray(gyro.transpose(1, 0, 2))
+    acc = np.ascontiguousarray(acc.transpose(1, 0, 2))
+    dvl = tr.dvl[dvl_k][None] + 0.01 * normal(2, (len(dvl_k), 3))
+    dvl = np.ascontiguousarray(dvl.transpose(1, 0, 2))
+    pressure = tr.pressure[p_k][None] + 100.0 * normal(3, (len(p_k),))
+    pressure = np.ascontiguousarray(pressure.T)
+    weights = np.array([0.0, 1.0 / 3.0, 2.0 / 3.0, 1.0])
+    cells = len(weights)
+    vn = tr.v_nav[a_k]
+    wv3 = np.array([tr.wv[0], tr.wv[1], 0.0])
+    wvb3 = np.array([tr.wvb[0], tr.wvb[1], 0.0])
+    rb = _rotz_T(tr.psi[a_k], vn - wvb3)[:, None, :2]
+    rw = _rotz_T(tr.psi[a_k], vn - wv3)[:, None, :2]
+    adcp_true = weights[None, :, None] * rb + (1 - weights)[None, :, None] * rw  # [n, cells, 2]
+    adcp = adcp_true[None] + 0.05 * normal(4, (len(a_k), cells, 2))
+    adcp = np.ascontiguousarray(adcp.transpose(1, 2, 0, 3))  # [n][cells][batch][2]
+    M, Dl, Dq = uwv_arrays(uwv)
+    vel6 = np.concatenate([_rotz_T(tr.psi[e_k], tr.v_nav[e_k] - wv3), np.zeros((len(e_k), 2)),
+                           tr.r[e_k][:, None]], -1)
+    acc6 = np.concatenate([_rotz_T(tr.psi[e_k], tr.a_nav[e_k]), np.zeros((len(e_k), 3))], -1)
+    tau_true = calc_efforts_np(M, Dl, Dq, acc6, vel6)
+    std = np.array(cfg.model_noise_parameters.body_efforts_std[:])
+    efforts = tau_true[None] + std * normal(5, (len(e_k), 6))
+    efforts = np.ascontiguousarray(efforts.transpose(1, 0, 2))
+
+    # initial pose estimate, perturbed per instance
+    pos_cov = np.diag([1.0, 1.0, 0.25])
+    rot_cov = np.diag([1e-4, 1e-4, 2.5e-3])
+    n0 = normal(6, (6,))
+    pos0 = tr.pos[0][None] + n0[:, :3] * np.sqrt(np.diag(pos_cov))
+    rv = n0[:, 3:] * np.sqrt(np.diag(rot_cov))
+    th = np.linalg.norm(rv, axis=1)
+    s = np.where(th > 0, np.sin(th / 2) / np.where(th > 0, th, 1), 0.5)
+    dq = np.concatenate([np.cos(th / 2)[:, None], s[:, None] * rv], 1)
+    q0 = _qmul(dq, np.broadcast_to(tr.q[0], dq.shape))
+    return dict(
+        mode=mode, dof=dof, batch=batch, epochs=epochs, dt=dt, flags=flags,
+        gyro=gyro, acc=acc, acc_cov=np.eye(3) * sa ** 2,
+        dvl_index=dvl_index, dvl=dvl, dvl_cov=np.eye(3) * 0.01 ** 2,
+        pressure_index=p_index, pressure=pressure, pressure_cov=100.0 ** 2, pressure_sensor_in_imu=np.zeros(3),
+        adcp_index=a_index, adcp=adcp, adcp_cells=cells, adcp_cell_weighting=weights, adcp_cov=np.eye(2) * 0.05 ** 2,
+        efforts_index=e_index, efforts=efforts, efforts_cov=np.diag(std ** 2),
+        pos0=pos0, pos_cov=np.broadcast_to(pos_cov, (batch, 3, 3)).copy(), rot0=q0,
+        rot_cov=np.broadcast_to(rot_cov, (batch, 3, 3)).copy(), truth=tr,
+    )
+
+
+def _qmul(a, b):
+    aw, ax, ay, az = a[..., 0], a[..., 1], a[..., 2], a[..., 3]
+    bw, bx, by, bz = b[..., 0], b[..., 1], b[..., 2], b[..., 3]
+    return np.stack([aw * bw - ax * bx - ay * by - az * bz, aw * bx + ax * bw + ay * bz - az * by,
+                     aw * by + ay * bw + az * bx - ax * bz, aw * bz + az * bw + ax * by - ay * bx], -1)
+
+
+def make_vel_log(batch, epochs, seed=SEED, dt=1e-3, first_instance=0):
+    """VelocityUKF log (config C2): 1 kHz gyro + body efforts, 5 Hz DVL, 10 Hz depth."""
+    uwv = default_uwv()
+    tr = Truth(epochs, dt)
+    k = np.arange(1, epochs + 1)
+    flags = np.zeros(epochs, np.uint32)
+    flags[k % 200 == 0] |= abi.EV_DVL
+    flags[k % 100 == 0] |= abi.EV_PRESSURE
+    dvl_index = np.full(epochs, -1, np.int32)
+    dsel = (flags & abi.EV_DVL) != 0
+    dvl_index[dsel] = np.arange(dsel.sum())
+    p_index = np.full(epochs, -1, np.int32)
+    psel = (flags & abi.EV_PRESSURE) != 0
+    p_index[psel] = np.arange(psel.sum())
+    inst = np.arange(first_instance, first_instance + batch)
+
+    def normal(stream, shape_tail):
+        out = np.empty((batch,) + shape_tail)
+        for j, i in enumerate(inst):
+            g = np.random.Generator(np.random.Philox(key=[seed + 1, int(i) * 16 + stream]))
+            out[j] = g.standard_normal(shape_tail)
+        return out
+
+    M, Dl, Dq = uwv_arrays(uwv)
+    wv3 = np.zeros(3)
+    kk = k - 1  # inputs held over [t_e, t_e+1)
+    vel6 = np.concatenate([_rotz_T(tr.psi[kk], tr.v_nav[kk] - wv3), np.zeros((epochs, 2)), tr.r[kk][:, None]], -1)
+    acc6 = np.concatenate([_rotz_T(tr.psi[kk], tr.a_nav[kk]), np.zeros((epochs, 3))], -1)
+    tau = calc_efforts_np(M, Dl, Dq, acc6, vel6)
+    w_body = np.zeros((epochs, 3))
+    w_body[:, 2] = tr.r[kk]
+    gyro = w_body[None] + 1e-3 * normal(0, (epochs, 3))
+    efforts = tau[None] + 1.0 * normal(1, (epochs, 6))
+    dvl = tr.dvl[k[dsel]][None] + 0.01 * normal(2, (int(dsel.sum()), 3))
+    depth = tr.pos[k[psel], 2][None] + 0.01 * normal(3, (int(psel.sum()),))
+    n0 = normal(4, (4,))
+    x0 = np.concatenate([np.array([1.0, 0.0, 0.0])[None] + 0.1 * n0[:, :3], (-10.0 + 0.1 * n0[:, 3])[:, None]], 1)
+    P0 = np.broadcast_to(np.diag([0.01, 0.01, 0.01, 0.01]), (batch, 4, 4)).copy()
+    return dict(batch=batch, epochs=epochs, dt=dt, flags=flags,
+                gyro=np.ascontiguousarray(gyro.transpose(1, 0, 2)),
+                efforts=np.ascontiguousarray(efforts.transpose(1, 0, 2)),
+                dvl_index=dvl_index, dvl=np.ascontiguousarray(dvl.transpose(1, 0, 2)), dvl_cov=np.eye(3) * 1e-4,
+                pressure_index=p_index, pressure=np.ascontiguousarray(depth.T), pressure_cov=1e-4,
+                x0=x0, P0=P0)

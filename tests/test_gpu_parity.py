@@ -1,0 +1,180 @@
+"""GPU parity: the HIP engine (libuwvk.so, via the C ABI) against the CPU
+oracle (oracle/liboracle.so) on identical seeded synthetic inputs.
+
+Tolerance (fp64, north_star "stated float tolerance"): mean errors in units of
+the oracle's standard deviation, covariance errors relative to
+sqrt(P_ii P_jj).  Single steps: 1e-9; multi-epoch logs: 1e-7 (summation-order
+and FMA-contraction differences accumulate through the recursion).
+"""
+import numpy as np
+import pytest
+
+from helpers import cov_err, init_both, pose_setup, state_err
+
+pytestmark = pytest.mark.gpu
+
+TOL_STEP = 1e-9
+TOL_LOG = 1e-7
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from uwvk import engine
+    if not engine.device_available(0):
+        pytest.fail("no gfx950 device / libuwvk.so not loadable: the HIP path is mandatory")
+    return engine
+
+
+@pytest.fixture(scope="module")
+def orc():
+    import oracle_ctypes
+    return oracle_ctypes
+
+
+def _pair(eng, orc, batch, dof=53, mode="C3", epochs=10):
+    cfg, uwv, log = pose_setup(batch, dof, mode, epochs)
+    o = orc.OraclePoseBatch(batch, dof)
+    g = eng.PoseUKFBatch(batch, dof)
+    init_both(o, g, cfg, uwv, log)
+    return cfg, uwv, log, o, g
+
+
+def _check(o, g, dof, tol):
+    xo, Po = o.get_state()
+    xg, Pg = g.get_state()
+    se = state_err(xg, xo, Po, dof)
+    ce = cov_err(Pg, Po)
+    assert np.all(np.isfinite(xg)) and np.all(np.isfinite(Pg))
+    assert se.max() < tol, "state error %g" % se.max()
+    assert ce.max() < tol, "covariance error %g" % ce.max()
+    return se.max(), ce.max()
+
+
+@pytest.mark.parametrize("dof", [53, 26])
+def test_init_and_predict(eng, orc, dof):
+    cfg, uwv, log, o, g = _pair(eng, orc, 6, dof)
+    _check(o, g, dof, 1e-15)
+    for f in (o, g):
+        f.set_rotation_rate(log["gyro"][0])
+        f.predict(1e-3)
+    _check(o, g, dof, TOL_STEP)
+
+
+@pytest.mark.parametrize("dof", [53, 26])
+@pytest.mark.parametrize("kind", ["acceleration", "velocity", "pressure", "water_velocity", "xy", "z",
+                                  "efforts", "efforts_vel", "geographic", "delayed_xy"])
+def test_single_update(eng, orc, dof, kind):
+    cfg, uwv, log, o, g = _pair(eng, orc, 5, dof)
+    for f in (o, g):
+        f.set_rotation_rate(log["gyro"][0])
+        f.predict(1e-3)
+    B = 5
+    x, _ = o.get_state()
+    rng = np.random.default_rng(7)
+    extra, only_vel = None, 0
+    if kind == "acceleration":
+        mu, cov = log["acc"][0], log["acc_cov"]
+    elif kind == "velocity":
+        mu, cov = x[:, 7:10] + 0.01 * rng.standard_normal((B, 3)), np.eye(3) * 1e-4
+    elif kind == "pressure":
+        mu, cov = (101325.0 + 10.0 * 9.81 * 1025 + 50 * rng.standard_normal(B))[:, None], np.array([[1e4]])
+        extra = np.array([0.1, -0.2, 0.3])
+    elif kind == "water_velocity":
+        mu, cov = 0.3 * rng.standard_normal((B, 2)), np.eye(2) * 0.05 ** 2
+        extra = np.array([0.0, 0.25, 0.5, 0.75, 1.0])
+    elif kind in ("xy", "delayed_xy"):
+        mu, cov = x[:, 0:2] + rng.standard_normal((B, 2)), np.eye(2) * 0.5
+        if kind == "delayed_xy":
+            extra = x[:, 0:2] - 0.3
+    elif kind == "z":
+        mu, cov = x[:, 2:3] + 0.1 * rng.standard_normal((B, 1)), np.array([[0.01]])
+    elif kind in ("efforts", "efforts_vel"):
+        mu, cov = 20 * rng.standard_normal((B, 6)), np.diag([25.0, 25, 25, 1, 1, 1])
+        only_vel = 1 if kind == "efforts_vel" else 0
+        kind = "efforts"
+    elif kind == "geographic":
+        from uwvk import synth
+        lat = synth.LAT0 + (x[:, 0] + rng.standard_normal(B)) / 6.39e6
+        lon = synth.LON0 - (x[:, 1] + rng.standard_normal(B)) / 3.84e6
+        mu, cov = np.stack([lat, lon], 1), np.eye(2) * 4.0
+        extra = np.array([0.5, 0.0, -0.2])
+    ao = o.update(kind, mu, cov, extra=extra, only_vel=only_vel)
+    ag = g.update(kind, mu, cov, extra=extra, only_vel=only_vel)
+    np.testing.assert_array_equal(ao, ag)
+    _check(o, g, dof, TOL_STEP)
+
+
+@pytest.mark.parametrize("dof,mode,epochs", [(53, "C3", 400), (26, "C3", 400), (53, "C4", 1000)])
+def test_run_log(eng, orc, dof, mode, epochs):
+    cfg, uwv, log, o, g = _pair(eng, orc, 4, dof, mode, epochs)
+    counts_o = o.run_log(log)
+    dlog = g.upload_log(log)
+    acc = eng.DeviceBuffer(np.zeros((4, 4), np.uint32))
+    g.run_log(dlog, accept_counts=acc)
+    counts_g = acc.read(np.uint32, (4, 4))
+    np.testing.assert_array_equal(counts_o, counts_g)
+    assert not g.get_status().any()
+    _check(o, g, dof, TOL_LOG)
+
+
+def test_velocity_ukf(eng, orc):
+    from uwvk import synth
+    B = 16
+    log = synth.make_vel_log(B, 600)
+    uwv = synth.default_uwv()
+    o = orc.OracleVelBatch(B)
+    g = eng.VelocityUKFBatch(B)
+    for f in (o, g):
+        f.init(log["x0"], log["P0"])
+        f.set_gyro(log["gyro"][0])
+        f.setup_motion_model(uwv)
+    o.run_log(log)
+    g.run_log(g.upload_log(log))
+    xo, Po, mo = o.get_state(model=True)
+    xg, Pg, mg = g.get_state(model=True)
+    sd = np.sqrt(np.diagonal(Po, axis1=1, axis2=2))
+    assert np.max(np.abs(xg - xo) / sd) < TOL_LOG
+    assert cov_err(Pg, Po).max() < TOL_LOG
+    assert np.max(np.abs(mg - mo)) < 1e-9
+
+
+def test_velocity_ukf_api(eng, orc):
+    from uwvk import synth
+    B = 8
+    log = synth.make_vel_log(B, 10)
+    uwv = synth.default_uwv()
+    o = orc.OracleVelBatch(B)
+    g = eng.VelocityUKFBatch(B)
+    for f in (o, g):
+        f.init(log["x0"], log["P0"])
+    with pytest.raises(eng.UWVKError):
+        g.predict(1e-3)  # VelocityUKF.cpp:117-118: no motion model -> error
+    for f in (o, g):
+        f.setup_motion_model(uwv)
+        f.set_gyro(log["gyro"][0])
+        f.set_efforts(log["efforts"][0])
+        f.predict(1e-3)
+        f.update_dvl(np.array([[1.0, 0.02, -0.01]] * B), log["dvl_cov"])
+        f.update_pressure(np.full(B, -10.02), log["pressure_cov"])
+    xo, Po = o.get_state()
+    xg, Pg = g.get_state()
+    sd = np.sqrt(np.diagonal(Po, axis1=1, axis2=2))
+    assert np.max(np.abs(xg - xo) / sd) < TOL_STEP
+    assert cov_err(Pg, Po).max() < TOL_STEP
+
+
+def test_nan_measurement_rejected(eng):
+    from uwvk import synth
+    cfg, uwv, log = pose_setup(3)
+    g = eng.PoseUKFBatch(3)
+    g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    g.set_process_noise_from_config(cfg, 1e-3)
+    x0, P0 = g.get_state()
+    bad = log["acc"][0].copy()
+    bad[1, 2] = np.nan
+    with pytest.raises(eng.UWVKError) as e:
+        g.update("acceleration", bad, log["acc_cov"])
+    assert e.value.code == 2
+    x1, P1 = g.get_state()
+    np.testing.assert_array_equal(x0, x1)
+    np.testing.assert_array_equal(P0, P1)
