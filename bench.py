@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""bench.py — batched PoseUKF predict+update throughput on MI355X.
+
+Metric (BASELINE.json): UKF predict+update steps/sec at batch = 65536 PoseUKF
+instances (config C3: full 53-DOF PoseState, 1 kHz IMU + 5 Hz DVL).
+One "step" = one IMU epoch of ONE filter instance: RotationRate store ->
+predictionStep(1 ms) -> Acceleration update, plus the DVL velocity update
+when the 5 Hz schedule is due.  `value` counts
+instance-epochs per second over the whole job (all ranks).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+instances are sharded across ranks (weak scaling: --batch-per-gpu instances on
+every GPU, no data-path collective); the only collective is the RCCL
+all-reduce of the ensemble statistics at the end of the timed region.
+
+Inputs are synthetic (uwvk.synth) and resident in HBM before timing starts.
+Timing: barrier + device sync on both sides of the timed region, max over
+ranks; the dominant kernel's average launch time comes from HIP events on the
+handle's stream.  cpu_baseline: the fp64 C oracle (oracle/, "port") on a
+bounded sample of the same workload, on rank 0 at N = 1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+
+METRIC = "UKF predict+update steps/sec at batch=65536 PoseUKF instances, 1 & 8 GPU"
+# frozen algorithmic work per step: n = 53, N = 107
+F_PRED = 700_377
+F_UPD3 = 853_707
+F_STEP = F_PRED + F_UPD3  # 1,554,084 flop: predict + Acceleration update (m = 3)
+B_STEP = 45_808           # fp64 mu + Sigma read + write
+PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector = matrix) spec; probe measured 74 (profiles/r01_probe_fp64.txt)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200, help="timed epochs")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch-per-gpu", type=int, default=65536)
+    ap.add_argument("--dof", type=int, default=53)
+    ap.add_argument("--mode", default="C3", choices=["C3", "C4"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    return ap.parse_args()
+
+
+def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance):
+    """Log of warmup+steps epochs whose 5 Hz DVL schedule puts at least one DVL
+    epoch inside the timed window (exactly the 1-in-200 rate when steps >= 200)."""
+    total = warmup + steps
+    # shift the start so that a DVL epoch (k % 200 == 0) lands mid-window
+    target = warmup + min(steps, 200) // 2
+    shift = (200 - (target + 1) % 200) % 200
+    log = synth.make_pose_log(batch, total + shift, mode=mode, dof=dof, first_instance=first_instance)
+    return log, shift
+
+
+def roofline_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(workload)
+        return None if e is None else float(e["bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def cpu_baseline(synth, cfg, uwv, mode, dof, threads):
+    """fp64 C oracle on a bounded sample of the same workload (host cores)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ctypes as O
+    batch, epochs = 16 * threads, 200
+    log = synth.make_pose_log(batch, epochs, mode=mode, dof=dof)
+    o = O.OraclePoseBatch(batch, dof)
+    o.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    o.set_process_noise_from_config(cfg, log["dt"])
+    t0 = time.perf_counter()
+    o.run_log(log, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": batch * epochs / dt, "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": "%d PoseUKF instances x %d epochs (%s, incl. %d DVL updates each), %d pthreads, %.2f s wall"
+                      % (batch, epochs, mode, int(((log["flags"] & 2) != 0).sum()), threads, dt)}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from uwvk import engine, synth
+
+    B = a.batch_per_gpu
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, a.mode, a.dof, first_instance=rank * B)
+    f = engine.PoseUKFBatch(B, a.dof, device=local)
+    f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    f.set_process_noise_from_config(cfg, log["dt"])
+    dlog = f.upload_log(log)
+    flags = log["flags"]
+    # advance through the alignment shift (untimed)
+    if shift:
+        f.run_log(dlog, 0, shift)
+    f.run_log(dlog, shift, a.warmup)  # warmup (untimed)
+    e0 = shift + a.warmup
+    window = flags[e0:e0 + a.steps]
+    n_dvl = int(((window & 2) != 0).sum())
+    truth = log["truth"].state(e0 + a.steps, a.dof)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    f.synchronize()
+    t0 = time.perf_counter()
+    f.timer_start()
+    f.run_log(dlog, e0, a.steps, sync=False)
+    kernel_ms = f.timer_stop()  # HIP events on the handle's stream around the epoch launches
+    stats = f.ensemble_stats(truth)  # synchronous
+    if dist is not None:
+        import torch
+        t = torch.from_numpy(stats).cuda()
+        dist.all_reduce(t)  # RCCL over xGMI: the only collective of the workload
+        stats = t.cpu().numpy()
+    f.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        w = torch.tensor([wall], dtype=torch.float64).cuda()
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w.item())
+    status = f.get_status()
+    if status.any():
+        print("warning: %d instances flagged (status bits)" % int((status != 0).sum()), file=sys.stderr)
+
+    steps_total = B * world * a.steps
+    value = steps_total / wall
+    per_launch_ms = kernel_ms / a.steps
+    flops_launch = B * (F_STEP * a.steps + F_UPD3 * n_dvl) / a.steps
+    achieved_tf = flops_launch / (per_launch_ms * 1e-3) / 1e12
+    workload = "C3-dof%d-b%d" % (a.dof, B) if a.mode == "C3" else "%s-dof%d-b%d" % (a.mode, a.dof, B)
+    traffic = roofline_traffic(workload)
+    out = {
+        "metric": METRIC, "value": value, "unit": "steps/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "%s: PoseUKF %d-DOF, batch %d per GPU, 1 kHz IMU + 5 Hz DVL%s"
+                               % (a.mode, a.dof, B, " + ADCP x4 + DVL drop-out/efforts + pressure"
+                                  if a.mode == "C4" else ""),
+                   "global_batch": B * world, "batch_per_gpu": B, "step": "one IMU epoch per instance",
+                   "dvl_epochs_in_window": n_dvl, "parallelism": "instance-sharded x%d (no data-path collective)"
+                                                                  % world,
+                   "kernel": "k_pose_epoch<%d>" % a.dof},
+        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": traffic,
+                     "kernel_ms_per_launch": per_launch_ms,
+                     "algorithmic_flop_per_launch": flops_launch,
+                     "hbm_frac_algorithmic": (B * B_STEP / (per_launch_ms * 1e-3)) / (PEAK_HBM_GBS * 1e9)},
+        "ensemble": {"nees_mean_pos_ori_vel": float(stats[-1] / (B * world))},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(synth, cfg, uwv, a.mode, a.dof, threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
