@@ -314,6 +314,14 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
  * truth: host store-vector (nullable -> zeros).  out: host doubles, 3*store+1. */
 uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* out);
 
+/* Engine options (not part of the reference surface).
+ * UWVK_OPT_LITERAL_APPLY_DELTA: 0 (default) applies ukfom's apply_delta through
+ *   its exact nav-frame identity mu <- mu [+] d, Sigma <- T Sigma T^T
+ *   (T rotates the orientation block by exp(d)); 1 runs the literal re-spread
+ *   (Cholesky + sigma points + covariance GEMM).  Results agree to rounding. */
+#define UWVK_OPT_LITERAL_APPLY_DELTA 1
+uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
+
 /* Kernel-timing helper: HIP events recorded on the handle's stream. */
 uwvk_status uwvk_pose_timer_start(uwvk_pose* h);
 uwvk_status uwvk_pose_timer_stop(uwvk_pose* h, float* elapsed_ms);

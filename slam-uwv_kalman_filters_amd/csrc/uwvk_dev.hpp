@@ -150,4 +150,41 @@ typedef double d4_t __attribute__((ext_vector_type(4)));
 
 UWVK_DEV d4_t mfma_f64(double a, double b, d4_t c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
 
+// ---------------------------------------------------------------------------
+// Diagnostic phase stamps (build with -DUWVK_STAMPS; never in the product .so).
+// Thread 0 of each workgroup adds the s_memtime delta since its previous stamp
+// to a per-phase sum; read back with uwvk_debug_read_stamps().
+// ---------------------------------------------------------------------------
+#ifdef UWVK_STAMPS
+static __device__ unsigned long long uwvk_stamp_sum[64];  // per translation unit
+static __device__ unsigned long long uwvk_stamp_cnt[64];
+UWVK_DEV unsigned long long stamp_now() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+struct Stamper {
+  unsigned long long last;
+  UWVK_DEV Stamper() : last(stamp_now()) {}
+  UWVK_DEV void mark(int ph) {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t = stamp_now();
+    __builtin_amdgcn_sched_barrier(0);
+    if (threadIdx.x == 0) {
+      atomicAdd(&uwvk_stamp_sum[ph], t - last);
+      atomicAdd(&uwvk_stamp_cnt[ph], 1ull);
+    }
+    last = t;
+  }
+};
+#else
+struct Stamper {
+  UWVK_DEV void mark(int) {}
+};
+#endif
+#define UWVK_STAMP(ph) \
+  do {                 \
+    if (st) st->mark(ph); \
+  } while (0)
+
 }  // namespace uwvk

@@ -398,6 +398,15 @@ uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* 
   return UWVK_OK;
 }
 
+uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
+  if (!h) return UWVK_EINVAL;
+  if (option == UWVK_OPT_LITERAL_APPLY_DELTA) {
+    h->sh.literal_apply_delta = value ? 1 : 0;
+    return UWVK_OK;
+  }
+  return UWVK_EINVAL;
+}
+
 uwvk_status uwvk_pose_timer_start(uwvk_pose* h) {
   if (!h) return UWVK_EINVAL;
   HIPCHK(hipEventRecord(h->ev0, h->stream));

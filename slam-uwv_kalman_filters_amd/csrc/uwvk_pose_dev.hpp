@@ -30,6 +30,7 @@ struct PoseShared {
   uwvk_pose_parameter p;
   double lat0, lon0, rm, rn_cos, inv_rm;  // GeographicProjection [EXT]: lat = lat0 + x/rm, lon = lon0 - y/rn_cos
   double uwv_weight, uwv_buoyancy, cog[3], cob[3];
+  int literal_apply_delta;  // 1: ukfom's literal re-spread (Cholesky + GEMM); 0: exact T Sigma T^T form
 };
 
 struct PoseBufs {
@@ -64,19 +65,29 @@ struct Geo {
   static constexpr int RROWS = 16 * NW;                // rows after folding each wave 64 -> 16
   static constexpr int A = DOF * DOF, B = 32 * STR, C = RROWS * RS;
   static constexpr int SZ = (A > B ? (A > C ? A : C) : (B > C ? B : C));
-  static constexpr int LP = DOF * (DOF + 1) / 2, LC = 16 * (DOF | 1);
-  static constexpr int LPSZ = LP > LC ? LP : LC;       // packed L / update staging
+  static constexpr int LP = DOF * (DOF + 1) / 2;
+  static constexpr int LC = 16 * (DOF | 1) + 16 * 8;   // update staging: dx rows + dz rows
+  static constexpr int LK = DOF * 6;                   // Kalman gain rows
+  static constexpr int LPSZ = LP > LC ? (LP > LK ? LP : LK) : (LC > LK ? LC : LK);  // packed L / staging / K
   static_assert(N <= T, "one sigma point per thread");
 };
 
 template <int NT>
+struct TileIJ;
+// compile-time (i, j) of upper tile TT (template constants: always folded)
+template <int NT, int TT>
+struct TileAt {
+  static constexpr int i = TileIJ<NT>::i(TT);
+  static constexpr int j = TileIJ<NT>::j(TT);
+};
+template <int NT>
 struct TileIJ {  // t -> (i, j) over the upper tiles, row-major
-  UWVK_DEV static constexpr int i(int t) {
+  __host__ __device__ static constexpr int i(int t) {
     int r = 0, k = t;
     while (k >= NT - r) { k -= NT - r; r++; }
     return r;
   }
-  UWVK_DEV static constexpr int j(int t) {
+  __host__ __device__ static constexpr int j(int t) {
     int r = 0, k = t;
     while (k >= NT - r) { k -= NT - r; r++; }
     return r + k;
@@ -91,14 +102,13 @@ struct alignas(16) Smem {
   double ref[56];          // scratch state (X0 / mean under construction)
   double col[2][64];       // Cholesky column broadcast (double-buffered)
   double vec[64];          // broadcast vectors (sums, delta)
-  double red[4][32];       // cross-wave partial sums
-  double kb[DOF * 6];      // Kalman gain rows
-  double dz[32 * 8];       // staged measurement deviations
+  double red[2][24];       // cross-wave partial sums
   double qori[9];          // R Q_ori R^T for the predict
 };
 
 UWVK_DEV int tid() { return threadIdx.x; }
-UWVK_DEV int wid() { return threadIdx.x >> 6; }
+// wave index as a scalar (SGPR): branches on it are uniform (s_cbranch_scc)
+UWVK_DEV int wid() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 // intra-wavefront ordering point for LDS exchanges done by one wave
 UWVK_DEV void wave_sync() {
@@ -114,7 +124,7 @@ UWVK_DEV void block_sum(Smem<DOF>& sm, double (&v)[K]) {
 #pragma unroll
   for (int k = 0; k < K; k++) v[k] = wave_sum(v[k]);
   if constexpr (NW > 1) {
-    static_assert(K <= 32, "block_sum width");
+    static_assert(K <= 24 && NW <= 2, "block_sum width");
     if (lane_id() == 0) {
 #pragma unroll
       for (int k = 0; k < K; k++) sm.red[wid()][k] = v[k];
@@ -135,16 +145,27 @@ UWVK_DEV void block_sum(Smem<DOF>& sm, double (&v)[K]) {
 // Cholesky of S into the packed factor sm.Lp by wavefront 0 (S is kept).  Returns false (uniform) if a
 // pivot is not > 0.
 // ---------------------------------------------------------------------------
-// one right-looking column step; template recursion keeps every register index
-// a compile-time constant (a runtime-indexed row would live in scratch)
+// 1/sqrt(x): hardware v_rsq_f64 seed + one third-order correction
+// (e = 1 - x r^2; r += r e (1/2 + 3/8 e)), full fp64 precision.
+UWVK_DEV double rsqrt_f64(double x) {
+  double r = __builtin_amdgcn_rsq(x);
+  const double e = fma(-(x * r), r, 1.0);
+  return fma(r * e, fma(0.375, e, 0.5), r);
+}
+
+// One right-looking column step; template recursion keeps every register index
+// a compile-time constant (a runtime-indexed row would live in scratch).
+// piv is the final value of A[K][K].  The next pivot comes from lane K+1's own
+// registers (L[K+1][K]^2), so the LDS column broadcast is off the critical path.
 template <int DOF, int K>
-UWVK_DEV void chol_step(double (&a)[DOF], Smem<DOF>& sm, int r, bool& ok) {
+UWVK_DEV void chol_step(double (&a)[DOF], Smem<DOF>& sm, int r, bool& ok, double piv) {
   if constexpr (K < DOF) {
-    const double akk = readlane_d(a[K], K);
-    ok = ok && (akk > 0.0);
-    const double d = sqrt(akk);
-    const double inv = 1.0 / d;
+    ok = ok && (piv > 0.0);
+    const double inv = rsqrt_f64(piv);
+    const double d = piv * inv;
     a[K] = (r == K) ? d : a[K] * inv;
+    double pnext = 0.0;
+    if constexpr (K + 1 < DOF) pnext = readlane_d(a[K + 1] - a[K] * a[K], K + 1);
     sm.col[K & 1][r] = a[K];
     wave_sync();
 #pragma unroll
@@ -153,7 +174,7 @@ UWVK_DEV void chol_step(double (&a)[DOF], Smem<DOF>& sm, int r, bool& ok) {
     // update to its first use and keeps O(n^2) column values live (spills)
 #pragma unroll
     for (int c = K + 1; c < DOF; c++) asm volatile("" : "+v"(a[c]));
-    chol_step<DOF, K + 1>(a, sm, r, ok);
+    chol_step<DOF, K + 1>(a, sm, r, ok, pnext);
   }
 }
 
@@ -161,11 +182,12 @@ template <int DOF>
 UWVK_DEV bool chol_lds(Smem<DOF>& sm) {
   if (wid() == 0) {
     const int r = lane_id();
+    const int rr = r < DOF ? r : DOF - 1;  // lanes >= DOF shadow the last row (discarded)
     double a[DOF];
 #pragma unroll
-    for (int c = 0; c < DOF; c++) a[c] = (r < DOF) ? sm.S[r * DOF + c] : 0.0;
+    for (int c = 0; c < DOF; c++) a[c] = sm.S[rr * DOF + c];
     bool ok = true;
-    chol_step<DOF, 0>(a, sm, r, ok);
+    chol_step<DOF, 0>(a, sm, r, ok, readlane_d(a[0], 0));
     if (r < DOF) {
       const int base = r * (r + 1) / 2;
 #pragma unroll
@@ -268,67 +290,89 @@ UWVK_DEV void lane_sum_vec(Smem<DOF>& sm, double (&v)[DOF]) {
 // Sigma = 0.5 * D D^T over the per-thread deviations d (point = thread), via
 // v_mfma_f64_16x16x4_f64.  Upper tile t is owned by wave t % NW.
 // ---------------------------------------------------------------------------
-template <int DOF>
-UWVK_DEV void cov_gemm(Smem<DOF>& sm, const double (&d)[DOF], d4_t (&acc)[Geo<DOF>::TPW]) {
+// MFMAs of wave W's tiles U, U+1, ... for one k-step (fragments f)
+template <int DOF, int W, int U>
+UWVK_DEV void mfma_tiles(const double (&f)[Geo<DOF>::NT], d4_t (&acc)[Geo<DOF>::TPW]) {
   using G = Geo<DOF>;
-  const int l = lane_id(), w = wid(), t = tid();
+  constexpr int TT = W + G::NW * U;
+  if constexpr (U < G::TPW && TT < G::NTILE) {
+    acc[U] = mfma_f64(f[TileAt<G::NT, TT>::i], f[TileAt<G::NT, TT>::j], acc[U]);
+    mfma_tiles<DOF, W, U + 1>(f, acc);
+  }
+}
+
+// one staged chunk of KS k-steps for wave W: straight-line, static tile list
+template <int DOF, int W, int KS>
+UWVK_DEV void gemm_chunk(const Smem<DOF>& sm, d4_t (&acc)[Geo<DOF>::TPW]) {
+  using G = Geo<DOF>;
+  const int l = lane_id();
+  double f[KS][G::NT];
 #pragma unroll
-  for (int u = 0; u < G::TPW; u++) acc[u] = d4_t{0.0, 0.0, 0.0, 0.0};
+  for (int s = 0; s < KS; s++)
 #pragma unroll
-  for (int c = 0; c < G::NCHUNK; c++) {
-    if ((t >> 5) == c) {  // threads 32c .. 32c+31 stage their points
+    for (int i = 0; i < G::NT; i++) f[s][i] = sm.S[(4 * s + (l >> 4)) * G::STR + 16 * i + (l & 15)];
+#pragma unroll
+  for (int s = 0; s < KS; s++) mfma_tiles<DOF, W, 0>(f[s], acc);
+}
+
+// chunk C of 32 points: stage (threads 32C..32C+31), barrier, MFMAs, barrier
+template <int DOF, int C>
+UWVK_DEV void gemm_chunks(Smem<DOF>& sm, const double (&d)[DOF], d4_t (&acc)[Geo<DOF>::TPW]) {
+  using G = Geo<DOF>;
+  if constexpr (C < G::NCHUNK) {
+    const int t = tid(), w = wid();
+    if ((t >> 5) == C) {
       const int row = t & 31;
       const bool valid = t < G::N;
 #pragma unroll
       for (int k = 0; k < 16 * G::NT; k++) sm.S[row * G::STR + k] = (k < DOF && valid) ? d[k] : 0.0;
     }
     __syncthreads();
-    const int npts = (G::N - 32 * c) < 32 ? (G::N - 32 * c) : 32;
-    const int ks = (npts + 3) / 4;
-#pragma unroll
-    for (int s = 0; s < 8; s++) {
-      if (s < ks) {
-        double f[G::NT];
-#pragma unroll
-        for (int i = 0; i < G::NT; i++) f[i] = sm.S[(4 * s + (l >> 4)) * G::STR + 16 * i + (l & 15)];
-#pragma unroll
-        for (int u = 0; u < G::TPW; u++) {
-#pragma unroll
-          for (int ww = 0; ww < G::NW; ww++) {
-            const int tt = ww + G::NW * u;
-            if (tt < G::NTILE && ww == w)
-              acc[u] = mfma_f64(f[TileIJ<G::NT>::i(tt)], f[TileIJ<G::NT>::j(tt)], acc[u]);
-          }
-        }
-      }
+    constexpr int NP = (G::N - 32 * C) < 32 ? (G::N - 32 * C) : 32;
+    constexpr int KS = (NP + 3) / 4;
+    if (w == 0) gemm_chunk<DOF, 0, KS>(sm, acc);
+    if constexpr (G::NW > 1) {
+      if (w == 1) gemm_chunk<DOF, 1, KS>(sm, acc);
     }
     __syncthreads();
+    gemm_chunks<DOF, C + 1>(sm, d, acc);
+  }
+}
+
+template <int DOF>
+UWVK_DEV void cov_gemm(Smem<DOF>& sm, const double (&d)[DOF], d4_t (&acc)[Geo<DOF>::TPW]) {
+#pragma unroll
+  for (int u = 0; u < Geo<DOF>::TPW; u++) acc[u] = d4_t{0.0, 0.0, 0.0, 0.0};
+  gemm_chunks<DOF, 0>(sm, d, acc);
+}
+
+template <int DOF, int W, int U, class QF>
+UWVK_DEV void store_tiles(Smem<DOF>& sm, const d4_t (&acc)[Geo<DOF>::TPW], QF& qfun) {
+  using G = Geo<DOF>;
+  constexpr int TT = W + G::NW * U;
+  if constexpr (U < G::TPW && TT < G::NTILE) {
+    constexpr int i = TileAt<G::NT, TT>::i, j = TileAt<G::NT, TT>::j;
+    const int l = lane_id();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int r = 16 * i + (l >> 4) + 4 * q, c = 16 * j + (l & 15);
+      if (r < DOF && c < DOF) {
+        const double v = 0.5 * acc[U][q] + qfun(r, c);
+        sm.S[r * DOF + c] = v;
+        if (i != j) sm.S[c * DOF + r] = v;
+      }
+    }
+    store_tiles<DOF, W, U + 1>(sm, acc, qfun);
   }
 }
 
 // write 0.5*acc + qfun(r, c) into sm.S (full symmetric)
 template <int DOF, class QF>
 UWVK_DEV void store_cov(Smem<DOF>& sm, const d4_t (&acc)[Geo<DOF>::TPW], QF qfun) {
-  using G = Geo<DOF>;
-  const int l = lane_id(), w = wid();
-#pragma unroll
-  for (int u = 0; u < G::TPW; u++) {
-#pragma unroll
-    for (int ww = 0; ww < G::NW; ww++) {
-      const int tt = ww + G::NW * u;
-      if (tt < G::NTILE && ww == w) {
-        const int i = TileIJ<G::NT>::i(tt), j = TileIJ<G::NT>::j(tt);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int r = 16 * i + (l >> 4) + 4 * q, c = 16 * j + (l & 15);
-          if (r < DOF && c < DOF) {
-            const double v = 0.5 * acc[u][q] + qfun(r, c);
-            sm.S[r * DOF + c] = v;
-            if (i != j) sm.S[c * DOF + r] = v;
-          }
-        }
-      }
-    }
+  const int w = wid();
+  if (w == 0) store_tiles<DOF, 0, 0>(sm, acc, qfun);
+  if constexpr (Geo<DOF>::NW > 1) {
+    if (w == 1) store_tiles<DOF, 1, 0>(sm, acc, qfun);
   }
   __syncthreads();
 }
@@ -401,7 +445,8 @@ UWVK_DEV void process_point(double x[Lay<DOF>::store], const PoseShared& sh, con
 // predictionStepImpl (PoseUKF.cpp:446-465) + ukf::predict [EXT]
 // ---------------------------------------------------------------------------
 template <int DOF>
-UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q) {
+UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q,
+                           Stamper* st = nullptr) {
   using L = Lay<DOF>;
   using G = Geo<DOF>;
   const int t = tid();
@@ -427,6 +472,7 @@ UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& p
   const double dt2 = dt * dt;
   // --- sigma points through the process model
   const bool ok = chol_lds<DOF>(sm);
+  UWVK_STAMP(0);
   double x[L::store];
   gen_point<DOF>(sm, t, x);
   process_point<DOF>(x, sh, pc);
@@ -436,6 +482,7 @@ UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& p
     for (int s = 0; s < L::store; s++) sm.ref[s] = x[s];
   }
   __syncthreads();  // L dead from here on; ref visible
+  UWVK_STAMP(1);
   // --- manifold mean (Gauss-Newton, |delta| <= 1e-6, max 1e4 iterations)
   double nrm2 = 0.0;
   double dori[3];
@@ -487,6 +534,7 @@ UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& p
   __syncthreads();
   if (t < 4) sm.ref[3 + t] = mq[t];
   __syncthreads();
+  UWVK_STAMP(2);
   // --- deviations and covariance reconstruction
   d4_t acc[G::TPW];
   {
@@ -504,6 +552,7 @@ UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& p
   store_cov<DOF>(sm, acc, qf);
   if (t < L::store) sm.mu[t] = sm.ref[t];
   __syncthreads();
+  UWVK_STAMP(3);
   return ok;
 }
 
@@ -580,10 +629,11 @@ UWVK_DEV void small_inv(const double* A, double* X) {
 // delta (tangent) is in sm.vec.
 // ---------------------------------------------------------------------------
 template <int DOF>
-UWVK_DEV bool apply_delta(Smem<DOF>& sm) {
+UWVK_DEV bool apply_delta_literal(Smem<DOF>& sm, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   const int t = tid();
   const bool ok = chol_lds<DOF>(sm);
+  UWVK_STAMP(8);
   double x[L::store];
   gen_point<DOF>(sm, t, x);
   boxplus_vec<DOF>(x, sm.vec);
@@ -596,6 +646,7 @@ UWVK_DEV bool apply_delta(Smem<DOF>& sm) {
     for (int s = 0; s < L::store; s++) sm.ref[s] = m[s];
   }
   __syncthreads();
+  UWVK_STAMP(9);
   d4_t acc[Geo<DOF>::TPW];
   {
     double d[DOF];
@@ -605,7 +656,59 @@ UWVK_DEV bool apply_delta(Smem<DOF>& sm) {
   store_cov<DOF>(sm, acc, [](int, int) { return 0.0; });
   if (t < L::store) sm.mu[t] = sm.ref[t];
   __syncthreads();
+  UWVK_STAMP(10);
   return ok;
+}
+
+// ---------------------------------------------------------------------------
+// apply_delta, exact nav-frame form.  With X_p = mu [+] +-L_j and the left
+// SO3 boxplus, (X_p [+] d) [-] (mu [+] d) = T (+-L_j) exactly, T = blockdiag(I,
+// R(exp(d_ori)), I): the re-spread covariance of ukfom's apply_delta equals
+// T (L L^T) T^T = T Sigma T^T.  So: mu <- mu [+] d, Sigma <- T Sigma T^T
+// (O(n) work instead of a Cholesky + sigma spread + GEMM).  Differences to the
+// literal form are rounding only; apply_delta_literal keeps the literal path.
+// ---------------------------------------------------------------------------
+template <int DOF>
+UWVK_DEV bool apply_delta_rot(Smem<DOF>& sm, Stamper* st = nullptr) {
+  using L = Lay<DOF>;
+  const int t = tid();
+  double R[9];
+  {
+    const double dv[3] = {sm.vec[3], sm.vec[4], sm.vec[5]};
+    double e[4];
+    so3_exp(dv, e);
+    qmatrix(e, R);
+  }
+  // Sigma T^T: columns 3..5 of every row
+  if (t < DOF) {
+    const double s0 = sm.S[t * DOF + 3], s1 = sm.S[t * DOF + 4], s2 = sm.S[t * DOF + 5];
+#pragma unroll
+    for (int i = 0; i < 3; i++) sm.S[t * DOF + 3 + i] = R[i * 3] * s0 + R[i * 3 + 1] * s1 + R[i * 3 + 2] * s2;
+  }
+  __syncthreads();
+  // T (Sigma T^T): rows 3..5 of every column
+  if (t < DOF) {
+    const double s0 = sm.S[3 * DOF + t], s1 = sm.S[4 * DOF + t], s2 = sm.S[5 * DOF + t];
+#pragma unroll
+    for (int i = 0; i < 3; i++) sm.S[(3 + i) * DOF + t] = R[i * 3] * s0 + R[i * 3 + 1] * s1 + R[i * 3 + 2] * s2;
+  }
+  if (t == 0) {
+    double m[L::store];
+#pragma unroll
+    for (int s = 0; s < L::store; s++) m[s] = sm.mu[s];
+    boxplus_vec<DOF>(m, sm.vec);
+#pragma unroll
+    for (int s = 0; s < L::store; s++) sm.mu[s] = m[s];
+  }
+  __syncthreads();
+  UWVK_STAMP(10);
+  return true;
+}
+
+template <int DOF>
+UWVK_DEV bool apply_delta(Smem<DOF>& sm, bool literal, Stamper* st = nullptr) {
+  if (literal) return apply_delta_literal<DOF>(sm, st);
+  return apply_delta_rot<DOF>(sm, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -617,12 +720,13 @@ UWVK_DEV bool apply_delta(Smem<DOF>& sm) {
 // ---------------------------------------------------------------------------
 template <int DOF, int M, class H>
 UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)[M * M], int zmode, int gate, H h,
-                          bool* ok) {
+                          bool* ok, Stamper* st = nullptr, bool literal = false) {
   using L = Lay<DOF>;
   using G = Geo<DOF>;
   const int t = tid();
   const bool mine = t < G::N;
   const bool cok = chol_lds<DOF>(sm);
+  UWVK_STAMP(4);
   double x[L::store];
   gen_point<DOF>(sm, t, x);
   __syncthreads();  // L dead from here on
@@ -684,6 +788,7 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
         S[b * M + a] = s + R[b * M + a];
       }
   }
+  UWVK_STAMP(5);
   // cross covariance C = 1/2 sum dx dz^T; thread r (< DOF) accumulates row r.
   // dx is staged through the (dead) Cholesky-factor region in 16-point chunks;
   // Sigma in sm.S stays intact for the covariance update below.
@@ -701,7 +806,7 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
 #pragma unroll
         for (int k = 0; k < DOF; k++) sm.Lp[row * CS + k] = mine ? dx[k] : 0.0;
 #pragma unroll
-        for (int a = 0; a < M; a++) sm.dz[row * 8 + a] = dz[a];
+        for (int a = 0; a < M; a++) sm.Lp[16 * CS + row * 8 + a] = dz[a];
       }
       __syncthreads();
       const int npts = (G::N - 16 * c) < 16 ? (G::N - 16 * c) : 16;
@@ -709,7 +814,7 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
         for (int q = 0; q < npts; q++) {
           const double v = sm.Lp[q * CS + t];
 #pragma unroll
-          for (int a = 0; a < M; a++) C[a] += v * sm.dz[q * 8 + a];
+          for (int a = 0; a < M; a++) C[a] += v * sm.Lp[16 * CS + q * 8 + a];
         }
       }
       __syncthreads();
@@ -717,6 +822,7 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
   }
 #pragma unroll
   for (int a = 0; a < M; a++) C[a] = 0.5 * C[a];
+  UWVK_STAMP(6);
   small_inv<M>(S, Si);
   double K[M];
 #pragma unroll
@@ -745,14 +851,14 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
   // Sigma -= C K^T ; delta = K nu
   if (t < DOF) {
 #pragma unroll
-    for (int a = 0; a < M; a++) sm.kb[t * M + a] = K[a];
+    for (int a = 0; a < M; a++) sm.Lp[t * M + a] = K[a];  // K rows (the factor is dead)
   }
   __syncthreads();
   if (t < DOF) {
     for (int c = 0; c < DOF; c++) {
       double s = 0.0;
 #pragma unroll
-      for (int a = 0; a < M; a++) s += C[a] * sm.kb[c * M + a];
+      for (int a = 0; a < M; a++) s += C[a] * sm.Lp[c * M + a];
       sm.S[t * DOF + c] -= s;
     }
     double dl = 0.0;
@@ -761,7 +867,8 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
     sm.vec[t] = dl;
   }
   __syncthreads();
-  const bool aok = apply_delta<DOF>(sm);
+  UWVK_STAMP(7);
+  const bool aok = apply_delta<DOF>(sm, literal, st);
   *ok = cok && aok;
   return true;
 }

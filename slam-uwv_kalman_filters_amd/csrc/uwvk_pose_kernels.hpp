@@ -62,9 +62,21 @@ hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const d
 template <int DOF>
 UWVK_DEV void load_instance(Smem<DOF>& sm, const PoseBufs& b, int64_t i) {
   const int l = tid();
+  constexpr int T = Geo<DOF>::T, NL = (DOF * DOF + T - 1) / T;
   const double* gs = b.sigma + i * (int64_t)(DOF * DOF);
-  for (int k = l; k < DOF * DOF; k += Geo<DOF>::T) sm.S[k] = gs[k];
-  if (l < Lay<DOF>::store) sm.mu[l] = b.mu[i * Lay<DOF>::store + l];
+  double v[NL];
+#pragma unroll
+  for (int u = 0; u < NL; u++) {  // all loads in flight before the first LDS store
+    const int k = l + u * T;
+    v[u] = (k < DOF * DOF) ? gs[k] : 0.0;
+  }
+  const double m = (l < Lay<DOF>::store) ? b.mu[i * Lay<DOF>::store + l] : 0.0;
+#pragma unroll
+  for (int u = 0; u < NL; u++) {
+    const int k = l + u * T;
+    if (k < DOF * DOF) sm.S[k] = v[u];
+  }
+  if (l < Lay<DOF>::store) sm.mu[l] = m;
   __syncthreads();
 }
 
@@ -85,29 +97,29 @@ UWVK_DEV bool all_finite(const double* a, int n) {
 // one measurement update of kind K on instance i (Sigma in LDS)
 template <int DOF, int K>
 UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, int64_t i, const double* zin,
-                        const double* Rin, const MeasArgs& ma, double wrot[3], bool* ok) {
+                        const double* Rin, const MeasArgs& ma, double wrot[3], bool* ok, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   if constexpr (K == MK_ACC) {
     double z[3], R[9];
     for (int k = 0; k < 3; k++) z[k] = zin[k];
     for (int k = 0; k < 9; k++) R[k] = Rin[k];
-    return pose_update<DOF, 3>(sm, z, R, 1, 0, HAcc<DOF>{}, ok);
+    return pose_update<DOF, 3>(sm, z, R, 1, 0, HAcc<DOF>{}, ok, st, sh.literal_apply_delta != 0);
   } else if constexpr (K == MK_VEL) {
     double z[3], R[9];
     for (int k = 0; k < 3; k++) z[k] = zin[k];
     for (int k = 0; k < 9; k++) R[k] = Rin[k];
-    return pose_update<DOF, 3>(sm, z, R, 1, 0, HVel<DOF>{}, ok);
+    return pose_update<DOF, 3>(sm, z, R, 1, 0, HVel<DOF>{}, ok, st, sh.literal_apply_delta != 0);
   } else if constexpr (K == MK_PRESSURE) {
     double z[1] = {zin[0]}, R[1] = {Rin[0]};
     HPressure<DOF> h;
     h.s[0] = ma.v3[0]; h.s[1] = ma.v3[1]; h.s[2] = ma.v3[2];
     h.patm = sh.p.atmospheric_pressure;
-    return pose_update<DOF, 1>(sm, z, R, 0, 0, h, ok);
+    return pose_update<DOF, 1>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0);
   } else if constexpr (K == MK_WATER) {
     double z[2] = {zin[0], zin[1]}, R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
     HWater<DOF> h;
     h.cw = ma.extra ? ma.extra[i] : 0.0;
-    return pose_update<DOF, 2>(sm, z, R, 1, 1, h, ok);
+    return pose_update<DOF, 2>(sm, z, R, 1, 1, h, ok, st, sh.literal_apply_delta != 0);
   } else if constexpr (K == MK_XY || K == MK_GEO || K == MK_DELAYED) {
     double z[2] = {zin[0], zin[1]}, R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
     int gate = 0;
@@ -124,10 +136,10 @@ UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, 
       z[0] = zin[0] + (sm.mu[L::s_pos] - ma.extra[2 * i]);
       z[1] = zin[1] + (sm.mu[L::s_pos + 1] - ma.extra[2 * i + 1]);
     }
-    return pose_update<DOF, 2>(sm, z, R, 0, gate, HXY<DOF>{}, ok);
+    return pose_update<DOF, 2>(sm, z, R, 0, gate, HXY<DOF>{}, ok, st, sh.literal_apply_delta != 0);
   } else if constexpr (K == MK_Z) {
     double z[1] = {zin[0]}, R[1] = {Rin[0]};
-    return pose_update<DOF, 1>(sm, z, R, 0, 0, HZ<DOF>{}, ok);
+    return pose_update<DOF, 1>(sm, z, R, 0, 0, HZ<DOF>{}, ok, st, sh.literal_apply_delta != 0);
   } else {  // MK_EFFORTS, PoseUKF.cpp:581-602
     double z[6], R[36];
     for (int k = 0; k < 6; k++) z[k] = zin[k];
@@ -153,7 +165,7 @@ UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, 
       cross3(wb, h.imu, cr);
       cross3(wb, cr, cc);
       for (int k = 0; k < 3; k++) h.ab[k] = ra[k] - cc[k];
-      return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok);
+      return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0);
     }
     HEfforts<DOF> h;
     h.ef = ef;
@@ -168,7 +180,7 @@ UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, 
         model[18 + l] = sm.mu[L::s_quad + l];
       }
     }
-    return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok);
+    return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0);
   }
 }
 
@@ -218,7 +230,14 @@ template <int DOF>
 __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_epoch(PoseBufs b, PoseShared sh, EpochArgs ea) {
   __shared__ Smem<DOF> sm;
   const int64_t i = blockIdx.x, B = b.batch;
+#ifdef UWVK_STAMPS
+  Stamper stamper;
+  Stamper* st = &stamper;
+#else
+  Stamper* st = nullptr;
+#endif
   load_instance<DOF>(sm, b, i);
+  UWVK_STAMP(11);
   bool ok = true, nan = false;
   uint32_t cnt[4] = {0, 0, 0, 0};
   MeasArgs ma;
@@ -237,12 +256,12 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_epoch(PoseBufs b, PoseShar
     } else {
       nan = true;
     }
-    bool sok = pose_predict<DOF>(sm, sh, pc, b.Q);
+    bool sok = pose_predict<DOF>(sm, sh, pc, b.Q, st);
     ok = ok && sok;
     if (fl & UWVK_EV_ACC) {
       const double* z = ea.acc + (e * B + i) * 3;
       if (all_finite(z, 3)) {
-        do_update<DOF, MK_ACC>(sm, sh, b, i, z, ea.acc_cov, ma, w, &sok);
+        do_update<DOF, MK_ACC>(sm, sh, b, i, z, ea.acc_cov, ma, w, &sok, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -251,7 +270,7 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_epoch(PoseBufs b, PoseShar
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + i) * 3;
       if (all_finite(z, 3)) {
-        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, b, i, z, ea.dvl_cov, ma, w, &sok);
+        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, b, i, z, ea.dvl_cov, ma, w, &sok, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -273,7 +292,7 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_epoch(PoseBufs b, PoseShar
         double zz[2] = {z[0], z[1]}, R[4] = {ea.adcp_cov[0], ea.adcp_cov[1], ea.adcp_cov[2], ea.adcp_cov[3]};
         HWater<DOF> h;
         h.cw = ea.cw[c];
-        cnt[2] += pose_update<DOF, 2>(sm, zz, R, 1, 1, h, &sok);
+        cnt[2] += pose_update<DOF, 2>(sm, zz, R, 1, 1, h, &sok, st, sh.literal_apply_delta != 0);
         ok = ok && sok;
       }
     }
@@ -298,7 +317,9 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_epoch(PoseBufs b, PoseShar
     if (ea.accept_counts)
       for (int k = 0; k < 4; k++) ea.accept_counts[i * 4 + k] += cnt[k];
   }
+  UWVK_STAMP(12);
   store_instance<DOF>(sm, b, i);
+  UWVK_STAMP(13);
 }
 
 template <int DOF>

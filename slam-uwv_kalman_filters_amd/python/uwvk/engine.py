@@ -27,7 +27,7 @@ SYMBOLS = [
     "uwvk_pose_update_water_velocity", "uwvk_pose_update_efforts", "uwvk_pose_update_xy", "uwvk_pose_update_z",
     "uwvk_pose_update_geographic", "uwvk_pose_update_delayed_xy", "uwvk_pose_reset_with_external_pose",
     "uwvk_pose_get_state", "uwvk_pose_get_rotation_rate", "uwvk_pose_get_status", "uwvk_pose_run_log",
-    "uwvk_pose_ensemble_stats", "uwvk_pose_timer_start", "uwvk_pose_timer_stop",
+    "uwvk_pose_ensemble_stats", "uwvk_pose_set_option", "uwvk_pose_timer_start", "uwvk_pose_timer_stop",
     "uwvk_vel_create", "uwvk_vel_destroy", "uwvk_vel_stream", "uwvk_vel_init", "uwvk_vel_setup_motion_model",
     "uwvk_vel_set_gyro", "uwvk_vel_set_efforts", "uwvk_vel_predict", "uwvk_vel_update_dvl",
     "uwvk_vel_update_pressure", "uwvk_vel_get_state", "uwvk_vel_get_model_state", "uwvk_vel_run_log",
@@ -130,6 +130,10 @@ class PoseUKFBatch:
     @property
     def stream(self):
         return self.L.uwvk_pose_stream(self.h)
+
+    def set_literal_apply_delta(self, on=True):
+        """ukfom's literal apply_delta re-spread instead of the exact T Sigma T^T form."""
+        _chk(self.L.uwvk_pose_set_option(self.h, 1, int(bool(on))), "set_option")
 
     def init_from_config(self, pos, pos_cov, rot, rot_cov, cfg, uwv, imu_in_body=None):
         pos, pos_cov, rot, rot_cov, ib = map(_f64, (pos, pos_cov, rot, rot_cov, imu_in_body))

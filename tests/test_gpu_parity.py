@@ -31,10 +31,12 @@ def orc():
     return oracle_ctypes
 
 
-def _pair(eng, orc, batch, dof=53, mode="C3", epochs=10):
+def _pair(eng, orc, batch, dof=53, mode="C3", epochs=10, literal=False):
     cfg, uwv, log = pose_setup(batch, dof, mode, epochs)
     o = orc.OraclePoseBatch(batch, dof)
     g = eng.PoseUKFBatch(batch, dof)
+    if literal:
+        g.set_literal_apply_delta(True)
     init_both(o, g, cfg, uwv, log)
     return cfg, uwv, log, o, g
 
@@ -60,11 +62,12 @@ def test_init_and_predict(eng, orc, dof):
     _check(o, g, dof, TOL_STEP)
 
 
+@pytest.mark.parametrize("literal", [False, True])
 @pytest.mark.parametrize("dof", [53, 26])
 @pytest.mark.parametrize("kind", ["acceleration", "velocity", "pressure", "water_velocity", "xy", "z",
                                   "efforts", "efforts_vel", "geographic", "delayed_xy"])
-def test_single_update(eng, orc, dof, kind):
-    cfg, uwv, log, o, g = _pair(eng, orc, 5, dof)
+def test_single_update(eng, orc, dof, kind, literal):
+    cfg, uwv, log, o, g = _pair(eng, orc, 5, dof, literal=literal)
     for f in (o, g):
         f.set_rotation_rate(log["gyro"][0])
         f.predict(1e-3)
@@ -104,9 +107,11 @@ def test_single_update(eng, orc, dof, kind):
     _check(o, g, dof, TOL_STEP)
 
 
-@pytest.mark.parametrize("dof,mode,epochs", [(53, "C3", 400), (26, "C3", 400), (53, "C4", 1000)])
-def test_run_log(eng, orc, dof, mode, epochs):
-    cfg, uwv, log, o, g = _pair(eng, orc, 4, dof, mode, epochs)
+@pytest.mark.parametrize("dof,mode,epochs,literal", [(53, "C3", 400, False), (26, "C3", 400, False),
+                                                     (53, "C4", 1000, False), (53, "C3", 400, True),
+                                                     (53, "C4", 1000, True)])
+def test_run_log(eng, orc, dof, mode, epochs, literal):
+    cfg, uwv, log, o, g = _pair(eng, orc, 4, dof, mode, epochs, literal=literal)
     counts_o = o.run_log(log)
     dlog = g.upload_log(log)
     acc = eng.DeviceBuffer(np.zeros((4, 4), np.uint32))
