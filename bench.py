@@ -34,7 +34,11 @@ METRIC = "UKF predict+update steps/sec at batch=65536 PoseUKF instances, 1 & 8 G
 # frozen algorithmic work per step: n = 53, N = 107
 F_PRED = 700_377
 F_UPD3 = 853_707
-F_STEP = F_PRED + F_UPD3  # 1,554,084 flop: predict + Acceleration update (m = 3)
+F_STEP = F_PRED + F_UPD3  # 1,554,084 flop: predict + Acceleration update (m = 3), reference algorithm
+# flops the engine executes per m = 3 update: apply_delta is the exact rotation
+# identity instead of a second LLT + sigma-point GEMM
+F_UPD3_EXEC = 155_237
+F_STEP_EXEC = F_PRED + F_UPD3_EXEC  # 855,614
 B_STEP = 45_808           # fp64 mu + Sigma read + write
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector = matrix) spec; probe measured 74 (profiles/r01_probe_fp64.txt)
 PEAK_HBM_GBS = 8000.0
@@ -104,7 +108,7 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from uwvk import engine, synth
+    from uwvk import engine, ensemble, synth
 
     B = a.batch_per_gpu
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
@@ -135,10 +139,8 @@ def main():
     kernel_ms = f.timer_stop()  # HIP events on the handle's stream around the epoch launches
     stats = f.ensemble_stats(truth)  # synchronous
     if dist is not None:
-        import torch
-        t = torch.from_numpy(stats).cuda()
-        dist.all_reduce(t)  # RCCL over xGMI: the only collective of the workload
-        stats = t.cpu().numpy()
+        # RCCL over xGMI: the only collective of the workload
+        stats = ensemble.allreduce_stats(stats, dist, device="cuda")
     f.synchronize()
     barrier()
     wall = time.perf_counter() - t0
@@ -154,7 +156,8 @@ def main():
     steps_total = B * world * a.steps
     value = steps_total / wall
     per_launch_ms = kernel_ms / a.steps
-    flops_launch = B * (F_STEP * a.steps + F_UPD3 * n_dvl) / a.steps
+    flops_launch = B * (F_STEP_EXEC * a.steps + F_UPD3_EXEC * n_dvl) / a.steps
+    flops_ref_launch = B * (F_STEP * a.steps + F_UPD3 * n_dvl) / a.steps
     achieved_tf = flops_launch / (per_launch_ms * 1e-3) / 1e12
     workload = "C3-dof%d-b%d" % (a.dof, B) if a.mode == "C3" else "%s-dof%d-b%d" % (a.mode, a.dof, B)
     traffic = roofline_traffic(workload)
@@ -173,6 +176,7 @@ def main():
                      "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": traffic,
                      "kernel_ms_per_launch": per_launch_ms,
                      "algorithmic_flop_per_launch": flops_launch,
+                     "reference_equivalent_tflops": flops_ref_launch / (per_launch_ms * 1e-3) / 1e12,
                      "hbm_frac_algorithmic": (B * B_STEP / (per_launch_ms * 1e-3)) / (PEAK_HBM_GBS * 1e9)},
         "ensemble": {"nees_mean_pos_ori_vel": float(stats[-1] / (B * world))},
     }

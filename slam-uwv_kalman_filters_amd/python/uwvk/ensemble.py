@@ -1,0 +1,55 @@
+"""Ensemble (Monte-Carlo / multi-vehicle) helpers for instance-sharded runs.
+
+Instances are independent (no coupling anywhere in the reference: each filter
+is self-contained, PoseUKF.hpp:195-205), so N ranks own contiguous instance
+ranges and exchange nothing on the data path.  The one collective is the sum
+of the ensemble statistics (uwvk_pose_ensemble_stats) — over RCCL on GPUs, over
+gloo in the CPU tests.
+"""
+import numpy as np
+
+
+def shard_range(rank, world, global_batch):
+    """Contiguous instance range [lo, hi) owned by `rank`."""
+    lo = global_batch * rank // world
+    hi = global_batch * (rank + 1) // world
+    return lo, hi
+
+
+def _qlog_delta(q, t):
+    """log(q * conj(t)) for arrays of unit quaternions (w, x, y, z)."""
+    w = q[..., 0] * t[0] + np.sum(q[..., 1:] * t[1:], -1)
+    v = t[0] * q[..., 1:] - q[..., :1] * t[1:] - np.cross(q[..., 1:], t[1:])
+    sgn = np.where(w < 0, -1.0, 1.0)
+    w, v = w * sgn, v * sgn[..., None]
+    nv = np.linalg.norm(v, axis=-1)
+    k = np.where(nv > 0, 2 * np.arctan2(nv, w) / np.where(nv > 0, nv, 1), 0.0)
+    return k[..., None] * v
+
+
+def ensemble_stats_host(x, P, truth):
+    """Host reference of uwvk_pose_ensemble_stats (same layout of `out`)."""
+    store = x.shape[1]
+    out = np.zeros(3 * store + 1)
+    out[:store] = x.sum(0)
+    out[store:2 * store] = (x * x).sum(0)
+    e = x - truth
+    e[:, 3:7] = 0.0
+    r = _qlog_delta(x[:, 3:7], truth[3:7])
+    sq = (e * e).sum(0)
+    sq[3:6] += (r * r).sum(0)
+    out[2 * store:3 * store] = sq
+    err = np.concatenate([x[:, 0:3] - truth[0:3], r, x[:, 7:10] - truth[7:10]], 1)
+    sub = P[:, :9, :9]
+    out[3 * store] = float(np.einsum("bi,bi->", err, np.linalg.solve(sub, err[..., None])[..., 0]))
+    return out
+
+
+def allreduce_stats(stats, dist, device=None):
+    """Sum the per-rank statistics vectors (torch.distributed, any backend)."""
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(stats, dtype=np.float64))
+    if device is not None:
+        t = t.to(device)
+    dist.all_reduce(t)
+    return t.cpu().numpy()

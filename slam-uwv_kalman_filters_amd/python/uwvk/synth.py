@@ -159,7 +159,8 @@ class Truth:
 MODES = ("C1", "C3", "C4")
 
 
-def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_instance=0, cfg=None):
+def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_instance=0, cfg=None,
+                  dropout_on=30.0, dropout_off=10.0, adcp_every=1000, efforts_velocity_only=False):
     """Per-instance noisy measurement log.  Returns a dict of numpy arrays.
 
     mode C1/C3: 1 kHz IMU + 5 Hz DVL.
@@ -175,13 +176,15 @@ def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_in
     t_meas = k * dt
     dropout = np.zeros(epochs, bool)
     if mode == "C4":
-        dropout = np.mod(t_meas, 40.0) >= 30.0 - 1e-12
+        dropout = np.mod(t_meas, dropout_on + dropout_off) >= dropout_on - 1e-12
     dvl_due = (k % 200 == 0) & ~dropout
     flags[dvl_due] |= abi.EV_DVL
     if mode == "C4":
         flags[k % 100 == 0] |= abi.EV_PRESSURE
-        flags[k % 1000 == 0] |= abi.EV_ADCP
+        flags[k % adcp_every == 0] |= abi.EV_ADCP
         flags[(k % 100 == 0) & dropout] |= abi.EV_EFFORTS
+        if efforts_velocity_only:
+            flags[(flags & abi.EV_EFFORTS) != 0] |= abi.EV_EFFORTS_VELOCITY_ONLY
 
     def idx_of(bit):
         sel = (flags & bit) != 0

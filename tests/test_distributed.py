@@ -1,0 +1,88 @@
+"""Instance sharding over ranks (world_size 2, gloo on CPU): each rank runs its
+contiguous shard with the CPU oracle; per-instance results are bit-identical to
+the single-process run and the all-reduced ensemble statistics equal the
+single-process statistics."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+B, EPOCHS = 6, 220
+
+
+def _run_shard(lo, hi):
+    sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ctypes as O
+    from uwvk import synth
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(hi - lo, EPOCHS, "C3", first_instance=lo)
+    o = O.OraclePoseBatch(hi - lo)
+    o.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    o.set_process_noise_from_config(cfg, log["dt"])
+    o.run_log(log)
+    x, P = o.get_state()
+    return x, P, log["truth"].state(EPOCHS)
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+    from uwvk import ensemble
+    lo, hi = ensemble.shard_range(rank, world, B)
+    x, P, truth = _run_shard(lo, hi)
+    stats = ensemble.allreduce_stats(ensemble.ensemble_stats_host(x, P, truth), dist)
+    q.put((rank, lo, hi, x, P, stats))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_shards_match_single_process():
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+    from uwvk import ensemble
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    x1, P1, truth = _run_shard(0, B)
+    for rank, lo, hi, x, P, stats in res:
+        assert np.array_equal(x, x1[lo:hi]) and np.array_equal(P, P1[lo:hi])  # bit-identical per instance
+        np.testing.assert_allclose(stats, ensemble.ensemble_stats_host(x1, P1, truth), rtol=1e-12, atol=1e-12)
+
+
+def test_shard_ranges_cover_batch():
+    sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+    from uwvk import ensemble
+    for world in (1, 2, 3, 8):
+        r = [ensemble.shard_range(k, world, 1048576 + 5) for k in range(world)]
+        assert r[0][0] == 0 and r[-1][1] == 1048576 + 5
+        assert all(r[k][1] == r[k + 1][0] for k in range(world - 1))
+
+
+@pytest.mark.gpu
+def test_ensemble_stats_kernel_matches_host():
+    sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+    from uwvk import engine, ensemble, synth
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(300, 50, "C3")
+    f = engine.PoseUKFBatch(300)
+    f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    f.set_process_noise_from_config(cfg, log["dt"])
+    f.run_log(f.upload_log(log))
+    truth = log["truth"].state(50)
+    x, P = f.get_state()
+    np.testing.assert_allclose(f.ensemble_stats(truth), ensemble.ensemble_stats_host(x, P, truth), rtol=1e-9,
+                               atol=1e-12)
