@@ -84,7 +84,7 @@ def cpu_baseline(synth, cfg, uwv, mode, dof, threads):
     """fp64 C oracle on a bounded sample of the same workload (host cores)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as O
-    batch, epochs = 16 * threads, 200
+    batch, epochs = 32 * threads, 2000  # ~10-20 s of CPU work
     log = synth.make_pose_log(batch, epochs, mode=mode, dof=dof)
     o = O.OraclePoseBatch(batch, dof)
     o.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)

@@ -298,10 +298,15 @@ typedef struct uwvk_pose_log {
   const int32_t* efforts_index;
   const double* efforts;     /* [n_efforts][batch][6] */
   double efforts_cov[36];
+  /* HOST copy of flags (nullable): lets run_log plan its launches without a
+   * device->host read of `flags`. */
+  const uint32_t* host_flags;
 } uwvk_pose_log;
 
-/* Runs epochs [first, first+count) of the log; one fused kernel launch per
- * epoch (predict + all flagged updates with Sigma resident in LDS).
+/* Runs epochs [first, first+count) of the log.  Default (PSP) path: one launch
+ * per run of epochs, each instance's Sigma resident in LDS across the run;
+ * BodyEfforts epochs run through the literal kernel (one launch per epoch).
+ * UWVK_OPT_DENSE_SIGMA = 1: one literal fused launch per epoch.
  * accept_counts (device, nullable): [batch][4] uint32 accepted DVL/pressure/ADCP/efforts. */
 uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t first, int64_t count,
                               uint32_t* accept_counts);
@@ -320,6 +325,13 @@ uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* 
  *   (T rotates the orientation block by exp(d)); 1 runs the literal re-spread
  *   (Cholesky + sigma points + covariance GEMM).  Results agree to rounding. */
 #define UWVK_OPT_LITERAL_APPLY_DELTA 1
+/* UWVK_OPT_DENSE_SIGMA: 0 (default) evaluates ukfom's unscented transform in
+ *   partitioned form (PSP): sigma points only along the Cholesky columns a model
+ *   is non-affine in, the affine remainder in closed form (A Sigma A^T, H Sigma
+ *   H^T); equal to the literal spread up to rounding.
+ *   1 propagates all 2n+1 sigma points (MFMA covariance GEMM).  Setting
+ *   UWVK_OPT_LITERAL_APPLY_DELTA also selects the literal kernels. */
+#define UWVK_OPT_DENSE_SIGMA 2
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
 
 /* Kernel-timing helper: HIP events recorded on the handle's stream. */

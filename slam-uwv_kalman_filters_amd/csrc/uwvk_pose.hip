@@ -8,6 +8,7 @@
 //   [-> Velocity (DVL) -> Pressure -> ADCP cells -> BodyEfforts]
 // with Sigma resident in LDS across all steps of the epoch.
 #include "uwvk_pose_kernels.hpp"
+#include "uwvk_psp.hpp"
 #include "uwvk_host.hpp"
 
 #include <cmath>
@@ -35,8 +36,12 @@ struct uwvk_pose {
   uwvk_location loc{};
   uwvk_uwv_params uwv{};
   bool has_state = false, has_Q = false;
+  int dense = 0;  // UWVK_OPT_DENSE_SIGMA
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
+
+// literal (all 2n+1 sigma points) kernels requested?
+static bool use_dense(const uwvk_pose* h) { return h->dense || h->sh.literal_apply_delta; }
 
 static PoseBufs bufs(const uwvk_pose* h) {
   PoseBufs b;
@@ -214,7 +219,10 @@ uwvk_status uwvk_pose_predict(uwvk_pose* h, double dt) {
   if (!h->has_state) return UWVK_ENOTINIT;
   PoseBufs b = bufs(h);
   PoseShared sh = h->sh;
-  HIPCHK(launch_pose_predict(h->dof, h->stream, b, sh, dt));
+  if (use_dense(h))
+    HIPCHK(launch_pose_predict(h->dof, h->stream, b, sh, dt));
+  else
+    HIPCHK(launch_psp_predict(h->dof, h->stream, b, sh, dt));
   return UWVK_OK;
 }
 
@@ -259,7 +267,10 @@ static uwvk_status launch_update(uwvk_pose* h, int m, const double* mu, const do
   ma.accepted = h->d_accepted;
   PoseBufs b = bufs(h);
   PoseShared sh = h->sh;
-  HIPCHK(launch_pose_update(h->dof, K, h->stream, b, sh, ma, m));
+  if (K == MK_EFFORTS || use_dense(h))
+    HIPCHK(launch_pose_update(h->dof, K, h->stream, b, sh, ma, m));
+  else
+    HIPCHK(launch_psp_update(h->dof, K, h->stream, b, sh, ma, m));
   if (accepted) HIPCHK(hipMemcpyAsync(accepted, h->d_accepted, (size_t)B, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return UWVK_OK;
@@ -369,11 +380,40 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   ea.accept_counts = accept_counts;
   PoseBufs b = bufs(h);
   PoseShared sh = h->sh;
-  // one launch per epoch: the driver's "step" granularity
-  for (int64_t e = first; e < first + count; e++) {
-    ea.first = e;
-    ea.count = 1;
-    HIPCHK(launch_pose_epoch(h->dof, h->stream, b, sh, ea));
+  if (use_dense(h)) {  // literal kernels: one fused launch per epoch
+    for (int64_t e = first; e < first + count; e++) {
+      ea.first = e;
+      ea.count = 1;
+      HIPCHK(launch_pose_epoch(h->dof, h->stream, b, sh, ea));
+    }
+    return UWVK_OK;
+  }
+  // PSP: one launch per run of epochs without BodyEfforts; efforts epochs
+  // go through the literal fused kernel (same HBM state layout)
+  std::vector<uint32_t> fl;
+  const uint32_t* hf = log->host_flags ? log->host_flags + first : nullptr;
+  if (!hf && count > 0) {
+    fl.resize((size_t)count);
+    HIPCHK(hipMemcpyAsync(fl.data(), log->flags + first, (size_t)count * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    hf = fl.data();
+  }
+  int64_t e = first;
+  while (e < first + count) {
+    int64_t r = e;
+    while (r < first + count && !(hf[r - first] & UWVK_EV_EFFORTS)) r++;
+    if (r > e) {
+      ea.first = e;
+      ea.count = r - e;
+      HIPCHK(launch_psp_epoch(h->dof, h->stream, b, sh, ea));
+    }
+    if (r < first + count) {
+      ea.first = r;
+      ea.count = 1;
+      HIPCHK(launch_pose_epoch(h->dof, h->stream, b, sh, ea));
+      r++;
+    }
+    e = r;
   }
   return UWVK_OK;
 }
@@ -402,6 +442,10 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
   if (!h) return UWVK_EINVAL;
   if (option == UWVK_OPT_LITERAL_APPLY_DELTA) {
     h->sh.literal_apply_delta = value ? 1 : 0;
+    return UWVK_OK;
+  }
+  if (option == UWVK_OPT_DENSE_SIGMA) {
+    h->dense = value ? 1 : 0;
     return UWVK_OK;
   }
   return UWVK_EINVAL;

@@ -1,0 +1,278 @@
+// uwvk_psp_k.hip — PSP PoseUKF kernels (one wavefront per filter instance).
+//
+// k_psp_epoch is the hot path of uwvk_pose_run_log: each workgroup (one wave)
+// loads its instance's (mu, Sigma) from HBM once, runs every epoch of the
+// requested range with Sigma packed in LDS, and writes it back once:
+//   RotationRate -> predictionStep(dt) -> Acceleration update
+//   [-> Velocity (DVL) -> Pressure -> ADCP cells]
+// BodyEfforts epochs are routed by the host to the literal kernels
+// (k_pose_epoch), whose HBM layout is shared.
+#define UWVK_POSE_KERNEL_BODIES
+#include "uwvk_pose_kernels.hpp"
+#include "uwvk_psp_dev.hpp"
+#include "uwvk_psp.hpp"
+
+namespace uwvk {
+namespace psp {
+
+template <int DOF>
+UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
+  using G = PG<DOF>;
+  const int l = lane_id();
+  const double* gs = b.sigma + inst * (int64_t)(DOF * DOF);
+  double v[G::NSLOT];
+#pragma unroll
+  for (int t = 0; t < G::NSLOT; t++) {  // all loads in flight before the LDS stores
+    const int e = l + 64 * t;
+    int i = 0, j = 0;
+    if (e < G::NP) unpack(e, i, j);
+    v[t] = e < G::NP ? gs[i * DOF + j] : 0.0;
+  }
+  const double m = l < Lay<DOF>::store ? b.mu[inst * Lay<DOF>::store + l] : 0.0;
+#pragma unroll
+  for (int t = 0; t < G::NSLOT; t++) {
+    const int e = l + 64 * t;
+    if (e < G::NP) sm.S[e] = v[t];
+  }
+  if (l < Lay<DOF>::store) sm.mu[l] = m;
+  psync();
+}
+
+template <int DOF>
+UWVK_DEV void store_psp(const PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
+  using G = PG<DOF>;
+  const int l = lane_id();
+  double* gs = b.sigma + inst * (int64_t)(DOF * DOF);
+#pragma unroll 4
+  for (int t = 0; t < G::NSLOT; t++) {
+    const int e = l + 64 * t;
+    if (e < G::NP) {
+      int i, j;
+      unpack(e, i, j);
+      const double s = sm.S[e];
+      gs[i * DOF + j] = s;
+      if (i != j) gs[j * DOF + i] = s;
+    }
+  }
+  if (l < Lay<DOF>::store) b.mu[inst * Lay<DOF>::store + l] = sm.mu[l];
+}
+
+template <int M>
+UWVK_DEV void copy_zr(const double* zin, const double* Rin, double (&z)[M], double (&R)[M * M]) {
+#pragma unroll
+  for (int k = 0; k < M; k++) z[k] = zin[k];
+#pragma unroll
+  for (int k = 0; k < M * M; k++) R[k] = Rin[k];
+}
+
+// one measurement update of kind KIND on instance inst (PSP form)
+template <int DOF, int KIND>
+UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, const double* zin, const double* Rin,
+                        const MeasArgs& ma, bool* ok) {
+  using L = Lay<DOF>;
+  if constexpr (KIND == MK_ACC) {
+    double z[3], R[9];
+    copy_zr<3>(zin, Rin, z, R);
+    return psp_update<DOF>(sm, z, R, 0, PAcc<DOF>{}, ok);
+  } else if constexpr (KIND == MK_VEL) {
+    double z[3], R[9];
+    copy_zr<3>(zin, Rin, z, R);
+    return psp_update<DOF>(sm, z, R, 0, PVel<DOF>{}, ok);
+  } else if constexpr (KIND == MK_PRESSURE) {
+    double z[1], R[1];
+    copy_zr<1>(zin, Rin, z, R);
+    PPressure<DOF> h;
+    h.h.s[0] = ma.v3[0]; h.h.s[1] = ma.v3[1]; h.h.s[2] = ma.v3[2];
+    h.h.patm = sh.p.atmospheric_pressure;
+    return psp_update<DOF>(sm, z, R, 0, h, ok);
+  } else if constexpr (KIND == MK_WATER) {
+    double z[2], R[4];
+    copy_zr<2>(zin, Rin, z, R);
+    PWater<DOF> h;
+    h.cw = ma.extra ? ma.extra[inst] : 0.0;
+    return psp_update<DOF>(sm, z, R, 1, h, ok);
+  } else if constexpr (KIND == MK_XY || KIND == MK_GEO || KIND == MK_DELAYED) {
+    double z[2], R[4];
+    copy_zr<2>(zin, Rin, z, R);
+    int gate = 0;
+    if constexpr (KIND == MK_GEO) {  // PoseUKF.cpp:571-578
+      double r[3];
+      const double x = (zin[0] - sh.lat0) * sh.rm;
+      const double y = -(zin[1] - sh.lon0) * sh.rn_cos;
+      qrot(sm.mu + L::s_quat, ma.v3, r);
+      z[0] = x - r[0];
+      z[1] = y - r[1];
+      gate = 1;
+    }
+    if constexpr (KIND == MK_DELAYED) {  // PoseUKF.cpp:516-521
+      z[0] = zin[0] + (sm.mu[L::s_pos] - ma.extra[2 * inst]);
+      z[1] = zin[1] + (sm.mu[L::s_pos + 1] - ma.extra[2 * inst + 1]);
+    }
+    return psp_update<DOF>(sm, z, R, gate, PXY<DOF>{}, ok);
+  } else {
+    static_assert(KIND == MK_Z, "PSP update kind");
+    double z[1], R[1];
+    copy_zr<1>(zin, Rin, z, R);
+    return psp_update<DOF>(sm, z, R, 0, PZ<DOF>{}, ok);
+  }
+}
+
+template <int DOF>
+__global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, double dt) {
+  __shared__ PspSmem<DOF> sm;
+  const int64_t inst = blockIdx.x;
+  load_psp<DOF>(sm, b, inst);
+  ProcCtx pc;
+  for (int k = 0; k < 3; k++) pc.w[k] = b.rot[inst * 3 + k];
+  pc.dt = dt;
+  pc.off = b.off + inst * 28;
+  const bool ok = psp_predict<DOF>(sm, sh, pc, b.Q);
+  if (!ok && lane_id() == 0) b.status[inst] |= UWVK_ST_NOTPD;
+  store_psp<DOF>(sm, b, inst);
+}
+
+template <int DOF, int KIND>
+__global__ __launch_bounds__(64) void k_psp_update(PoseBufs b, PoseShared sh, MeasArgs ma, int m) {
+  __shared__ PspSmem<DOF> sm;
+  const int64_t inst = blockIdx.x;
+  if (ma.mask && !ma.mask[inst]) {
+    if (ma.accepted && lane_id() == 0) ma.accepted[inst] = 0;
+    return;
+  }
+  const double* z = ma.mu + inst * m;
+  const double* R = ma.cov ? ma.cov + inst * m * m : ma.shared_cov;
+  if (!all_finite(z, m) || !all_finite(R, m * m)) {  // checkMeasurment [EXT]
+    if (lane_id() == 0) {
+      b.status[inst] |= UWVK_ST_NAN;
+      if (ma.accepted) ma.accepted[inst] = 0;
+    }
+    return;
+  }
+  load_psp<DOF>(sm, b, inst);
+  bool ok = true;
+  const bool acc = do_update<DOF, KIND>(sm, sh, inst, z, R, ma, &ok);
+  if (lane_id() == 0) {
+    if (!ok) b.status[inst] |= UWVK_ST_NOTPD;
+    if (ma.accepted) ma.accepted[inst] = acc ? 1 : 0;
+  }
+  store_psp<DOF>(sm, b, inst);
+}
+
+template <int DOF>
+__global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh, EpochArgs ea) {
+  __shared__ PspSmem<DOF> sm;
+  const int64_t inst = blockIdx.x, B = b.batch;
+  load_psp<DOF>(sm, b, inst);
+  bool ok = true, nan = false;
+  uint32_t cnt[4] = {0, 0, 0, 0};
+  MeasArgs ma{};
+  ma.v3[0] = ea.p_sens[0]; ma.v3[1] = ea.p_sens[1]; ma.v3[2] = ea.p_sens[2];
+  double w[3] = {b.rot[inst * 3], b.rot[inst * 3 + 1], b.rot[inst * 3 + 2]};
+  ProcCtx pc;
+  for (int k = 0; k < 3; k++) pc.w[k] = w[k];
+  pc.dt = ea.dt;
+  pc.off = b.off + inst * 28;
+#pragma unroll 1
+  for (int64_t e = ea.first; e < ea.first + ea.count; e++) {
+    const uint32_t fl = ea.flags[e];
+    const double* g = ea.gyro + (e * B + inst) * 3;
+    if (all_finite(g, 3)) {  // integrateMeasurement(RotationRate): checkMeasurment, then store
+      for (int k = 0; k < 3; k++) { w[k] = g[k]; pc.w[k] = g[k]; }
+    } else {
+      nan = true;
+    }
+    bool sok = psp_predict<DOF>(sm, sh, pc, b.Q);
+    ok = ok && sok;
+    if (fl & UWVK_EV_ACC) {
+      const double* z = ea.acc + (e * B + inst) * 3;
+      if (all_finite(z, 3)) {
+        do_update<DOF, MK_ACC>(sm, sh, inst, z, ea.acc_cov, ma, &sok);
+        ok = ok && sok;
+      } else {
+        nan = true;
+      }
+    }
+    if (fl & UWVK_EV_DVL) {
+      const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + inst) * 3;
+      if (all_finite(z, 3)) {
+        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, inst, z, ea.dvl_cov, ma, &sok);
+        ok = ok && sok;
+      } else {
+        nan = true;
+      }
+    }
+    if (fl & UWVK_EV_PRESSURE) {
+      const double* z = ea.pressure + (int64_t)ea.p_index[e] * B + inst;
+      if (all_finite(z, 1)) {
+        cnt[1] += do_update<DOF, MK_PRESSURE>(sm, sh, inst, z, &ea.p_cov, ma, &sok);
+        ok = ok && sok;
+      } else {
+        nan = true;
+      }
+    }
+    if (fl & UWVK_EV_ADCP) {
+      for (int c = 0; c < ea.cells; c++) {
+        const double* z = ea.adcp + (((int64_t)ea.a_index[e] * ea.cells + c) * B + inst) * 2;
+        if (!all_finite(z, 2)) { nan = true; continue; }
+        double zz[2] = {z[0], z[1]}, R[4] = {ea.adcp_cov[0], ea.adcp_cov[1], ea.adcp_cov[2], ea.adcp_cov[3]};
+        PWater<DOF> h;
+        h.cw = ea.cw[c];
+        cnt[2] += psp_update<DOF>(sm, zz, R, 1, h, &sok);
+        ok = ok && sok;
+      }
+    }
+  }
+  if (lane_id() == 0) {
+    if (!ok) b.status[inst] |= UWVK_ST_NOTPD;
+    if (nan) b.status[inst] |= UWVK_ST_NAN;
+    if (ea.count > 0) {
+      b.rot[inst * 3] = w[0]; b.rot[inst * 3 + 1] = w[1]; b.rot[inst * 3 + 2] = w[2];
+    }
+    if (ea.accept_counts)
+      for (int k = 0; k < 4; k++) ea.accept_counts[inst * 4 + k] += cnt[k];
+  }
+  store_psp<DOF>(sm, b, inst);
+}
+
+}  // namespace psp
+
+template <int DOF>
+static hipError_t psp_update_dof(int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                                 const MeasArgs& ma, int m) {
+  const dim3 g((unsigned)b.batch), t(64);
+  switch (kind) {
+    case MK_ACC: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_ACC>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_VEL: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_VEL>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_PRESSURE: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_PRESSURE>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_WATER: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_WATER>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_XY: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_XY>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_Z: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_Z>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_GEO: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_GEO>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_DELAYED: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_DELAYED>), g, t, 0, st, b, sh, ma, m); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_psp_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt) {
+  if (dof == 53)
+    hipLaunchKernelGGL(psp::k_psp_predict<53>, dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, dt);
+  else
+    hipLaunchKernelGGL(psp::k_psp_predict<26>, dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, dt);
+  return hipGetLastError();
+}
+
+hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                             const MeasArgs& ma, int m) {
+  return dof == 53 ? psp_update_dof<53>(kind, st, b, sh, ma, m) : psp_update_dof<26>(kind, st, b, sh, ma, m);
+}
+
+hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea) {
+  if (dof == 53)
+    hipLaunchKernelGGL(psp::k_psp_epoch<53>, dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, ea);
+  else
+    hipLaunchKernelGGL(psp::k_psp_epoch<26>, dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, ea);
+  return hipGetLastError();
+}
+
+}  // namespace uwvk

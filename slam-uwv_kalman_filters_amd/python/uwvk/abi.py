@@ -70,7 +70,8 @@ class PoseLog(C.Structure):  # uwvk_pose_log (device pointers)
                 ("pressure_index", P), ("pressure", P), ("pressure_cov", D),
                 ("pressure_sensor_in_imu", _arr(D, 3)), ("adcp_index", P), ("adcp", P),
                 ("adcp_cells", C.c_int32), ("adcp_cell_weighting", _arr(D, 8)), ("adcp_cov", _arr(D, 4)),
-                ("efforts_index", P), ("efforts", P), ("efforts_cov", _arr(D, 36))]
+                ("efforts_index", P), ("efforts", P), ("efforts_cov", _arr(D, 36)),
+                ("host_flags", P)]
 
 
 class VelLog(C.Structure):  # uwvk_vel_log (device pointers)

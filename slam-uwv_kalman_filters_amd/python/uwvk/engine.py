@@ -131,6 +131,10 @@ class PoseUKFBatch:
     def stream(self):
         return self.L.uwvk_pose_stream(self.h)
 
+    def set_dense_sigma(self, on=True):
+        """Propagate all 2n+1 sigma points (literal kernels) instead of the PSP form."""
+        _chk(self.L.uwvk_pose_set_option(self.h, 2, int(bool(on))), "set_option")
+
     def set_literal_apply_delta(self, on=True):
         """ukfom's literal apply_delta re-spread instead of the exact T Sigma T^T form."""
         _chk(self.L.uwvk_pose_set_option(self.h, 1, int(bool(on))), "set_option")
@@ -268,6 +272,8 @@ class DevicePoseLog:
         s.efforts_index = up("efforts_index", log["efforts_index"], np.int32)
         s.efforts = up("efforts", log["efforts"], np.float64)
         abi.fill(s.efforts_cov, np.asarray(log["efforts_cov"]).ravel())
+        self.host_flags = np.ascontiguousarray(log["flags"], dtype=np.uint32)
+        s.host_flags = self.host_flags.ctypes.data
         self.s = s
         self.epochs = s.epochs
 

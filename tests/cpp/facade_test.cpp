@@ -1,0 +1,152 @@
+// facade_test.cpp — drives the C++ facade (PoseUKF.hpp) the way a reference
+// user drives pose_estimation::PoseUKF (integrateMeasurement / predictionStep,
+// PoseUKF.hpp:126-190) and compares every instance with the CPU oracle
+// (oracle/uwvk_oracle.h, test infrastructure).  Exit 0 = parity.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "uwv_kalman_filters_amd/PoseUKF.hpp"
+extern "C" {
+#include "../../oracle/uwvk_oracle.h"
+}
+
+namespace U = uwv_kalman_filters_amd;
+
+static void fill(double* d, std::initializer_list<double> v) {
+  int i = 0;
+  for (double x : v) d[i++] = x;
+}
+
+int main() {
+  const int64_t B = 16;
+  const double dt = 1e-3;
+  uwvk_pose_config cfg{};
+  fill(cfg.acceleration.randomwalk, {1e-3, 1e-3, 1e-3});
+  fill(cfg.acceleration.bias_instability, {1e-4, 1e-4, 1e-4});
+  cfg.acceleration.bias_tau = 600;
+  fill(cfg.rotation_rate.randomwalk, {1e-4, 1e-4, 1e-4});
+  fill(cfg.rotation_rate.bias_instability, {1e-5, 1e-5, 1e-5});
+  cfg.rotation_rate.bias_tau = 600;
+  auto& m = cfg.model_noise_parameters;
+  fill(m.body_efforts_std, {5, 5, 5, 1, 1, 1});
+  for (int i = 0; i < 9; i++) m.inertia_instability[i] = 10, m.lin_damping_instability[i] = 5,
+                              m.quad_damping_instability[i] = 5;
+  m.inertia_tau = m.lin_damping_tau = m.quad_damping_tau = 3600;
+  cfg.water_velocity.tau = 900; cfg.water_velocity.limits = 0.1; cfg.water_velocity.scale = 1e-3;
+  fill(cfg.water_velocity.measurement_std, {0.05, 0.05, 0.05});
+  cfg.water_velocity.adcp_bias_tau = 900; cfg.water_velocity.adcp_bias_limits = 0.05;
+  cfg.location = {0.9, 0.15, 0.0};
+  cfg.hydrostatics = {1025, 2, 3600, 101325, 100};
+  uwvk_uwv_params uwv{};
+  const double Md[6] = {200, 250, 300, 20, 30, 30}, Dl[6] = {20, 30, 40, 5, 5, 5}, Dq[6] = {50, 80, 100, 10, 10, 10};
+  for (int i = 0; i < 6; i++) {
+    uwv.inertia_matrix[i * 7] = Md[i];
+    uwv.damping_matrices[0][i * 7] = Dl[i];
+    uwv.damping_matrices[1][i * 7] = Dq[i];
+  }
+  uwv.weight = uwv.buoyancy = 2000;
+  uwv.distance_body2centerofbuoyancy[2] = 0.05;
+
+  std::mt19937_64 rng(7);
+  std::normal_distribution<double> n01;
+  std::vector<double> pos(B * 3), pos_cov(B * 9, 0), rot(B * 4), rot_cov(B * 9, 0);
+  for (int64_t b = 0; b < B; b++) {
+    for (int i = 0; i < 3; i++) {
+      pos[b * 3 + i] = 5 * n01(rng);
+      pos_cov[b * 9 + i * 4] = 0.1;
+      rot_cov[b * 9 + i * 4] = 1e-3;
+    }
+    double q[4] = {1, 0.05 * n01(rng), 0.05 * n01(rng), 0.3 * n01(rng)};
+    double nq = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int i = 0; i < 4; i++) rot[b * 4 + i] = q[i] / nq;
+  }
+
+  U::PoseUKF f(B, pos, pos_cov, rot, rot_cov, cfg, uwv);
+  f.setProcessNoiseFromConfig(cfg, dt);
+  std::vector<or_pose*> o(B);
+  for (int64_t b = 0; b < B; b++) {
+    o[b] = (or_pose*)calloc(1, or_pose_sizeof());
+    or_pose_init_from_config(o[b], 53, &pos[b * 3], &pos_cov[b * 9], &rot[b * 4], &rot_cov[b * 9], &cfg, &uwv,
+                             nullptr);
+    or_pose_set_process_noise_from_config(o[b], &cfg, dt, nullptr);
+  }
+
+  U::RotationRate w;
+  U::Acceleration a;
+  U::Velocity v;
+  U::Pressure p;
+  w.mu.resize(B * 3);
+  a.mu.resize(B * 3);
+  v.mu.resize(B * 3);
+  p.mu.resize(B);
+  for (int i = 0; i < 3; i++) a.shared_cov[i * 4] = 1e-4, v.shared_cov[i * 4] = 1e-4;
+  p.shared_cov[0] = 1e4;
+  int mismatch_gate = 0;
+  for (int e = 0; e < 300; e++) {
+    for (int64_t b = 0; b < B; b++)
+      for (int i = 0; i < 3; i++) {
+        w.mu[b * 3 + i] = 0.01 * n01(rng);
+        a.mu[b * 3 + i] = (i == 2 ? 9.81 : 0.0) + 0.02 * n01(rng);
+        v.mu[b * 3 + i] = 0.05 * n01(rng);
+      }
+    f.integrateMeasurement(w);
+    f.predictionStep(dt);
+    f.integrateMeasurement(a);
+    for (int64_t b = 0; b < B; b++) {
+      int acc;
+      or_pose_set_rotation_rate(o[b], &w.mu[b * 3], nullptr);
+      or_pose_predict(o[b], dt);
+      or_pose_update_acceleration(o[b], &a.mu[b * 3], a.shared_cov.data(), &acc);
+    }
+    if (e % 50 == 49) {
+      f.integrateMeasurement(v);
+      auto gate = f.lastAccepted();
+      for (int64_t b = 0; b < B; b++) {
+        int acc;
+        or_pose_update_velocity(o[b], &v.mu[b * 3], v.shared_cov.data(), &acc);
+        mismatch_gate += (acc != 0) != (gate[b] != 0);
+      }
+    }
+    if (e % 100 == 99) {
+      for (int64_t b = 0; b < B; b++) p.mu[b] = 101325 + 1025 * 9.81 * 2.0 + 50 * n01(rng);
+      f.integrateMeasurement(p);
+      for (int64_t b = 0; b < B; b++) {
+        int acc;
+        const double s[3] = {0, 0, 0};
+        or_pose_update_pressure(o[b], &p.mu[b], p.shared_cov.data(), s, &acc);
+      }
+    }
+  }
+  std::vector<double> x, P;
+  f.getState(x, &P);
+  double worst = 0;
+  std::vector<double> xo(54), Po(53 * 53);
+  for (int64_t b = 0; b < B; b++) {
+    or_pose_get_state(o[b], xo.data(), Po.data());
+    for (int i = 0; i < 53; i++)
+      for (int j = 0; j < 53; j++) {
+        double d = std::sqrt(Po[i * 53 + i] * Po[j * 53 + j]);
+        worst = std::fmax(worst, std::fabs(P[b * 2809 + i * 53 + j] - Po[i * 53 + j]) / d);
+      }
+    for (int i = 0; i < 54; i++) {
+      if (i >= 3 && i < 7) continue;
+      int d = i < 3 ? i : i - 1;
+      worst = std::fmax(worst, std::fabs(x[b * 54 + i] - xo[i]) / std::sqrt(Po[d * 53 + d]));
+    }
+    free(o[b]);
+  }
+  // error behaviour: a NaN measurement throws like the reference's checkMeasurment
+  bool threw = false;
+  try {
+    a.mu[0] = NAN;
+    f.integrateMeasurement(a);
+  } catch (const U::Error& e) {
+    threw = true;
+  }
+  std::printf("facade parity: worst %.3e (std units), gate mismatches %d, nan throws %d\n", worst, mismatch_gate,
+              (int)threw);
+  return (worst < 1e-7 && mismatch_gate == 0 && threw) ? 0 : 1;
+}

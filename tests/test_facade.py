@@ -1,0 +1,32 @@
+"""C++ facade (include/uwv_kalman_filters_amd/PoseUKF.hpp): compiles against the
+C ABI (CPU), and on the GPU a 300-epoch run matches the CPU oracle per instance."""
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
+
+
+def _build(tmp):
+    exe = os.path.join(tmp, "facade_test")
+    cmd = ["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(PKG, "include"),
+           os.path.join(HERE, "cpp", "facade_test.cpp"), "-o", exe,
+           "-L", PKG, "-luwvk", "-Wl,-rpath," + PKG,
+           "-L", os.path.join(ROOT, "oracle"), "-loracle", "-Wl,-rpath," + os.path.join(ROOT, "oracle"), "-lm"]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+def test_facade_compiles(tmp_path):
+    _build(str(tmp_path))
+
+
+@pytest.mark.gpu
+def test_facade_matches_oracle(tmp_path):
+    exe = _build(str(tmp_path))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr

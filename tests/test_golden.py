@@ -75,9 +75,9 @@ def test_oracle_reproduces_vel_fixture():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("literal", [False, True])
+@pytest.mark.parametrize("engine_path", ["psp", "dense", "literal"])
 @pytest.mark.parametrize("path", POSE, ids=[os.path.basename(p) for p in POSE])
-def test_engine_reproduces_fixture(path, literal):
+def test_engine_reproduces_fixture(path, engine_path):
     from uwvk import engine
     if not engine.device_available(0):
         pytest.fail("no gfx950 device: the HIP path is mandatory for -m gpu")
@@ -85,7 +85,8 @@ def test_engine_reproduces_fixture(path, literal):
     log = _log(g)
     dof, B = int(g["dof"]), g["mu"].shape[1]
     f = engine.PoseUKFBatch(B, dof)
-    f.set_literal_apply_delta(literal)
+    f.set_dense_sigma(engine_path == "dense")
+    f.set_literal_apply_delta(engine_path == "literal")
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     f.init_from_config(g["pos0"], g["pos_cov"], g["rot0"], g["rot_cov"], cfg, uwv)
     f.set_process_noise_from_config(cfg, log["dt"])

@@ -31,11 +31,18 @@ def orc():
     return oracle_ctypes
 
 
-def _pair(eng, orc, batch, dof=53, mode="C3", epochs=10, literal=False):
+# engine paths: "psp" (default, partitioned sigma points), "dense" (all 2n+1
+# points, exact apply_delta identity), "literal" (dense + ukfom's re-spread)
+PATHS = ["psp", "dense", "literal"]
+
+
+def _pair(eng, orc, batch, dof=53, mode="C3", epochs=10, path="psp"):
     cfg, uwv, log = pose_setup(batch, dof, mode, epochs)
     o = orc.OraclePoseBatch(batch, dof)
     g = eng.PoseUKFBatch(batch, dof)
-    if literal:
+    if path == "dense":
+        g.set_dense_sigma(True)
+    elif path == "literal":
         g.set_literal_apply_delta(True)
     init_both(o, g, cfg, uwv, log)
     return cfg, uwv, log, o, g
@@ -52,9 +59,10 @@ def _check(o, g, dof, tol):
     return se.max(), ce.max()
 
 
+@pytest.mark.parametrize("path", ["psp", "dense"])
 @pytest.mark.parametrize("dof", [53, 26])
-def test_init_and_predict(eng, orc, dof):
-    cfg, uwv, log, o, g = _pair(eng, orc, 6, dof)
+def test_init_and_predict(eng, orc, dof, path):
+    cfg, uwv, log, o, g = _pair(eng, orc, 6, dof, path=path)
     _check(o, g, dof, 1e-15)
     for f in (o, g):
         f.set_rotation_rate(log["gyro"][0])
@@ -62,12 +70,12 @@ def test_init_and_predict(eng, orc, dof):
     _check(o, g, dof, TOL_STEP)
 
 
-@pytest.mark.parametrize("literal", [False, True])
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("dof", [53, 26])
 @pytest.mark.parametrize("kind", ["acceleration", "velocity", "pressure", "water_velocity", "xy", "z",
                                   "efforts", "efforts_vel", "geographic", "delayed_xy"])
-def test_single_update(eng, orc, dof, kind, literal):
-    cfg, uwv, log, o, g = _pair(eng, orc, 5, dof, literal=literal)
+def test_single_update(eng, orc, dof, kind, path):
+    cfg, uwv, log, o, g = _pair(eng, orc, 5, dof, path=path)
     for f in (o, g):
         f.set_rotation_rate(log["gyro"][0])
         f.predict(1e-3)
@@ -107,11 +115,12 @@ def test_single_update(eng, orc, dof, kind, literal):
     _check(o, g, dof, TOL_STEP)
 
 
-@pytest.mark.parametrize("dof,mode,epochs,literal", [(53, "C3", 400, False), (26, "C3", 400, False),
-                                                     (53, "C4", 1000, False), (53, "C3", 400, True),
-                                                     (53, "C4", 1000, True)])
-def test_run_log(eng, orc, dof, mode, epochs, literal):
-    cfg, uwv, log, o, g = _pair(eng, orc, 4, dof, mode, epochs, literal=literal)
+@pytest.mark.parametrize("dof,mode,epochs,path", [(53, "C3", 400, "psp"), (26, "C3", 400, "psp"),
+                                                  (53, "C4", 1000, "psp"), (26, "C4", 1000, "psp"),
+                                                  (53, "C3", 400, "dense"), (53, "C4", 1000, "dense"),
+                                                  (53, "C3", 400, "literal"), (53, "C4", 1000, "literal")])
+def test_run_log(eng, orc, dof, mode, epochs, path):
+    cfg, uwv, log, o, g = _pair(eng, orc, 4, dof, mode, epochs, path=path)
     counts_o = o.run_log(log)
     dlog = g.upload_log(log)
     acc = eng.DeviceBuffer(np.zeros((4, 4), np.uint32))
