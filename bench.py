@@ -38,7 +38,27 @@ F_STEP = F_PRED + F_UPD3  # 1,554,084 flop: predict + Acceleration update (m = 3
 # flops the engine executes per m = 3 update: apply_delta is the exact rotation
 # identity instead of a second LLT + sigma-point GEMM
 F_UPD3_EXEC = 155_237
-F_STEP_EXEC = F_PRED + F_UPD3_EXEC  # 855,614
+F_STEP_EXEC = F_PRED + F_UPD3_EXEC  # 855,614 (literal kernels, UWVK_OPT_DENSE_SIGMA)
+
+
+def psp_flops(n=53, k_pred=15, updates=((6, 3, 7),)):
+    """Flops the PSP kernels execute per step: k-column
+    partial Cholesky, 2k+1 model evaluations, O(n^2) covariance algebra.
+    updates: (k, m, ncols) per update of the step."""
+    def pchol(k):
+        return 2 * sum((k - 1 - j) * (n - j) for j in range(k)) + 3 * k * (n - k // 2)
+    np_ = n * (n + 1) // 2
+    f = pchol(k_pred) + (2 * k_pred + 1) * (120 + 3 * 60)  # points + 3 mean iterations
+    f += 2 * n * k_pred * 3 + 6 * 2 * (2 * k_pred + 1)      # L Delta, ori x ori
+    f += 7 * 6 * n + 4 * np_                                # A-coupled rows, decays + Q'
+    for k, m, nc in updates:
+        f += pchol(k) + (2 * k + 1) * 50 + 2 * m * k * nc + 2 * n * nc * m
+        f += 2 * n * k * m + 2 * n * m * m + 2 * np_ * m + 2 * 9 * n
+    return f
+
+
+F_STEP_PSP = psp_flops()
+F_UPD3_PSP = psp_flops(updates=((6, 3, 7), (6, 3, 3))) - F_STEP_PSP  # one DVL update
 B_STEP = 45_808           # fp64 mu + Sigma read + write
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector = matrix) spec; probe measured 74 (profiles/r01_probe_fp64.txt)
 PEAK_HBM_GBS = 8000.0
@@ -53,6 +73,7 @@ def parse():
     ap.add_argument("--dof", type=int, default=53)
     ap.add_argument("--mode", default="C3", choices=["C3", "C4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dense", action="store_true", help="literal kernels (all 2n+1 sigma points)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     return ap.parse_args()
 
@@ -114,6 +135,8 @@ def main():
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, a.mode, a.dof, first_instance=rank * B)
     f = engine.PoseUKFBatch(B, a.dof, device=local)
+    if a.dense:
+        f.set_dense_sigma(True)
     f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
     f.set_process_noise_from_config(cfg, log["dt"])
     dlog = f.upload_log(log)
@@ -155,11 +178,19 @@ def main():
 
     steps_total = B * world * a.steps
     value = steps_total / wall
-    per_launch_ms = kernel_ms / a.steps
-    flops_launch = B * (F_STEP_EXEC * a.steps + F_UPD3_EXEC * n_dvl) / a.steps
-    flops_ref_launch = B * (F_STEP * a.steps + F_UPD3 * n_dvl) / a.steps
-    achieved_tf = flops_launch / (per_launch_ms * 1e-3) / 1e12
-    workload = "C3-dof%d-b%d" % (a.dof, B) if a.mode == "C3" else "%s-dof%d-b%d" % (a.mode, a.dof, B)
+    # launches in the timed window: the PSP path runs the whole window in one
+    # k_psp_epoch launch (efforts epochs split it); the literal path one per epoch
+    n_eff = int(((window & 0x10) != 0).sum())
+    launches = a.steps if a.dense else 1 + 2 * n_eff
+    per_launch_ms = kernel_ms / launches
+    # roofline.achieved: SURVEY 8(d)'s frozen algorithmic work (reference algorithm)
+    flops_ref = B * (F_STEP * a.steps + F_UPD3 * n_dvl)
+    flops_exec = B * ((F_STEP_EXEC * a.steps + F_UPD3_EXEC * n_dvl) if a.dense
+                      else (F_STEP_PSP * a.steps + F_UPD3_PSP * n_dvl))
+    achieved_tf = flops_ref / (kernel_ms * 1e-3) / 1e12
+    exec_tf = flops_exec / (kernel_ms * 1e-3) / 1e12
+    kname = ("k_pose_epoch<%d>" if a.dense else "k_psp_epoch<%d>") % a.dof
+    workload = "%s-dof%d-b%d%s" % (a.mode, a.dof, B, "-dense" if a.dense else "")
     traffic = roofline_traffic(workload)
     out = {
         "metric": METRIC, "value": value, "unit": "steps/s", "n_gpus": world, "steps": a.steps,
@@ -171,13 +202,16 @@ def main():
                    "global_batch": B * world, "batch_per_gpu": B, "step": "one IMU epoch per instance",
                    "dvl_epochs_in_window": n_dvl, "parallelism": "instance-sharded x%d (no data-path collective)"
                                                                   % world,
-                   "kernel": "k_pose_epoch<%d>" % a.dof},
+                   "path": "dense (all 2n+1 sigma points)" if a.dense else "PSP (partitioned sigma points)",
+                   "kernel": kname},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": traffic,
-                     "kernel_ms_per_launch": per_launch_ms,
-                     "algorithmic_flop_per_launch": flops_launch,
-                     "reference_equivalent_tflops": flops_ref_launch / (per_launch_ms * 1e-3) / 1e12,
-                     "hbm_frac_algorithmic": (B * B_STEP / (per_launch_ms * 1e-3)) / (PEAK_HBM_GBS * 1e9)},
+                     "kernel": kname, "launches": launches, "kernel_ms_per_launch": per_launch_ms,
+                     "algorithmic_flop_per_launch": flops_ref / launches,
+                     "algorithmic_flop_per_step": F_STEP,
+                     "executed_flop_per_step": (F_STEP_EXEC if a.dense else F_STEP_PSP),
+                     "executed_tflops": exec_tf, "executed_frac": exec_tf / PEAK_FP64_TFLOPS,
+                     "hbm_frac_algorithmic": (B * B_STEP * a.steps / (kernel_ms * 1e-3)) / (PEAK_HBM_GBS * 1e9)},
         "ensemble": {"nees_mean_pos_ori_vel": float(stats[-1] / (B * world))},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -152,8 +152,9 @@ UWVK_DEV d4_t mfma_f64(double a, double b, d4_t c) { return __builtin_amdgcn_mfm
 
 // ---------------------------------------------------------------------------
 // Diagnostic phase stamps (build with -DUWVK_STAMPS; never in the product .so).
-// Thread 0 of each workgroup adds the s_memtime delta since its previous stamp
-// to a per-phase sum; read back with uwvk_debug_read_stamps().
+// Thread 0 of every 64th workgroup adds the s_memtime delta since its previous
+// stamp to a per-phase sum (sampling keeps the atomics from serialising the
+// kernel); read back with uwvk_debug_read_stamps().
 // ---------------------------------------------------------------------------
 #ifdef UWVK_STAMPS
 static __device__ unsigned long long uwvk_stamp_sum[64];  // per translation unit
@@ -170,7 +171,7 @@ struct Stamper {
     __builtin_amdgcn_sched_barrier(0);
     const unsigned long long t = stamp_now();
     __builtin_amdgcn_sched_barrier(0);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && (blockIdx.x & 63) == 0) {
       atomicAdd(&uwvk_stamp_sum[ph], t - last);
       atomicAdd(&uwvk_stamp_cnt[ph], 1ull);
     }

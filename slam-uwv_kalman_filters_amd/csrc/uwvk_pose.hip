@@ -32,6 +32,10 @@ struct uwvk_pose {
   uint8_t* d_mask = nullptr;
   uint8_t* d_accepted = nullptr;
   double* d_scratch = nullptr;  // ensemble stats / rotation rate outputs
+  PoseShared* d_shared = nullptr;  // device copy of sh for the PSP kernels
+  double* d_Qp = nullptr;          // dt^2 Q packed (PSP)
+  double qp_dt = -1.0;             // dt d_Qp was made for (-1: stale)
+  std::vector<double> Qh;          // host copy of Q
   PoseShared sh{};
   uwvk_location loc{};
   uwvk_uwv_params uwv{};
@@ -47,6 +51,8 @@ static PoseBufs bufs(const uwvk_pose* h) {
   PoseBufs b;
   b.batch = h->batch; b.mu = h->d_mu; b.sigma = h->d_sigma; b.Q = h->d_Q; b.rot = h->d_rot; b.off = h->d_off;
   b.model = h->d_model; b.uwv = h->d_uwv; b.status = h->d_status;
+  b.shared = h->d_shared;
+  b.Qp = h->d_Qp;
   return b;
 }
 
@@ -62,12 +68,30 @@ static void set_shared(uwvk_pose* h, const uwvk_pose_parameter& p, const uwvk_lo
   h->sh.rm = rm;
   h->sh.inv_rm = 1.0 / rm;
   h->sh.rn_cos = rn * std::cos(loc.latitude);
+  const double taus[8] = {p.gyro_bias_tau, p.acc_bias_tau, p.inertia_tau, p.lin_damping_tau, p.quad_damping_tau,
+                          p.water_velocity_tau, p.adcp_bias_tau, p.water_density_tau};
+  for (int k = 0; k < 8; k++) h->sh.ntau[k] = -1.0 / taus[k];
   h->sh.uwv_weight = uwv.weight;
   h->sh.uwv_buoyancy = uwv.buoyancy;
   for (int k = 0; k < 3; k++) {
     h->sh.cog[k] = uwv.distance_body2centerofgravity[k];
     h->sh.cob[k] = uwv.distance_body2centerofbuoyancy[k];
   }
+}
+
+// PSP kernels read the batch-shared parameters and dt^2 Q (packed) from device memory
+static hipError_t upload_shared(uwvk_pose* h, double dt) {
+  hipError_t e = hipMemcpyAsync(h->d_shared, &h->sh, sizeof(PoseShared), hipMemcpyHostToDevice, h->stream);
+  if (e != hipSuccess || dt == h->qp_dt) return e;
+  const int n = h->dof;
+  std::vector<double> qp((size_t)n * (n + 1) / 2);
+  const double dt2 = dt * dt;
+  for (int i = 0, k = 0; i < n; i++)
+    for (int j = 0; j <= i; j++) qp[k++] = dt2 * (h->Qh.empty() ? 0.0 : h->Qh[(size_t)i * n + j]);
+  e = hipMemcpyAsync(h->d_Qp, qp.data(), qp.size() * 8, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);  // qp is a local
+  if (e == hipSuccess) h->qp_dt = dt;
+  return e;
 }
 
 #define HIPCHK(x)                              \
@@ -104,6 +128,8 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
             hipMalloc(&h->d_uwv, 108 * 8) == hipSuccess && hipMalloc(&h->d_status, B * 4) == hipSuccess &&
             hipMalloc(&h->d_meas, B * 74 * 8) == hipSuccess && hipMalloc(&h->d_mask, B) == hipSuccess &&
             hipMalloc(&h->d_accepted, B) == hipSuccess && hipMalloc(&h->d_scratch, (B * 3 + 256) * 8) == hipSuccess &&
+            hipMalloc(&h->d_shared, sizeof(PoseShared)) == hipSuccess &&
+            hipMalloc(&h->d_Qp, n * (n + 1) / 2 * 8) == hipSuccess &&
             hipEventCreate(&h->ev0) == hipSuccess && hipEventCreate(&h->ev1) == hipSuccess;
   if (!ok) {
     uwvk_pose_destroy(h);
@@ -125,7 +151,7 @@ void uwvk_pose_destroy(uwvk_pose* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_Q, (void*)h->d_rot, (void*)h->d_off,
                   (void*)h->d_model, (void*)h->d_uwv, (void*)h->d_status, (void*)h->d_meas, (void*)h->d_mask,
-                  (void*)h->d_accepted, (void*)h->d_scratch})
+                  (void*)h->d_accepted, (void*)h->d_scratch, (void*)h->d_shared, (void*)h->d_Qp})
     if (p) (void)hipFree(p);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -201,6 +227,14 @@ uwvk_status uwvk_pose_set_process_noise_from_config(uwvk_pose* h, const uwvk_pos
 uwvk_status uwvk_pose_set_process_noise(uwvk_pose* h, const double* Q) {
   if (!h || !Q) return UWVK_EINVAL;
   HIPCHK(hipMemcpyAsync(h->d_Q, Q, (size_t)h->dof * h->dof * 8, hipMemcpyHostToDevice, h->stream));
+  h->Qh.assign(Q, Q + (size_t)h->dof * h->dof);
+  h->qp_dt = -1.0;
+  {
+    const int n = h->dof, o = 3, wv = n == 53 ? 46 : 19;
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) h->sh.q_ori[r * 3 + c] = Q[(o + r) * n + o + c];
+    for (int k = 0; k < 4; k++) h->sh.q_wv[k] = Q[(wv + k) * n + wv + k];
+  }
   HIPCHK(hipStreamSynchronize(h->stream));
   h->has_Q = true;
   return UWVK_OK;
@@ -221,8 +255,11 @@ uwvk_status uwvk_pose_predict(uwvk_pose* h, double dt) {
   PoseShared sh = h->sh;
   if (use_dense(h))
     HIPCHK(launch_pose_predict(h->dof, h->stream, b, sh, dt));
-  else
+  else {
+    HIPCHK(upload_shared(h, dt));
+    b = bufs(h);
     HIPCHK(launch_psp_predict(h->dof, h->stream, b, sh, dt));
+  }
   return UWVK_OK;
 }
 
@@ -269,8 +306,10 @@ static uwvk_status launch_update(uwvk_pose* h, int m, const double* mu, const do
   PoseShared sh = h->sh;
   if (K == MK_EFFORTS || use_dense(h))
     HIPCHK(launch_pose_update(h->dof, K, h->stream, b, sh, ma, m));
-  else
+  else {
+    HIPCHK(upload_shared(h, h->qp_dt));
     HIPCHK(launch_psp_update(h->dof, K, h->stream, b, sh, ma, m));
+  }
   if (accepted) HIPCHK(hipMemcpyAsync(accepted, h->d_accepted, (size_t)B, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return UWVK_OK;
@@ -398,6 +437,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     HIPCHK(hipStreamSynchronize(h->stream));
     hf = fl.data();
   }
+  HIPCHK(upload_shared(h, log->dt));
   int64_t e = first;
   while (e < first + count) {
     int64_t r = e;

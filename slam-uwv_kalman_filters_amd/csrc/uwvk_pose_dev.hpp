@@ -31,6 +31,11 @@ struct PoseShared {
   double lat0, lon0, rm, rn_cos, inv_rm;  // GeographicProjection [EXT]: lat = lat0 + x/rm, lon = lon0 - y/rn_cos
   double uwv_weight, uwv_buoyancy, cog[3], cob[3];
   int literal_apply_delta;  // 1: ukfom's literal re-spread (Cholesky + GEMM); 0: exact T Sigma T^T form
+  // -1/tau of the first-order Markov states (host-computed; IEEE division, so
+  // bitwise equal to evaluating (-1.0 / tau) in the process model)
+  double ntau[8];  // gyro bias, acc bias, inertia, lin damping, quad damping, water velocity, ADCP bias, density
+  double q_ori[9];  // Q's orientation block (PSP kernels; host copy of process_noise_cov)
+  double q_wv[4];   // Q's water-velocity / water-velocity-below diagonal
 };
 
 struct PoseBufs {
@@ -43,6 +48,8 @@ struct PoseBufs {
   double* model;      // [batch][27] the shared DynamicModel's (surge,sway,yaw) blocks (PoseUKF.cpp:173)
   const double* uwv;  // [108] base M, D_l, D_q (row-major 6x6)
   uint32_t* status;   // [batch]
+  const PoseShared* shared;  // device copy of the handle's PoseShared (PSP kernels)
+  const double* Qp;          // dt^2 Q, packed lower triangle (PSP kernels; host-made per dt)
 };
 
 template <int DOF>

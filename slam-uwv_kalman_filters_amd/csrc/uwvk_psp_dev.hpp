@@ -47,6 +47,10 @@ struct alignas(16) PspSmem {
   double stg[PG<DOF>::STG];
   double W[PG<DOF>::WS];
   double vec[64];         // delta / small broadcasts
+  double ad[64];          // predict: diagonal of the process Jacobian A per DOF
+  double off[32];         // per-instance model-parameter / density offsets (loaded once)
+  double H[32];           // update: affine Jacobian H[i][t] (M x NC)
+  double P[64];           // update: P = H L_a (M x K), then Dz/2 - P (K x M)
 };
 
 UWVK_DEV constexpr int pidx(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
@@ -58,6 +62,15 @@ UWVK_DEV void unpack(int e, int& i, int& j) {
   if (r * (r + 1) / 2 > e) r--;
   i = r;
   j = e - r * (r + 1) / 2;
+}
+
+// lane id that the optimiser cannot treat as loop-invariant: phases inside the
+// multi-epoch loop recompute their lane-derived addresses instead of having
+// LICM hoist hundreds of them out of the epoch loop (register blow-up)
+UWVK_DEV int olane() {
+  int l = (int)threadIdx.x;
+  asm volatile("" : "+v"(l));
+  return l;
 }
 
 UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
@@ -187,37 +200,37 @@ UWVK_DEV double proc_vect(int s, const double* mu, const PoseShared& sh, const P
   if (s < 3) return x + dt * mu[L::s_vel + s];
   if (s >= L::s_vel && s < L::s_vel + 3) return x + dt * mu[L::s_acc + s - L::s_vel];
   if (s >= L::s_bg && s < L::s_bg + 3) {
-    const double d = (-1.0 / P.gyro_bias_tau) * (x - P.gyro_bias_offset[s - L::s_bg]);
+    const double d = sh.ntau[0] * (x - P.gyro_bias_offset[s - L::s_bg]);
     return x + dt * d;
   }
   if (s >= L::s_ba && s < L::s_ba + 3) {
-    const double d = (-1.0 / P.acc_bias_tau) * (x - P.acc_bias_offset[s - L::s_ba]);
+    const double d = sh.ntau[1] * (x - P.acc_bias_offset[s - L::s_ba]);
     return x + dt * d;
   }
   if constexpr (L::has_params) {
     if (s >= L::s_inertia && s < L::s_inertia + 9) {
-      const double d = (-1.0 / P.inertia_tau) * (x - c.off[s - L::s_inertia]);
+      const double d = sh.ntau[2] * (x - c.off[s - L::s_inertia]);
       return x + dt * d;
     }
     if (s >= L::s_lin && s < L::s_lin + 9) {
-      const double d = (-1.0 / P.lin_damping_tau) * (x - c.off[9 + s - L::s_lin]);
+      const double d = sh.ntau[3] * (x - c.off[9 + s - L::s_lin]);
       return x + dt * d;
     }
     if (s >= L::s_quad && s < L::s_quad + 9) {
-      const double d = (-1.0 / P.quad_damping_tau) * (x - c.off[18 + s - L::s_quad]);
+      const double d = sh.ntau[4] * (x - c.off[18 + s - L::s_quad]);
       return x + dt * d;
     }
   }
   if (s >= L::s_wv && s < L::s_wv + 4) {
-    const double d = (-1.0 / P.water_velocity_tau) * x;
+    const double d = sh.ntau[5] * x;
     return x + dt * d;
   }
   if (s >= L::s_badcp && s < L::s_badcp + 2) {
-    const double d = (-1.0 / P.adcp_bias_tau) * x;
+    const double d = sh.ntau[6] * x;
     return x + dt * d;
   }
   if (s == L::s_rho) {
-    const double d = (-1.0 / P.water_density_tau) * (x - c.off[27]);
+    const double d = sh.ntau[7] * (x - c.off[27]);
     return x + dt * d;
   }
   return x;  // acceleration, gravity
@@ -227,17 +240,16 @@ UWVK_DEV double proc_vect(int s, const double* mu, const PoseShared& sh, const P
 template <int DOF>
 UWVK_DEV double proc_diag(int d, const PoseShared& sh, double dt) {
   using L = Lay<DOF>;
-  const uwvk_pose_parameter& P = sh.p;
-  if (d >= L::d_bg && d < L::d_bg + 3) return 1.0 + dt * (-1.0 / P.gyro_bias_tau);
-  if (d >= L::d_ba && d < L::d_ba + 3) return 1.0 + dt * (-1.0 / P.acc_bias_tau);
+  if (d >= L::d_bg && d < L::d_bg + 3) return 1.0 + dt * sh.ntau[0];
+  if (d >= L::d_ba && d < L::d_ba + 3) return 1.0 + dt * sh.ntau[1];
   if constexpr (L::has_params) {
-    if (d >= L::d_inertia && d < L::d_inertia + 9) return 1.0 + dt * (-1.0 / P.inertia_tau);
-    if (d >= L::d_lin && d < L::d_lin + 9) return 1.0 + dt * (-1.0 / P.lin_damping_tau);
-    if (d >= L::d_quad && d < L::d_quad + 9) return 1.0 + dt * (-1.0 / P.quad_damping_tau);
+    if (d >= L::d_inertia && d < L::d_inertia + 9) return 1.0 + dt * sh.ntau[2];
+    if (d >= L::d_lin && d < L::d_lin + 9) return 1.0 + dt * sh.ntau[3];
+    if (d >= L::d_quad && d < L::d_quad + 9) return 1.0 + dt * sh.ntau[4];
   }
-  if (d >= L::d_wv && d < L::d_wv + 4) return 1.0 + dt * (-1.0 / P.water_velocity_tau);
-  if (d >= L::d_badcp && d < L::d_badcp + 2) return 1.0 + dt * (-1.0 / P.adcp_bias_tau);
-  if (d == L::d_rho) return 1.0 + dt * (-1.0 / P.water_density_tau);
+  if (d >= L::d_wv && d < L::d_wv + 4) return 1.0 + dt * sh.ntau[5];
+  if (d >= L::d_badcp && d < L::d_badcp + 2) return 1.0 + dt * sh.ntau[6];
+  if (d == L::d_rho) return 1.0 + dt * sh.ntau[7];
   return 1.0;
 }
 // coupled column of row d (pos -> vel, vel -> acc) or -1
@@ -252,28 +264,31 @@ struct PredRows {
 // ---------------------------------------------------------------------------
 // predictionStepImpl (PoseUKF.cpp:446-474) + ukf::predict, PSP form
 // ---------------------------------------------------------------------------
+// Q: process_noise_cov (DOF x DOF); Qp: dt^2 Q in packed order (host-made per dt)
 template <int DOF>
-UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q) {
+UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q,
+                          const double* Qp, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   using G = PG<DOF>;
   constexpr int K = G::KP;
-  const int l = lane_id();
+  const int l = olane();
   const double dt = pc.dt, dt2 = dt * dt;
   // process-noise shaping from the pre-predict mean (PoseUKF.cpp:448-460)
   if (l < 9) {
     double R[9];
     qmatrix(sm.mu + L::s_quat, R);
-    const int r = l / 3, c = l % 3, o = L::d_ori;
+    const int r = l / 3, c = l % 3;
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       double u = 0.0;
 #pragma unroll
-      for (int m = 0; m < 3; m++) u += R[r * 3 + m] * Q[(o + m) * DOF + o + k];
+      for (int m = 0; m < 3; m++) u += R[r * 3 + m] * sh.q_ori[m * 3 + k];
       s += u * R[c * 3 + k];
     }
     sm.vec[48 + l] = s;
   }
+  if (l < DOF) sm.ad[l] = proc_diag<DOF>(l, sh, dt);
   const double vs0 = sm.mu[L::s_vel], vs1 = sm.mu[L::s_vel + 1], vs2 = 10 * sm.mu[L::s_vel + 2];
   const double wv_add = sh.p.water_velocity_scale * (vs0 * vs0 + vs1 * vs1 + vs2 * vs2) * dt;
   // partial Cholesky and row staging
@@ -281,6 +296,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   const bool ok = pchol<DOF, K>(sm.S, l, a);
   stage_rows<PredRows, K>(sm.stg, l, a);
   psync();
+  UWVK_STAMP(20);
   // sigma points: lanes < 2K plus the centre lane 2K; orientation output only
   const bool pt = l < 2 * K, ctr = l == 2 * K;
   double o[4];
@@ -289,6 +305,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     gen_rows<PredRows, DOF, K>(sm.mu, sm.stg, l, x);
     proc_orientation<DOF>(x, sh, pc, o);
   }
+  UWVK_STAMP(21);
   // manifold mean of the orientations (ukfom: ref = X_0, Gauss-Newton, |d| <= 1e-6)
   constexpr double wc = 1.0 + 2.0 * (DOF - K);
   double mq[4];
@@ -315,6 +332,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       nrm = sqrt(nrm);
     } while (nrm > 1e-6 && ++it < 10000);
   }
+  UWVK_STAMP(22);
   // deviations; ori x ori block; Delta_j = d_{j+} - d_{j-}
   double d[3];
   qboxminus(o, mq, d);
@@ -354,6 +372,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       X[i] = 0.5 * (cp >= 0 ? (ar * Y[i] + dt * yc) : ar * Y[i]);
     }
   }
+  UWVK_STAMP(23);
   // rows/cols coupled by A (pos, vel): new values into registers first
   constexpr int pv[6] = {0, 1, 2, 6, 7, 8};
   double nv[6];
@@ -379,32 +398,42 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     for (int i = 0; i < 3; i++) sm.W[64 + l * 3 + i] = X[i];
   }
   psync();
-  // flat pass: ori rows/cols, decays, + Q'
-#pragma unroll 1
-  for (int t = 0; t < G::NSLOT; t++) {
-    const int e = l + 64 * t;
-    if (e < G::NP) {
-      int i, j;
-      unpack(e, i, j);
-      const bool io = i >= 3 && i < 6, jo = j >= 3 && j < 6;
-      double v, q = Q[i * DOF + j];
-      if (io && jo) {
-        const int a2 = i - 3, b2 = j - 3;
-        v = oo[a2 * (a2 + 1) / 2 + b2];
-        q = sm.vec[48 + a2 * 3 + b2];
-      } else if (io) {
-        v = sm.W[64 + j * 3 + (i - 3)];
-      } else if (jo) {
-        v = sm.W[64 + i * 3 + (j - 3)];
-      } else if (proc_couple(i) >= 0 || proc_couple(j) >= 0) {
-        v = sm.S[e];
-      } else {
-        v = proc_diag<DOF>(i, sh, dt) * proc_diag<DOF>(j, sh, dt) * sm.S[e];
+  UWVK_STAMP(24);
+  // flat pass: ori rows/cols, decays, + Q' (packed dt^2 Q loads issued up front)
+  {
+    double qv[G::NSLOT];
+#pragma unroll
+    for (int t = 0; t < G::NSLOT; t++) {
+      const int e = l + 64 * t;
+      qv[t] = e < G::NP ? Qp[e] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < G::NSLOT; t++) {
+      const int e = l + 64 * t;
+      if (e < G::NP) {
+        int i, j;
+        unpack(e, i, j);
+        const bool io = i >= 3 && i < 6, jo = j >= 3 && j < 6;
+        double v, q = qv[t];
+        if (io && jo) {
+          const int a2 = i - 3, b2 = j - 3;
+          v = oo[a2 * (a2 + 1) / 2 + b2];
+          q = dt2 * sm.vec[48 + a2 * 3 + b2];
+        } else if (io) {
+          v = sm.W[64 + j * 3 + (i - 3)];
+        } else if (jo) {
+          v = sm.W[64 + i * 3 + (j - 3)];
+        } else if (proc_couple(i) >= 0 || proc_couple(j) >= 0) {
+          v = sm.S[e];
+        } else {
+          v = sm.ad[i] * sm.ad[j] * sm.S[e];
+        }
+        if (i == j && i >= L::d_wv && i < L::d_wv + 4) q = dt2 * (sh.q_wv[i - L::d_wv] + wv_add);
+        sm.S[e] = v + q;
       }
-      if (i == j && ((i >= L::d_wv && i < L::d_wv + 2) || (i >= L::d_wvb && i < L::d_wvb + 2))) q = q + wv_add;
-      sm.S[e] = v + dt2 * q;
     }
   }
+  UWVK_STAMP(25);
   // new mean: vect parts f(mu), orientation the manifold mean
   double mv = 0.0;
   if (l < L::store && !(l >= 3 && l < 7)) mv = proc_vect<DOF>(l, sm.mu, sh, pc);
@@ -412,6 +441,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   if (l < L::store && !(l >= 3 && l < 7)) sm.mu[l] = mv;
   if (l < 4) sm.mu[3 + l] = mq[l];
   psync();
+  UWVK_STAMP(26);
   return ok;
 }
 
@@ -524,11 +554,11 @@ struct PZ {  // measurementZPosition, PoseUKF.cpp:100-105: linear (k = 0)
 // ---------------------------------------------------------------------------
 template <int DOF, class HM>
 UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const double (&Rm)[HM::M * HM::M], int gate,
-                         const HM& hm, bool* ok) {
+                         const HM& hm, bool* ok, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   using G = PG<DOF>;
   constexpr int M = HM::M, K = HM::K, NC = HM::NC, KA = K > 0 ? K : 1;
-  const int l = lane_id();
+  const int l = olane();
   double a[KA];
   bool cok = true;
   if constexpr (K > 0) {
@@ -536,6 +566,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     stage_rows<HM, K>(sm.stg, l, a);
     psync();
   }
+  UWVK_STAMP(30);
   const bool pt = l < 2 * K;
   double zp[M];
   {
@@ -575,20 +606,26 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       for (int i = 0; i < M; i++) sm.W[(l >> 1) * M + i] = zp[i] - zn[i];
     }
   }
-  // affine part: H at mu, P = H L_a, G = Sigma H^T (lane r)
-  double H[M][NC];
-  hm.jac(sm.mu, H);
-  double P[M][KA];
-  if constexpr (K > 0) {
+  UWVK_STAMP(31);
+  // affine part: H at mu (staged), P = H L_a and Qp = Dz/2 - P lane-parallel,
+  // G = Sigma H^T (lane r).  Uniform matrices live in LDS, not in VGPRs.
+  if (l == 0) {
+    double H[M][NC];
+    hm.jac(sm.mu, H);
 #pragma unroll
     for (int i = 0; i < M; i++)
 #pragma unroll
-      for (int j = 0; j < K; j++) {
-        double s = 0.0;
+      for (int t = 0; t < NC; t++) sm.H[i * NC + t] = H[i][t];
+  }
+  psync();
+  if constexpr (K > 0) {
+    if (l < M * K) {
+      const int i = l / K, j = l - (l / K) * K;
+      double s = 0.0;
 #pragma unroll
-        for (int t = 0; t < NC; t++) s += H[i][t] * sm.stg[row_pos(HM::rows, HM::cols[t]) * K + j];
-        P[i][j] = s;
-      }
+      for (int t = 0; t < NC; t++) s += sm.H[i * NC + t] * sm.stg[row_pos(HM::rows, HM::cols[t]) * K + j];
+      sm.P[i * K + j] = s;
+    }
   }
   const int rl = l < DOF ? l : DOF - 1;
   double Gr[M];
@@ -598,9 +635,10 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   for (int t = 0; t < NC; t++) {
     const double s = sm.S[pidx(rl, HM::cols[t])];
 #pragma unroll
-    for (int i = 0; i < M; i++) Gr[i] += s * H[i][t];
+    for (int i = 0; i < M; i++) Gr[i] += s * sm.H[i * NC + t];
   }
   psync();
+  UWVK_STAMP(32);
   // C_r = G_r + sum_j L[r][j] (Dz_j / 2 - P[:, j])
   double C[M];
 #pragma unroll
@@ -608,7 +646,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     double s = Gr[i];
     if constexpr (K > 0) {
 #pragma unroll
-      for (int j = 0; j < K; j++) s += a[j] * (0.5 * sm.W[j * M + i] - P[i][j]);
+      for (int j = 0; j < K; j++) s += a[j] * (0.5 * sm.W[j * M + i] - sm.P[i * K + j]);
     }
     C[i] = s;
   }
@@ -619,11 +657,11 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     for (int j = 0; j <= i; j++) {
       double hg = 0.0;
 #pragma unroll
-      for (int t = 0; t < NC; t++) hg += H[i][t] * readlane_d(Gr[j], HM::cols[t]);
+      for (int t = 0; t < NC; t++) hg += sm.H[i * NC + t] * readlane_d(Gr[j], HM::cols[t]);
       double pp = 0.0;
       if constexpr (K > 0) {
 #pragma unroll
-        for (int k = 0; k < K; k++) pp += P[i][k] * P[j][k];
+        for (int k = 0; k < K; k++) pp += sm.P[i * K + k] * sm.P[j * K + k];
       }
       const double s = S[i * M + j] + (hg - pp);
       S[i * M + j] = s + Rm[i * M + j];
@@ -653,6 +691,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   *ok = cok;
   const bool accept = gate == 0 ? true : !(d2 > kD2P95);
   if (!accept) return false;
+  UWVK_STAMP(33);
   // Sigma -= C K^T (flat), delta = K nu
   psync();
   if (l < DOF) {
@@ -680,6 +719,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     }
   }
   psync();
+  UWVK_STAMP(34);
   // apply_delta, exact nav-frame form: mu <- mu [+] delta, Sigma <- T Sigma T^T
   {
     double R[9];
@@ -727,6 +767,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     if (l < 4) sm.mu[3 + l] = qn[l];
     psync();
   }
+  UWVK_STAMP(35);
   return true;
 }
 

@@ -35,6 +35,7 @@ UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
     if (e < G::NP) sm.S[e] = v[t];
   }
   if (l < Lay<DOF>::store) sm.mu[l] = m;
+  if (l < 28) sm.off[l] = b.off[inst * 28 + l];
   psync();
 }
 
@@ -68,29 +69,29 @@ UWVK_DEV void copy_zr(const double* zin, const double* Rin, double (&z)[M], doub
 // one measurement update of kind KIND on instance inst (PSP form)
 template <int DOF, int KIND>
 UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, const double* zin, const double* Rin,
-                        const MeasArgs& ma, bool* ok) {
+                        const MeasArgs& ma, bool* ok, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   if constexpr (KIND == MK_ACC) {
     double z[3], R[9];
     copy_zr<3>(zin, Rin, z, R);
-    return psp_update<DOF>(sm, z, R, 0, PAcc<DOF>{}, ok);
+    return psp_update<DOF>(sm, z, R, 0, PAcc<DOF>{}, ok, st);
   } else if constexpr (KIND == MK_VEL) {
     double z[3], R[9];
     copy_zr<3>(zin, Rin, z, R);
-    return psp_update<DOF>(sm, z, R, 0, PVel<DOF>{}, ok);
+    return psp_update<DOF>(sm, z, R, 0, PVel<DOF>{}, ok, st);
   } else if constexpr (KIND == MK_PRESSURE) {
     double z[1], R[1];
     copy_zr<1>(zin, Rin, z, R);
     PPressure<DOF> h;
     h.h.s[0] = ma.v3[0]; h.h.s[1] = ma.v3[1]; h.h.s[2] = ma.v3[2];
     h.h.patm = sh.p.atmospheric_pressure;
-    return psp_update<DOF>(sm, z, R, 0, h, ok);
+    return psp_update<DOF>(sm, z, R, 0, h, ok, st);
   } else if constexpr (KIND == MK_WATER) {
     double z[2], R[4];
     copy_zr<2>(zin, Rin, z, R);
     PWater<DOF> h;
     h.cw = ma.extra ? ma.extra[inst] : 0.0;
-    return psp_update<DOF>(sm, z, R, 1, h, ok);
+    return psp_update<DOF>(sm, z, R, 1, h, ok, st);
   } else if constexpr (KIND == MK_XY || KIND == MK_GEO || KIND == MK_DELAYED) {
     double z[2], R[4];
     copy_zr<2>(zin, Rin, z, R);
@@ -108,12 +109,12 @@ UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, co
       z[0] = zin[0] + (sm.mu[L::s_pos] - ma.extra[2 * inst]);
       z[1] = zin[1] + (sm.mu[L::s_pos + 1] - ma.extra[2 * inst + 1]);
     }
-    return psp_update<DOF>(sm, z, R, gate, PXY<DOF>{}, ok);
+    return psp_update<DOF>(sm, z, R, gate, PXY<DOF>{}, ok, st);
   } else {
     static_assert(KIND == MK_Z, "PSP update kind");
     double z[1], R[1];
     copy_zr<1>(zin, Rin, z, R);
-    return psp_update<DOF>(sm, z, R, 0, PZ<DOF>{}, ok);
+    return psp_update<DOF>(sm, z, R, 0, PZ<DOF>{}, ok, st);
   }
 }
 
@@ -125,8 +126,8 @@ __global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, d
   ProcCtx pc;
   for (int k = 0; k < 3; k++) pc.w[k] = b.rot[inst * 3 + k];
   pc.dt = dt;
-  pc.off = b.off + inst * 28;
-  const bool ok = psp_predict<DOF>(sm, sh, pc, b.Q);
+  pc.off = sm.off;
+  const bool ok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp);
   if (!ok && lane_id() == 0) b.status[inst] |= UWVK_ST_NOTPD;
   store_psp<DOF>(sm, b, inst);
 }
@@ -158,11 +159,26 @@ __global__ __launch_bounds__(64) void k_psp_update(PoseBufs b, PoseShared sh, Me
   store_psp<DOF>(sm, b, inst);
 }
 
+// batch-shared parameters read through a pointer laundered once per epoch:
+// nothing derived from them is hoisted out of the epoch loop (VGPR pressure)
+UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
+  const PoseShared* p = b.shared;
+  asm volatile("" : "+s"(p));
+  return *p;
+}
+
 template <int DOF>
-__global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh, EpochArgs ea) {
+__global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const int64_t inst = blockIdx.x, B = b.batch;
+#ifdef UWVK_STAMPS
+  Stamper stamper;
+  Stamper* st = &stamper;
+#else
+  Stamper* st = nullptr;
+#endif
   load_psp<DOF>(sm, b, inst);
+  UWVK_STAMP(40);
   bool ok = true, nan = false;
   uint32_t cnt[4] = {0, 0, 0, 0};
   MeasArgs ma{};
@@ -171,22 +187,38 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh, Epo
   ProcCtx pc;
   for (int k = 0; k < 3; k++) pc.w[k] = w[k];
   pc.dt = ea.dt;
-  pc.off = b.off + inst * 28;
+  pc.off = sm.off;
+  // the next epoch's IMU inputs are prefetched one epoch ahead (their load
+  // latency overlaps this epoch's arithmetic)
+  uint32_t fl_n = 0;
+  double g_n[3] = {0, 0, 0}, a_n[3] = {0, 0, 0};
+  const int64_t e_end = ea.first + ea.count;
+  auto fetch = [&](int64_t e) {
+    fl_n = ea.flags[e];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      g_n[k] = ea.gyro[(e * B + inst) * 3 + k];
+      a_n[k] = ea.acc[(e * B + inst) * 3 + k];
+    }
+  };
+  if (ea.count > 0) fetch(ea.first);
 #pragma unroll 1
-  for (int64_t e = ea.first; e < ea.first + ea.count; e++) {
-    const uint32_t fl = ea.flags[e];
-    const double* g = ea.gyro + (e * B + inst) * 3;
+  for (int64_t e = ea.first; e < e_end; e++) {
+    const uint32_t fl = fl_n;
+    const double g[3] = {g_n[0], g_n[1], g_n[2]}, za[3] = {a_n[0], a_n[1], a_n[2]};
+    if (e + 1 < e_end) fetch(e + 1);
     if (all_finite(g, 3)) {  // integrateMeasurement(RotationRate): checkMeasurment, then store
       for (int k = 0; k < 3; k++) { w[k] = g[k]; pc.w[k] = g[k]; }
     } else {
       nan = true;
     }
-    bool sok = psp_predict<DOF>(sm, sh, pc, b.Q);
+    const PoseShared& sh = shared_for_epoch(b);
+    UWVK_STAMP(41);
+    bool sok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, st);
     ok = ok && sok;
     if (fl & UWVK_EV_ACC) {
-      const double* z = ea.acc + (e * B + inst) * 3;
-      if (all_finite(z, 3)) {
-        do_update<DOF, MK_ACC>(sm, sh, inst, z, ea.acc_cov, ma, &sok);
+      if (all_finite(za, 3)) {
+        do_update<DOF, MK_ACC>(sm, sh, inst, za, ea.acc_cov, ma, &sok, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -195,7 +227,7 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh, Epo
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + inst) * 3;
       if (all_finite(z, 3)) {
-        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, inst, z, ea.dvl_cov, ma, &sok);
+        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, inst, z, ea.dvl_cov, ma, &sok, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -276,3 +308,17 @@ hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const Po
 }
 
 }  // namespace uwvk
+
+#ifdef UWVK_STAMPS
+// diagnostic build only: per-phase cycle sums of the PSP epoch kernel
+extern "C" int uwvk_debug_read_stamps_psp(unsigned long long* sum, unsigned long long* cnt, int reset) {
+  if (hipMemcpyFromSymbol(sum, HIP_SYMBOL(uwvk::uwvk_stamp_sum), 64 * 8) != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(uwvk::uwvk_stamp_cnt), 64 * 8) != hipSuccess) return 1;
+  if (reset) {
+    unsigned long long z[64] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(uwvk::uwvk_stamp_sum), z, 64 * 8) != hipSuccess) return 1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(uwvk::uwvk_stamp_cnt), z, 64 * 8) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif

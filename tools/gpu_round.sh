@@ -12,6 +12,8 @@ timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > "$OUT/p
 tail -2 "$OUT/pytest_gpu.log"
 timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { cat "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
+timeout -k 10 300 python bench.py --dense --no-cpu-baseline --steps 50 > "$OUT/bench_dense.json" 2>> "$OUT/bench.err" || { cat "$OUT/bench.err"; exit 1; }
+cat "$OUT/bench_dense.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps $SP --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1 || { tail -30 "$OUT/prof.log"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps $SP --warmup 2 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1 || { tail -30 "$OUT/pmc_fetch.log"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps $SP --warmup 2 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1 || { tail -30 "$OUT/pmc_write.log"; exit 1; }

@@ -20,27 +20,37 @@ NAMES = {0: "predict: Q' + Cholesky", 1: "predict: sigma gen + process model", 2
          3: "predict: deviations + MFMA GEMM + store", 4: "update: Cholesky", 5: "update: gen + h + z-mean + S",
          6: "update: cross-cov C", 7: "update: gain + Sigma -= C K^T", 8: "apply_delta: Cholesky",
          9: "apply_delta: gen + shift", 10: "apply_delta: MFMA GEMM + store", 11: "load mu/Sigma",
-         12: "epoch bookkeeping", 13: "store mu/Sigma"}
+         12: "epoch bookkeeping", 13: "store mu/Sigma",
+         20: "psp predict: partial Cholesky + stage", 21: "psp predict: points (orientation)",
+         22: "psp predict: manifold mean", 23: "psp predict: ori blocks + L Delta", 24: "psp predict: A-coupled rows",
+         25: "psp predict: flat pass (decay, ori, Q')", 26: "psp predict: mean update",
+         30: "psp update: partial Cholesky + stage", 31: "psp update: points + zbar + S_nl",
+         32: "psp update: H, P, G", 33: "psp update: C, S, gain", 34: "psp update: Sigma -= C K^T",
+         35: "psp update: apply_delta", 40: "psp load", 41: "psp epoch inputs"}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=65536)
 ap.add_argument("--epochs", type=int, default=20)
+ap.add_argument("--dense", action="store_true", help="literal kernels (k_pose_epoch) instead of PSP")
 a = ap.parse_args()
 L = engine.lib(os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "libuwvk_stamps.so"))
 cfg, uwv = synth.default_pose_config(), synth.default_uwv()
 log = synth.make_pose_log(a.batch, a.epochs + 1, "C3")
 f = engine.PoseUKFBatch(a.batch)
+if a.dense:
+    f.set_dense_sigma(True)
+read = L.uwvk_debug_read_stamps if a.dense else L.uwvk_debug_read_stamps_psp
 f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
 f.set_process_noise_from_config(cfg, log["dt"])
 d = f.upload_log(log)
 f.run_log(d, 0, 1)
 s = np.zeros(64, np.uint64)
 c = np.zeros(64, np.uint64)
-L.uwvk_debug_read_stamps(s.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p), 1)
+read(s.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p), 1)
 f.timer_start()
 f.run_log(d, 1, a.epochs)
 ms = f.timer_stop()
-L.uwvk_debug_read_stamps(s.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p), 1)
+read(s.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p), 1)
 tot = float(s.sum())
 print("diagnostic build: %.2f ms/epoch (stamped, serialised)" % (ms / a.epochs))
 print("%-45s %14s %8s" % ("phase", "cycles/call", "share"))
