@@ -11,6 +11,7 @@
 #include "uwvk_psp.hpp"
 #include "uwvk_host.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -33,7 +34,8 @@ struct uwvk_pose {
   uint8_t* d_accepted = nullptr;
   double* d_scratch = nullptr;  // ensemble stats / rotation rate outputs
   PoseShared* d_shared = nullptr;  // device copy of sh for the PSP kernels
-  double* d_Qp = nullptr;          // dt^2 Q packed (PSP)
+  double* d_Qp = nullptr;          // {A_ii A_jj, dt^2 Q_ij} per packed entry (PSP)
+  double* d_qband = nullptr;       // [128] dt^2 Q band of rows >= 9 (PSP)
   double qp_dt = -1.0;             // dt d_Qp was made for (-1: stale)
   std::vector<double> Qh;          // host copy of Q
   PoseShared sh{};
@@ -53,6 +55,7 @@ static PoseBufs bufs(const uwvk_pose* h) {
   b.model = h->d_model; b.uwv = h->d_uwv; b.status = h->d_status;
   b.shared = h->d_shared;
   b.Qp = h->d_Qp;
+  b.qband = h->d_qband;
   return b;
 }
 
@@ -67,10 +70,13 @@ static void set_shared(uwvk_pose* h, const uwvk_pose_parameter& p, const uwvk_lo
   h->sh.lon0 = loc.longitude;
   h->sh.rm = rm;
   h->sh.inv_rm = 1.0 / rm;
+  h->sh.slat0 = std::sin(loc.latitude);
+  h->sh.clat0 = std::cos(loc.latitude);
   h->sh.rn_cos = rn * std::cos(loc.latitude);
   const double taus[8] = {p.gyro_bias_tau, p.acc_bias_tau, p.inertia_tau, p.lin_damping_tau, p.quad_damping_tau,
                           p.water_velocity_tau, p.adcp_bias_tau, p.water_density_tau};
   for (int k = 0; k < 8; k++) h->sh.ntau[k] = -1.0 / taus[k];
+  h->qp_dt = -1.0;  // the packed {A_ii A_jj, dt^2 Q} table depends on the taus
   h->sh.uwv_weight = uwv.weight;
   h->sh.uwv_buoyancy = uwv.buoyancy;
   for (int k = 0; k < 3; k++) {
@@ -81,17 +87,62 @@ static void set_shared(uwvk_pose* h, const uwvk_pose_parameter& p, const uwvk_lo
 
 // PSP kernels read the batch-shared parameters and dt^2 Q (packed) from device memory
 static hipError_t upload_shared(uwvk_pose* h, double dt) {
-  hipError_t e = hipMemcpyAsync(h->d_shared, &h->sh, sizeof(PoseShared), hipMemcpyHostToDevice, h->stream);
-  if (e != hipSuccess || dt == h->qp_dt) return e;
-  const int n = h->dof;
-  std::vector<double> qp((size_t)n * (n + 1) / 2);
-  const double dt2 = dt * dt;
-  for (int i = 0, k = 0; i < n; i++)
-    for (int j = 0; j <= i; j++) qp[k++] = dt2 * (h->Qh.empty() ? 0.0 : h->Qh[(size_t)i * n + j]);
-  e = hipMemcpyAsync(h->d_Qp, qp.data(), qp.size() * 8, hipMemcpyHostToDevice, h->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);  // qp is a local
-  if (e == hipSuccess) h->qp_dt = dt;
-  return e;
+  hipError_t e = hipSuccess;
+  if (dt != h->qp_dt) {
+    const int n = h->dof;
+    // A_ii: the diagonal of the process model's Jacobian, the same expressions as
+    // psp::proc_diag (1 + dt (-1/tau) per Markov block, 1 otherwise)
+    std::vector<double> ad(n, 1.0);
+    auto block = [&](int d0, int len, double nt) {
+      for (int d = d0; d < d0 + len; d++) ad[d] = 1.0 + dt * nt;
+    };
+    const double* nt = h->sh.ntau;
+    if (n == 53) {
+      using L = Lay<53>;
+      block(L::d_bg, 3, nt[0]); block(L::d_ba, 3, nt[1]); block(L::d_inertia, 9, nt[2]);
+      block(L::d_lin, 9, nt[3]); block(L::d_quad, 9, nt[4]); block(L::d_wv, 4, nt[5]);
+      block(L::d_badcp, 2, nt[6]); block(L::d_rho, 1, nt[7]);
+    } else {
+      using L = Lay<26>;
+      block(L::d_bg, 3, nt[0]); block(L::d_ba, 3, nt[1]); block(L::d_wv, 4, nt[5]);
+      block(L::d_badcp, 2, nt[6]); block(L::d_rho, 1, nt[7]);
+    }
+    auto rewritten = [](int d) { return d < 9; };  // pos, ori, vel rows: rewritten by the kernel
+    auto Qij = [&](int i, int j) { return h->Qh.empty() ? 0.0 : h->Qh[(size_t)i * n + j]; };
+    std::vector<double> qp((size_t)n * (n + 1));
+    const double dt2 = dt * dt;
+    for (int i = 0, k = 0; i < n; i++)
+      for (int j = 0; j <= i; j++, k++) {
+        qp[2 * k] = (rewritten(i) || rewritten(j)) ? 0.0 : ad[i] * ad[j];
+        qp[2 * k + 1] = dt2 * Qij(i, j);
+      }
+    // band of rows >= 9: first nonzero column >= 9 .. diagonal
+    std::vector<double> band(128, 0.0);
+    int off = 0;
+    bool fits = true;
+    for (int i = 0; i < n; i++) {
+      int lo = i + 1;
+      if (i >= 9)
+        for (int j = 9; j <= i; j++)
+          if (Qij(i, j) != 0.0) { lo = j; break; }
+      h->sh.qlo[i] = lo;
+      h->sh.qoff[i] = off;
+      for (int j = lo; j <= i; j++, off++) {
+        if (off < 128) band[off] = dt2 * Qij(i, j);
+        else fits = false;
+      }
+    }
+    h->sh.q_band = fits ? 1 : 0;
+    int bw = 0;
+    for (int i = 9; i < n; i++) bw = std::max(bw, i - h->sh.qlo[i]);
+    h->sh.q_bw = bw;
+    e = hipMemcpyAsync(h->d_Qp, qp.data(), qp.size() * 8, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->d_qband, band.data(), 128 * 8, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);  // qp, band are locals
+    if (e != hipSuccess) return e;
+    h->qp_dt = dt;
+  }
+  return hipMemcpyAsync(h->d_shared, &h->sh, sizeof(PoseShared), hipMemcpyHostToDevice, h->stream);
 }
 
 #define HIPCHK(x)                              \
@@ -129,7 +180,7 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
             hipMalloc(&h->d_meas, B * 74 * 8) == hipSuccess && hipMalloc(&h->d_mask, B) == hipSuccess &&
             hipMalloc(&h->d_accepted, B) == hipSuccess && hipMalloc(&h->d_scratch, (B * 3 + 256) * 8) == hipSuccess &&
             hipMalloc(&h->d_shared, sizeof(PoseShared)) == hipSuccess &&
-            hipMalloc(&h->d_Qp, n * (n + 1) / 2 * 8) == hipSuccess &&
+            hipMalloc(&h->d_Qp, n * (n + 1) * 8) == hipSuccess && hipMalloc(&h->d_qband, 128 * 8) == hipSuccess &&
             hipEventCreate(&h->ev0) == hipSuccess && hipEventCreate(&h->ev1) == hipSuccess;
   if (!ok) {
     uwvk_pose_destroy(h);
@@ -151,7 +202,7 @@ void uwvk_pose_destroy(uwvk_pose* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_Q, (void*)h->d_rot, (void*)h->d_off,
                   (void*)h->d_model, (void*)h->d_uwv, (void*)h->d_status, (void*)h->d_meas, (void*)h->d_mask,
-                  (void*)h->d_accepted, (void*)h->d_scratch, (void*)h->d_shared, (void*)h->d_Qp})
+                  (void*)h->d_accepted, (void*)h->d_scratch, (void*)h->d_shared, (void*)h->d_Qp, (void*)h->d_qband})
     if (p) (void)hipFree(p);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);

@@ -29,6 +29,7 @@ namespace uwvk {
 struct PoseShared {
   uwvk_pose_parameter p;
   double lat0, lon0, rm, rn_cos, inv_rm;  // GeographicProjection [EXT]: lat = lat0 + x/rm, lon = lon0 - y/rn_cos
+  double slat0, clat0;                    // sin / cos of lat0 (PSP: latitude by angle addition)
   double uwv_weight, uwv_buoyancy, cog[3], cob[3];
   int literal_apply_delta;  // 1: ukfom's literal re-spread (Cholesky + GEMM); 0: exact T Sigma T^T form
   // -1/tau of the first-order Markov states (host-computed; IEEE division, so
@@ -36,6 +37,10 @@ struct PoseShared {
   double ntau[8];  // gyro bias, acc bias, inertia, lin damping, quad damping, water velocity, ADCP bias, density
   double q_ori[9];  // Q's orientation block (PSP kernels; host copy of process_noise_cov)
   double q_wv[4];   // Q's water-velocity / water-velocity-below diagonal
+  // dt^2 Q band of the rows >= 9 (PSP decay pass): row i holds cols [qlo[i], i]
+  // at qb[qoff[i]...]; q_band = 0 when the band does not fit (global fallback)
+  int qlo[56], qoff[56], q_band;
+  int q_bw;  // max band width below the diagonal over rows >= 9 (PSP keeps <= 2 in registers)
 };
 
 struct PoseBufs {
@@ -49,7 +54,8 @@ struct PoseBufs {
   const double* uwv;  // [108] base M, D_l, D_q (row-major 6x6)
   uint32_t* status;   // [batch]
   const PoseShared* shared;  // device copy of the handle's PoseShared (PSP kernels)
-  const double* Qp;          // dt^2 Q, packed lower triangle (PSP kernels; host-made per dt)
+  const double* Qp;          // {A_ii A_jj, dt^2 Q_ij} per packed entry (PSP kernels; host-made per dt)
+  const double* qband;       // [128] dt^2 Q band of rows >= 9 (PSP kernels)
 };
 
 template <int DOF>
@@ -391,6 +397,7 @@ struct ProcCtx {
   double w[3];        // stored rotation rate
   double dt;
   const double* off;  // per-instance offsets (global, uniform address)
+  double off_lane;    // PSP: the one offset storage component `lane` decays towards
 };
 
 template <int DOF>

@@ -27,6 +27,11 @@
 #pragma once
 #include "uwvk_pose_dev.hpp"
 
+// performance variants (A/B builds: make variant V=... VFLAGS=-D...)
+#ifndef PSP_RB
+#define PSP_RB 4          // rows per block of the row-block sweeps
+#endif
+
 namespace uwvk {
 namespace psp {
 
@@ -36,21 +41,17 @@ struct PG {
   static constexpr int NSLOT = (NP + 63) / 64;       // flat slots per lane
   static constexpr int N = 2 * DOF + 1;              // ukfom sigma points
   static constexpr int KP = 15;                      // predict: nonlinear prefix (pos.x .. gyro bias)
-  static constexpr int STG = 128;                    // staged rows of L_a for the point lanes
-  static constexpr int WS = 64 + 6 * DOF;            // work area (Delta/X or dz/C/K)
+  static constexpr int STG = 120;                    // staged rows of L_a for the point lanes
+
 };
 
 template <int DOF>
 struct alignas(16) PspSmem {
   double S[PG<DOF>::NP];  // Sigma, packed lower triangle
   double mu[56];          // mean (store layout)
-  double stg[PG<DOF>::STG];
-  double W[PG<DOF>::WS];
-  double vec[64];         // delta / small broadcasts
-  double ad[64];          // predict: diagonal of the process Jacobian A per DOF
-  double off[32];         // per-instance model-parameter / density offsets (loaded once)
-  double H[32];           // update: affine Jacobian H[i][t] (M x NC)
-  double P[64];           // update: P = H L_a (M x K), then Dz/2 - P (K x M)
+  double stg[PG<DOF>::STG];  // rows of L_a read by the sigma-point lanes
+  // everything else (Delta, Dz, H, P, delta, offsets, the Q band) lives in
+  // lane registers or uniform SGPRs: 12.9 KB per instance -> 12 waves per CU
 };
 
 UWVK_DEV constexpr int pidx(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
@@ -72,6 +73,90 @@ UWVK_DEV int olane() {
   asm volatile("" : "+v"(l));
   return l;
 }
+
+// ---------------------------------------------------------------------------
+// DPP wave reductions (no LDS crossbar): row_shr 1/2/3 -> 4-lane sums,
+// row_shr 4/8 with bank masks -> row sums in lane 15 of each row, row_bcast
+// 15/31 -> the total in lane 63, read back as a uniform (SGPR) value.
+// ---------------------------------------------------------------------------
+template <int CTRL, int ROW, int BANK>
+UWVK_DEV double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW, BANK, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW, BANK, true);
+  return __hiloint2double(hi, lo);
+}
+UWVK_DEV double wave_sum_dpp(double v) {
+  double s = v + dpp_d<0x111, 0xf, 0xf>(v);   // row_shr:1
+  s = s + dpp_d<0x112, 0xf, 0xf>(v);          // row_shr:2
+  s = s + dpp_d<0x113, 0xf, 0xf>(v);          // row_shr:3
+  s = s + dpp_d<0x114, 0xf, 0xe>(s);          // row_shr:4, banks 1-3
+  s = s + dpp_d<0x118, 0xf, 0xc>(s);          // row_shr:8, banks 2-3
+  s = s + dpp_d<0x142, 0xa, 0xf>(s);          // row_bcast:15, rows 1,3
+  s = s + dpp_d<0x143, 0xc, 0xf>(s);          // row_bcast:31, rows 2,3
+  return readlane_d(s, 63);
+}
+// ---------------------------------------------------------------------------
+// Small-angle SO3 exp / log (the same maps as so3_exp / so3_log, evaluated by
+// their Taylor series in the squared angle: no sqrt, sincos, atan2 or division
+// in the common case; truncation < 1e-20 relative inside the thresholds; the
+// library forms are the fallback).
+// ---------------------------------------------------------------------------
+UWVK_DEV void so3_exp_psp(const double v[3], double o[4]) {
+  const double t2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  if (t2 < 0.0625) {  // |v| < 0.25: h = |v|/2 < 0.125, u = h^2
+    const double u = 0.25 * t2;
+    // sin(h) / (2h) and cos(h), Horner in u
+    double s = 1.0 / 6227020800.0;
+    s = fma(s, u, -1.0 / 39916800.0);
+    s = fma(s, u, 1.0 / 362880.0);
+    s = fma(s, u, -1.0 / 5040.0);
+    s = fma(s, u, 1.0 / 120.0);
+    s = fma(s, u, -1.0 / 6.0);
+    s = fma(s, u, 1.0);
+    s = 0.5 * s;
+    double c = 1.0 / 479001600.0;
+    c = fma(c, u, -1.0 / 3628800.0);
+    c = fma(c, u, 1.0 / 40320.0);
+    c = fma(c, u, -1.0 / 720.0);
+    c = fma(c, u, 1.0 / 24.0);
+    c = fma(c, u, -0.5);
+    c = fma(c, u, 1.0);
+    o[0] = c; o[1] = s * v[0]; o[2] = s * v[1]; o[3] = s * v[2];
+  } else {
+    so3_exp(v, o);
+  }
+}
+UWVK_DEV void so3_log_psp(const double q[4], double o[3]) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  if (w < 0) { w = -w; x = -x; y = -y; z = -z; }
+  const double n2 = x * x + y * y + z * z, w2 = w * w;
+  if (n2 < 0.0025 * w2) {  // r = |v|/w < 0.05 (rotation < 0.1 rad)
+    const double iw = 1.0 / w;
+    const double r2 = n2 * (iw * iw);
+    // atan(r)/r = sum (-r^2)^k / (2k+1), k <= 8
+    double a = 1.0 / 17.0;
+    a = fma(a, -r2, 1.0 / 15.0);
+    a = fma(a, -r2, 1.0 / 13.0);
+    a = fma(a, -r2, 1.0 / 11.0);
+    a = fma(a, -r2, 1.0 / 9.0);
+    a = fma(a, -r2, 1.0 / 7.0);
+    a = fma(a, -r2, 1.0 / 5.0);
+    a = fma(a, -r2, 1.0 / 3.0);
+    a = fma(a, -r2, 1.0);
+    const double k = 2.0 * a * iw;  // 2 atan2(|v|, w) / |v|
+    o[0] = k * x; o[1] = k * y; o[2] = k * z;
+  } else {
+    so3_log(q, o);
+  }
+}
+UWVK_DEV void qboxminus_psp(const double a[4], const double b[4], double o[3]) {
+  double bc[4] = {b[0], -b[1], -b[2], -b[3]}, r[4];
+  qmul(a, bc, r);
+  so3_log_psp(r, o);
+}
+
+// value of lane l ^ 1 (quad_perm [1,0,3,2])
+UWVK_DEV double swap_pair_d(double v) { return dpp_d<0xb1, 0xf, 0xf>(v); }
 
 UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -98,11 +183,18 @@ UWVK_DEV void pchol_step(double (&a)[K], int r, bool& ok) {
   }
 }
 
+// DOFs whose first-order Markov decay is carried by the time scale
+// (Sigma = D Sigma~ D, D = diag(d)): gyro/acc bias, model parameters, water
+// velocities, ADCP bias, density.  Position, orientation, velocity,
+// acceleration and gravity keep d = 1.
+UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
+
+// panel Sigma[r][0..K) = d_r d_c Sigma~[r][c] (dl: this lane's d)
 template <int DOF, int K>
-UWVK_DEV bool pchol(const double* S, int r, double (&a)[K]) {
+UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl) {
   const int rr = r < DOF ? r : DOF - 1;
 #pragma unroll
-  for (int c = 0; c < K; c++) a[c] = S[pidx(rr, c)];
+  for (int c = 0; c < K; c++) a[c] = S[pidx(rr, c)] * (scaled_dof(c) ? dl * readlane_d(dl, c) : dl);
   bool ok = true;
   pchol_step<K, 0>(a, r, ok);
   return ok;
@@ -163,7 +255,7 @@ UWVK_DEV void gen_rows(const double* mu, const double* stg, int p, double x[Lay<
     gen_rows_q<RL, DOF, K, 0>(mu, stg, j, sg, v, x);
     if constexpr (has_rot<RL>()) {
       double e[4];
-      so3_exp(v, e);
+      so3_exp_psp(v, e);
       qmul(e, mu + L::s_quat, x + L::s_quat);
     }
   }
@@ -176,9 +268,19 @@ UWVK_DEV void gen_rows(const double* mu, const double* stg, int p, double x[Lay<
 template <int DOF>
 UWVK_DEV void proc_orientation(const double x[Lay<DOF>::store], const PoseShared& sh, const ProcCtx& c, double o[4]) {
   using L = Lay<DOF>;
-  const double lat = sh.lat0 + x[L::s_pos] * sh.inv_rm;
+  // sin / cos of lat = lat0 + x / R_M by angle addition from lat0 (Taylor in
+  // d = x / R_M, < 1e-20 relative for |d| < 0.01 rad, i.e. |x| < 64 km)
+  const double dl = x[L::s_pos] * sh.inv_rm;
   double sl, cl;
-  sincos(lat, &sl, &cl);
+  if (fabs(dl) < 0.01) {
+    const double u = dl * dl;
+    double sd = fma(fma(fma(fma(1.0 / 362880.0, u, -1.0 / 5040.0), u, 1.0 / 120.0), u, -1.0 / 6.0), u, 1.0) * dl;
+    double cd = fma(fma(fma(fma(1.0 / 40320.0, u, -1.0 / 720.0), u, 1.0 / 24.0), u, -0.5), u, 1.0);
+    sl = sh.slat0 * cd + sh.clat0 * sd;
+    cl = sh.clat0 * cd - sh.slat0 * sd;
+  } else {
+    sincos(sh.lat0 + dl, &sl, &cl);
+  }
   const double er[3] = {kEarthW * cl, 0.0, kEarthW * sl};
   double wb[3], wn[3];
 #pragma unroll
@@ -187,7 +289,7 @@ UWVK_DEV void proc_orientation(const double x[Lay<DOF>::store], const PoseShared
 #pragma unroll
   for (int i = 0; i < 3; i++) wn[i] = (wn[i] - er[i]) * c.dt;
   double e[4];
-  so3_exp(wn, e);
+  so3_exp_psp(wn, e);
   qmul(e, x + L::s_quat, o);
 }
 
@@ -209,15 +311,15 @@ UWVK_DEV double proc_vect(int s, const double* mu, const PoseShared& sh, const P
   }
   if constexpr (L::has_params) {
     if (s >= L::s_inertia && s < L::s_inertia + 9) {
-      const double d = sh.ntau[2] * (x - c.off[s - L::s_inertia]);
+      const double d = sh.ntau[2] * (x - c.off_lane);
       return x + dt * d;
     }
     if (s >= L::s_lin && s < L::s_lin + 9) {
-      const double d = sh.ntau[3] * (x - c.off[9 + s - L::s_lin]);
+      const double d = sh.ntau[3] * (x - c.off_lane);
       return x + dt * d;
     }
     if (s >= L::s_quad && s < L::s_quad + 9) {
-      const double d = sh.ntau[4] * (x - c.off[18 + s - L::s_quad]);
+      const double d = sh.ntau[4] * (x - c.off_lane);
       return x + dt * d;
     }
   }
@@ -230,7 +332,7 @@ UWVK_DEV double proc_vect(int s, const double* mu, const PoseShared& sh, const P
     return x + dt * d;
   }
   if (s == L::s_rho) {
-    const double d = sh.ntau[7] * (x - c.off[27]);
+    const double d = sh.ntau[7] * (x - c.off_lane);
     return x + dt * d;
   }
   return x;  // acceleration, gravity
@@ -264,16 +366,18 @@ struct PredRows {
 // ---------------------------------------------------------------------------
 // predictionStepImpl (PoseUKF.cpp:446-474) + ukf::predict, PSP form
 // ---------------------------------------------------------------------------
-// Q: process_noise_cov (DOF x DOF); Qp: dt^2 Q in packed order (host-made per dt)
+// Q: process_noise_cov (DOF x DOF); fq: per packed entry {., dt^2 Q_ij} (host-made per dt)
+// ds, ids: this lane's time scale d_l and 1/d_l (updated: d' = A_ll d)
 template <int DOF>
 UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q,
-                          const double* Qp, Stamper* st = nullptr) {
+                          const double* fq, double& ds, double& ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   using G = PG<DOF>;
   constexpr int K = G::KP;
   const int l = olane();
   const double dt = pc.dt, dt2 = dt * dt;
   // process-noise shaping from the pre-predict mean (PoseUKF.cpp:448-460)
+  double qo_lane = 0.0;  // lane a*3+b (< 9) keeps (R Q_ori R^T)[a][b]
   if (l < 9) {
     double R[9];
     qmatrix(sm.mu + L::s_quat, R);
@@ -286,14 +390,13 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       for (int m = 0; m < 3; m++) u += R[r * 3 + m] * sh.q_ori[m * 3 + k];
       s += u * R[c * 3 + k];
     }
-    sm.vec[48 + l] = s;
+    qo_lane = s;
   }
-  if (l < DOF) sm.ad[l] = proc_diag<DOF>(l, sh, dt);
   const double vs0 = sm.mu[L::s_vel], vs1 = sm.mu[L::s_vel + 1], vs2 = 10 * sm.mu[L::s_vel + 2];
   const double wv_add = sh.p.water_velocity_scale * (vs0 * vs0 + vs1 * vs1 + vs2 * vs2) * dt;
   // partial Cholesky and row staging
   double a[K];
-  const bool ok = pchol<DOF, K>(sm.S, l, a);
+  const bool ok = pchol<DOF, K>(sm.S, l, a, ds);
   stage_rows<PredRows, K>(sm.stg, l, a);
   psync();
   UWVK_STAMP(20);
@@ -316,16 +419,16 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     double nrm;
     do {
       double d[3];
-      qboxminus(o, mq, d);
+      qboxminus_psp(o, mq, d);
       const double w = pt ? 1.0 : (ctr ? wc : 0.0);
       nrm = 0.0;
 #pragma unroll
       for (int i = 0; i < 3; i++) {
-        d[i] = wave_sum(w * d[i]) / (double)G::N;
+        d[i] = wave_sum_dpp(w * d[i]) / (double)G::N;
         nrm += d[i] * d[i];
       }
       double e[4], q[4];
-      so3_exp(d, e);
+      so3_exp_psp(d, e);
       qmul(e, mq, q);
 #pragma unroll
       for (int i = 0; i < 4; i++) mq[i] = q[i];
@@ -335,7 +438,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   UWVK_STAMP(22);
   // deviations; ori x ori block; Delta_j = d_{j+} - d_{j-}
   double d[3];
-  qboxminus(o, mq, d);
+  qboxminus_psp(o, mq, d);
   double oo[6];
   {
     const double w = pt ? 1.0 : (ctr ? wc : 0.0);
@@ -343,18 +446,13 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
-      for (int j = 0; j <= i; j++) oo[k++] = 0.5 * wave_sum(w * d[i] * d[j]);
+      for (int j = 0; j <= i; j++) oo[k++] = 0.5 * wave_sum_dpp(w * d[i] * d[j]);
   }
-  {
-    double dn[3];
+  // Delta_j = d_{j+} - d_{j-} lives in lane 2j; it is read back as a uniform
+  // (SGPR) value below, no LDS staging
+  double dd[3];
 #pragma unroll
-    for (int i = 0; i < 3; i++) dn[i] = shfl_xor_d(d[i], 1);
-    if (pt && !(l & 1)) {
-#pragma unroll
-      for (int i = 0; i < 3; i++) sm.W[(l >> 1) * 3 + i] = d[i] - dn[i];
-    }
-  }
-  psync();
+  for (int i = 0; i < 3; i++) dd[i] = d[i] - swap_pair_d(d[i]);
   // ori x lin: X_r = 1/2 (A (L_a Delta))_r, lane r
   double X[3];
   {
@@ -362,7 +460,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #pragma unroll
     for (int j = 0; j < K; j++)
 #pragma unroll
-      for (int i = 0; i < 3; i++) Y[i] += a[j] * sm.W[j * 3 + i];
+      for (int i = 0; i < 3; i++) Y[i] += a[j] * readlane_d(dd[i], 2 * j);
     const int cp = proc_couple(l);
     const int src = cp >= 0 ? cp : l;
     const double ar = proc_diag<DOF>(l, sh, dt);
@@ -373,7 +471,8 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     }
   }
   UWVK_STAMP(23);
-  // rows/cols coupled by A (pos, vel): new values into registers first
+  // rows/cols coupled by A (pos, vel): new values into registers first.
+  // Sigma[p][jl] = d_jl Sigma~[p][jl] (p, jc < 12 carry d = 1)
   constexpr int pv[6] = {0, 1, 2, 6, 7, 8};
   double nv[6];
   const int jl = l < DOF ? l : DOF - 1;
@@ -382,54 +481,64 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #pragma unroll
   for (int q = 0; q < 6; q++) {
     const int r = pv[q], rc = proc_couple(r);
-    const double t0 = aj * sm.S[pidx(r, jl)] + (jc >= 0 ? dt * sm.S[pidx(r, jc)] : 0.0);
-    const double t1 = aj * sm.S[pidx(rc, jl)] + (jc >= 0 ? dt * sm.S[pidx(rc, jc)] : 0.0);
+    const double t0 = aj * (ds * sm.S[pidx(r, jl)]) + (jc >= 0 ? dt * sm.S[pidx(r, jc)] : 0.0);
+    const double t1 = aj * (ds * sm.S[pidx(rc, jl)]) + (jc >= 0 ? dt * sm.S[pidx(rc, jc)] : 0.0);
     nv[q] = t0 + dt * t1;  // A_rr = 1 for pos/vel rows
   }
-  psync();
-  if (l < DOF && !(l >= 3 && l < 6)) {
-    const bool jpv = jc >= 0;
-#pragma unroll
-    for (int q = 0; q < 6; q++)
-      if (!jpv || l <= pv[q]) sm.S[pidx(pv[q], l)] = nv[q];
-  }
-  if (l < DOF) {
-#pragma unroll
-    for (int i = 0; i < 3; i++) sm.W[64 + l * 3 + i] = X[i];
+  // new time scale d' = A_ll d (A_ll = 1 on the unscaled DOFs)
+  if (l < DOF && scaled_dof(l)) {
+    ds = aj * ds;
+    ids = 1.0 / ds;
   }
   psync();
   UWVK_STAMP(24);
-  // flat pass: ori rows/cols, decays, + Q' (packed dt^2 Q loads issued up front)
-  {
-    double qv[G::NSLOT];
+  // rewrite rows/cols < 9 (stored as Sigma / d'_l): A-coupled rows (pos, vel),
+  // orientation rows (cross terms), ori x ori
+  if (l < DOF && !(l >= 3 && l < 6)) {
+    const bool jpv = jc >= 0;
+    const double2* f2 = reinterpret_cast<const double2*>(fq);
 #pragma unroll
-    for (int t = 0; t < G::NSLOT; t++) {
-      const int e = l + 64 * t;
-      qv[t] = e < G::NP ? Qp[e] : 0.0;
+    for (int q = 0; q < 6; q++)
+      if (!jpv || l <= pv[q]) {
+        const int e = pidx(pv[q], l);
+        sm.S[e] = (nv[q] + f2[e].y) * ids;
+      }
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      const int e = pidx(3 + i, l);
+      sm.S[e] = (X[i] + f2[e].y) * ids;
     }
+  }
+  if (l < 9 && (l / 3) >= (l % 3)) {
+    const int a2 = l / 3, b2 = l % 3;
+    sm.S[pidx(3 + a2, 3 + b2)] = oo[a2 * (a2 + 1) / 2 + b2] + dt2 * qo_lane;
+  }
+  // rows/cols >= 9: A Sigma A^T = D' Sigma~ D' leaves Sigma~ unchanged; only
+  // dt^2 Q / (d'_i d'_j) is added on Q's band.  Lane l owns row l's band
+  // entries (l, l - k); k <= 2 from registers, wider bands from global memory.
+  {
+    constexpr int R0 = 9;
+    const double2* f2 = reinterpret_cast<const double2*>(fq);
+    const int bw = sh.q_bw;
+    double idk = ids;  // 1 / d'_{l-k}
 #pragma unroll
-    for (int t = 0; t < G::NSLOT; t++) {
-      const int e = l + 64 * t;
-      if (e < G::NP) {
-        int i, j;
-        unpack(e, i, j);
-        const bool io = i >= 3 && i < 6, jo = j >= 3 && j < 6;
-        double v, q = qv[t];
-        if (io && jo) {
-          const int a2 = i - 3, b2 = j - 3;
-          v = oo[a2 * (a2 + 1) / 2 + b2];
-          q = dt2 * sm.vec[48 + a2 * 3 + b2];
-        } else if (io) {
-          v = sm.W[64 + j * 3 + (i - 3)];
-        } else if (jo) {
-          v = sm.W[64 + i * 3 + (j - 3)];
-        } else if (proc_couple(i) >= 0 || proc_couple(j) >= 0) {
-          v = sm.S[e];
-        } else {
-          v = sm.ad[i] * sm.ad[j] * sm.S[e];
-        }
-        if (i == j && i >= L::d_wv && i < L::d_wv + 4) q = dt2 * (sh.q_wv[i - L::d_wv] + wv_add);
-        sm.S[e] = v + q;
+    for (int k = 0; k < 3; k++) {
+      if (k > 0) idk = dpp_d<0x138, 0xf, 0xf>(idk);  // wave_shr:1 -> lane l - k
+      const int j = l - k;
+      if (l >= R0 && l < DOF && j >= R0 && k <= bw) {
+        const int e = pidx(l, j);
+        double q = f2[e].y;
+        if (k == 0 && l >= L::d_wv && l < L::d_wv + 4) q = dt2 * (sh.q_wv[l - L::d_wv] + wv_add);
+        if (q != 0.0) sm.S[e] += q * (ids * idk);
+      }
+    }
+    for (int k = 3; k <= bw; k++) {  // uniform bound: wide Q bands only
+      const double idj = shfl_d(ids, l - k >= 0 ? l - k : 0);
+      const int j = l - k;
+      if (l >= R0 && l < DOF && j >= R0) {
+        const int e = pidx(l, j);
+        const double q = f2[e].y;
+        if (q != 0.0) sm.S[e] += q * (ids * idj);
       }
     }
   }
@@ -443,6 +552,28 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   psync();
   UWVK_STAMP(26);
   return ok;
+}
+
+// Sigma~ -> Sigma (d folded in, d = 1 afterwards).  Uses stg as the d table.
+template <int DOF>
+UWVK_DEV void psp_fold(PspSmem<DOF>& sm, double& ds, double& ids) {
+  using G = PG<DOF>;
+  const int l = olane();
+  psync();
+  if (l < DOF) sm.stg[l] = ds;
+  psync();
+#pragma unroll 1
+  for (int t = 0; t < G::NSLOT; t++) {
+    const int e = l + 64 * t;
+    if (e < G::NP) {
+      int i, j;
+      unpack(e, i, j);
+      if (scaled_dof(i) || scaled_dof(j)) sm.S[e] = sm.S[e] * (sm.stg[i] * sm.stg[j]);
+    }
+  }
+  psync();
+  ds = 1.0;
+  ids = 1.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -554,7 +685,7 @@ struct PZ {  // measurementZPosition, PoseUKF.cpp:100-105: linear (k = 0)
 // ---------------------------------------------------------------------------
 template <int DOF, class HM>
 UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const double (&Rm)[HM::M * HM::M], int gate,
-                         const HM& hm, bool* ok, Stamper* st = nullptr) {
+                         const HM& hm, bool* ok, double ds, double ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   using G = PG<DOF>;
   constexpr int M = HM::M, K = HM::K, NC = HM::NC, KA = K > 0 ? K : 1;
@@ -562,7 +693,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double a[KA];
   bool cok = true;
   if constexpr (K > 0) {
-    cok = pchol<DOF, K>(sm.S, l, a);
+    cok = pchol<DOF, K>(sm.S, l, a, ds);
     stage_rows<HM, K>(sm.stg, l, a);
     psync();
   }
@@ -580,7 +711,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   // zbar = z_0 + (1/N) sum_{2K} (z_p - z_0)  (the linear pairs cancel)
 #pragma unroll
   for (int i = 0; i < M; i++) {
-    const double s = K > 0 ? wave_sum(pt ? zp[i] - zc[i] : 0.0) : 0.0;
+    const double s = K > 0 ? wave_sum_dpp(pt ? zp[i] - zc[i] : 0.0) : 0.0;
     zb[i] = zc[i] + s / (double)G::N;
     e[i] = zc[i] - zb[i];
   }
@@ -593,38 +724,35 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   for (int i = 0; i < M; i++)
 #pragma unroll
     for (int j = 0; j <= i; j++) {
-      const double s = K > 0 ? wave_sum(pt ? dz[i] * dz[j] : 0.0) : 0.0;
+      const double s = K > 0 ? wave_sum_dpp(pt ? dz[i] * dz[j] : 0.0) : 0.0;
       S[i * M + j] = 0.5 * (s + wc * e[i] * e[j]);
     }
-  // Delta z_j = z_{j+} - z_{j-}, staged as W[j*M + i]
-  if constexpr (K > 0) {
-    double zn[M];
+  // Delta z_j = z_{j+} - z_{j-} lives in lane 2j (read back as uniform values)
+  double zd[M];
 #pragma unroll
-    for (int i = 0; i < M; i++) zn[i] = shfl_xor_d(zp[i], 1);
-    if (pt && !(l & 1)) {
-#pragma unroll
-      for (int i = 0; i < M; i++) sm.W[(l >> 1) * M + i] = zp[i] - zn[i];
-    }
-  }
+  for (int i = 0; i < M; i++) zd[i] = K > 0 ? zp[i] - swap_pair_d(zp[i]) : 0.0;
   UWVK_STAMP(31);
-  // affine part: H at mu (staged), P = H L_a and Qp = Dz/2 - P lane-parallel,
-  // G = Sigma H^T (lane r).  Uniform matrices live in LDS, not in VGPRs.
-  if (l == 0) {
+  // affine part.  H at mu: every lane evaluates it, the values become uniform
+  // (SGPR) copies; P = H L_a lane-parallel (lane i*K + j); G = Sigma H^T (lane r).
+  double Hs[M][NC];
+  {
     double H[M][NC];
     hm.jac(sm.mu, H);
 #pragma unroll
     for (int i = 0; i < M; i++)
 #pragma unroll
-      for (int t = 0; t < NC; t++) sm.H[i * NC + t] = H[i][t];
+      for (int t = 0; t < NC; t++) Hs[i][t] = readlane_d(H[i][t], 0);
   }
-  psync();
+  double Pl = 0.0;
   if constexpr (K > 0) {
-    if (l < M * K) {
-      const int i = l / K, j = l - (l / K) * K;
-      double s = 0.0;
+    const int q = l < M * K ? l : 0;
+    const int i = q / K, j = q - (q / K) * K;
 #pragma unroll
-      for (int t = 0; t < NC; t++) s += sm.H[i * NC + t] * sm.stg[row_pos(HM::rows, HM::cols[t]) * K + j];
-      sm.P[i * K + j] = s;
+    for (int t = 0; t < NC; t++) {
+      double h = Hs[0][t];
+#pragma unroll
+      for (int ii = 1; ii < M; ii++) h = (i == ii) ? Hs[ii][t] : h;
+      Pl += h * sm.stg[row_pos(HM::rows, HM::cols[t]) * K + j];
     }
   }
   const int rl = l < DOF ? l : DOF - 1;
@@ -633,37 +761,40 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   for (int i = 0; i < M; i++) Gr[i] = 0.0;
 #pragma unroll
   for (int t = 0; t < NC; t++) {
-    const double s = sm.S[pidx(rl, HM::cols[t])];
+    constexpr int dummy = 0;
+    (void)dummy;
+    double s = sm.S[pidx(rl, HM::cols[t])];
+    if (scaled_dof(HM::cols[t])) s = s * readlane_d(ds, HM::cols[t]);
 #pragma unroll
-    for (int i = 0; i < M; i++) Gr[i] += s * sm.H[i * NC + t];
+    for (int i = 0; i < M; i++) Gr[i] += s * Hs[i][t];
   }
-  psync();
+#pragma unroll
+  for (int i = 0; i < M; i++) Gr[i] = Gr[i] * ds;  // Sigma[r][c] = d_r d_c Sigma~[r][c]
   UWVK_STAMP(32);
-  // C_r = G_r + sum_j L[r][j] (Dz_j / 2 - P[:, j])
-  double C[M];
+  // Glin_r = G_r - sum_j L[r][j] P[:, j]: row r of (Sigma - L_a L_a^T) H^T;
+  // C_r = Glin_r + 1/2 sum_j L[r][j] Dz_j; S += H Glin + R  (H Glin = H Sigma H^T - P P^T)
+  double Gl[M], C[M];
 #pragma unroll
   for (int i = 0; i < M; i++) {
-    double s = Gr[i];
+    double g = Gr[i], c = 0.0;
     if constexpr (K > 0) {
 #pragma unroll
-      for (int j = 0; j < K; j++) s += a[j] * (0.5 * sm.W[j * M + i] - sm.P[i * K + j]);
+      for (int j = 0; j < K; j++) {
+        g -= a[j] * readlane_d(Pl, i * K + j);
+        c += a[j] * readlane_d(zd[i], 2 * j);
+      }
     }
-    C[i] = s;
+    Gl[i] = g;
+    C[i] = g + 0.5 * c;
   }
-  // S += H G - P P^T + R
 #pragma unroll
   for (int i = 0; i < M; i++)
 #pragma unroll
     for (int j = 0; j <= i; j++) {
       double hg = 0.0;
 #pragma unroll
-      for (int t = 0; t < NC; t++) hg += sm.H[i * NC + t] * readlane_d(Gr[j], HM::cols[t]);
-      double pp = 0.0;
-      if constexpr (K > 0) {
-#pragma unroll
-        for (int k = 0; k < K; k++) pp += sm.P[i * K + k] * sm.P[j * K + k];
-      }
-      const double s = S[i * M + j] + (hg - pp);
+      for (int t = 0; t < NC; t++) hg += Hs[i][t] * readlane_d(Gl[j], HM::cols[t]);
+      const double s = S[i * M + j] + hg;
       S[i * M + j] = s + Rm[i * M + j];
       if (j != i) S[j * M + i] = s + Rm[j * M + i];
     }
@@ -692,41 +823,50 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   const bool accept = gate == 0 ? true : !(d2 > kD2P95);
   if (!accept) return false;
   UWVK_STAMP(33);
-  // Sigma -= C K^T (flat), delta = K nu
+  // Sigma -= C K^T: row sweep, lane = column j holds K_j; C_i arrives as a
+  // uniform (readlane) value; the next row's load precedes this row's store.
+  // delta = K nu (lane r).
   psync();
-  if (l < DOF) {
+  double dl = 0.0;  // delta = K nu, lane r
 #pragma unroll
-    for (int i = 0; i < M; i++) {
-      sm.W[l * 2 * M + i] = C[i];
-      sm.W[l * 2 * M + M + i] = Kg[i];
-    }
-    double dl = 0.0;
+  for (int i = 0; i < M; i++) dl += Kg[i] * nu[i];
+  // Sigma~ -= (C / d)(K / d)^T
+  double Ct[M], Kt[M];
 #pragma unroll
-    for (int i = 0; i < M; i++) dl += Kg[i] * nu[i];
-    sm.vec[l] = dl;
+  for (int i = 0; i < M; i++) {
+    Ct[i] = C[i] * ids;
+    Kt[i] = Kg[i] * ids;
   }
-  psync();
+  {
+    // row blocks of RB: every load of a block is issued before its stores
+    constexpr int RB = PSP_RB;
 #pragma unroll 1
-  for (int t = 0; t < G::NSLOT; t++) {
-    const int ee = l + 64 * t;
-    if (ee < G::NP) {
-      int i, j;
-      unpack(ee, i, j);
-      double s = 0.0;
+    for (int i0 = 0; i0 < DOF; i0 += RB) {
+      double sv[RB];
 #pragma unroll
-      for (int k = 0; k < M; k++) s += sm.W[i * 2 * M + k] * sm.W[j * 2 * M + M + k];
-      sm.S[ee] -= s;
+      for (int r = 0; r < RB; r++) {
+        const int i = i0 + r;
+        sv[r] = (i < DOF && l <= i) ? sm.S[i * (i + 1) / 2 + l] : 0.0;
+      }
+#pragma unroll
+      for (int r = 0; r < RB; r++) {
+        const int i = i0 + r < DOF ? i0 + r : DOF - 1;
+        double s2 = 0.0;
+#pragma unroll
+        for (int a2 = 0; a2 < M; a2++) s2 += readlane_d(Ct[a2], i) * Kt[a2];
+        if (i0 + r < DOF && l <= i) sm.S[i * (i + 1) / 2 + l] = sv[r] - s2;
+      }
     }
   }
   psync();
   UWVK_STAMP(34);
   // apply_delta, exact nav-frame form: mu <- mu [+] delta, Sigma <- T Sigma T^T
   {
+    const double dv[3] = {readlane_d(dl, 3), readlane_d(dl, 4), readlane_d(dl, 5)};
     double R[9];
     {
-      const double dv[3] = {sm.vec[3], sm.vec[4], sm.vec[5]};
       double eq[4];
-      so3_exp(dv, eq);
+      so3_exp_psp(dv, eq);
       qmatrix(eq, R);
     }
     // rows 3..5 of every column j outside the block
@@ -749,16 +889,14 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       }
       nb = s;
     }
+    // storage s = l takes tangent delta_{l} (l < 3) or delta_{l-1} (l >= 7): DPP wave_shr:1
+    const double dsh = dpp_d<0x138, 0xf, 0xf>(dl);
     double mnew = 0.0;
-    if (l < L::store && !(l >= 3 && l < 7)) {
-      const int d = l < 3 ? l : l - 1;
-      mnew = sm.mu[l] + 1.0 * sm.vec[d];
-    }
+    if (l < L::store && !(l >= 3 && l < 7)) mnew = sm.mu[l] + 1.0 * (l < 3 ? dl : dsh);
     double qn[4];
     {
       double eq[4];
-      const double dv[3] = {sm.vec[3], sm.vec[4], sm.vec[5]};
-      so3_exp(dv, eq);
+      so3_exp_psp(dv, eq);
       qmul(eq, sm.mu + L::s_quat, qn);
     }
     psync();

@@ -35,8 +35,21 @@ UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
     if (e < G::NP) sm.S[e] = v[t];
   }
   if (l < Lay<DOF>::store) sm.mu[l] = m;
-  if (l < 28) sm.off[l] = b.off[inst * 28 + l];
   psync();
+}
+
+// the offset storage component `lane` decays towards (PoseUKF.cpp:43-59, 77-79)
+template <int DOF>
+UWVK_DEV double lane_offset(const PoseBufs& b, int64_t inst, int s) {
+  using L = Lay<DOF>;
+  int k = -1;
+  if constexpr (L::has_params) {
+    if (s >= L::s_inertia && s < L::s_inertia + 9) k = s - L::s_inertia;
+    if (s >= L::s_lin && s < L::s_lin + 9) k = 9 + s - L::s_lin;
+    if (s >= L::s_quad && s < L::s_quad + 9) k = 18 + s - L::s_quad;
+  }
+  if (s == L::s_rho) k = 27;
+  return k >= 0 ? b.off[inst * 28 + k] : 0.0;
 }
 
 template <int DOF>
@@ -69,29 +82,29 @@ UWVK_DEV void copy_zr(const double* zin, const double* Rin, double (&z)[M], doub
 // one measurement update of kind KIND on instance inst (PSP form)
 template <int DOF, int KIND>
 UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, const double* zin, const double* Rin,
-                        const MeasArgs& ma, bool* ok, Stamper* st = nullptr) {
+                        const MeasArgs& ma, bool* ok, double ds, double ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   if constexpr (KIND == MK_ACC) {
     double z[3], R[9];
     copy_zr<3>(zin, Rin, z, R);
-    return psp_update<DOF>(sm, z, R, 0, PAcc<DOF>{}, ok, st);
+    return psp_update<DOF>(sm, z, R, 0, PAcc<DOF>{}, ok, ds, ids, st);
   } else if constexpr (KIND == MK_VEL) {
     double z[3], R[9];
     copy_zr<3>(zin, Rin, z, R);
-    return psp_update<DOF>(sm, z, R, 0, PVel<DOF>{}, ok, st);
+    return psp_update<DOF>(sm, z, R, 0, PVel<DOF>{}, ok, ds, ids, st);
   } else if constexpr (KIND == MK_PRESSURE) {
     double z[1], R[1];
     copy_zr<1>(zin, Rin, z, R);
     PPressure<DOF> h;
     h.h.s[0] = ma.v3[0]; h.h.s[1] = ma.v3[1]; h.h.s[2] = ma.v3[2];
     h.h.patm = sh.p.atmospheric_pressure;
-    return psp_update<DOF>(sm, z, R, 0, h, ok, st);
+    return psp_update<DOF>(sm, z, R, 0, h, ok, ds, ids, st);
   } else if constexpr (KIND == MK_WATER) {
     double z[2], R[4];
     copy_zr<2>(zin, Rin, z, R);
     PWater<DOF> h;
     h.cw = ma.extra ? ma.extra[inst] : 0.0;
-    return psp_update<DOF>(sm, z, R, 1, h, ok, st);
+    return psp_update<DOF>(sm, z, R, 1, h, ok, ds, ids, st);
   } else if constexpr (KIND == MK_XY || KIND == MK_GEO || KIND == MK_DELAYED) {
     double z[2], R[4];
     copy_zr<2>(zin, Rin, z, R);
@@ -109,12 +122,12 @@ UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, co
       z[0] = zin[0] + (sm.mu[L::s_pos] - ma.extra[2 * inst]);
       z[1] = zin[1] + (sm.mu[L::s_pos + 1] - ma.extra[2 * inst + 1]);
     }
-    return psp_update<DOF>(sm, z, R, gate, PXY<DOF>{}, ok, st);
+    return psp_update<DOF>(sm, z, R, gate, PXY<DOF>{}, ok, ds, ids, st);
   } else {
     static_assert(KIND == MK_Z, "PSP update kind");
     double z[1], R[1];
     copy_zr<1>(zin, Rin, z, R);
-    return psp_update<DOF>(sm, z, R, 0, PZ<DOF>{}, ok, st);
+    return psp_update<DOF>(sm, z, R, 0, PZ<DOF>{}, ok, ds, ids, st);
   }
 }
 
@@ -126,9 +139,12 @@ __global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, d
   ProcCtx pc;
   for (int k = 0; k < 3; k++) pc.w[k] = b.rot[inst * 3 + k];
   pc.dt = dt;
-  pc.off = sm.off;
-  const bool ok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp);
+  pc.off = nullptr;
+  pc.off_lane = lane_offset<DOF>(b, inst, lane_id());
+  double ds = 1.0, ids = 1.0;
+  const bool ok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids);
   if (!ok && lane_id() == 0) b.status[inst] |= UWVK_ST_NOTPD;
+  psp_fold<DOF>(sm, ds, ids);
   store_psp<DOF>(sm, b, inst);
 }
 
@@ -151,7 +167,7 @@ __global__ __launch_bounds__(64) void k_psp_update(PoseBufs b, PoseShared sh, Me
   }
   load_psp<DOF>(sm, b, inst);
   bool ok = true;
-  const bool acc = do_update<DOF, KIND>(sm, sh, inst, z, R, ma, &ok);
+  const bool acc = do_update<DOF, KIND>(sm, sh, inst, z, R, ma, &ok, 1.0, 1.0);
   if (lane_id() == 0) {
     if (!ok) b.status[inst] |= UWVK_ST_NOTPD;
     if (ma.accepted) ma.accepted[inst] = acc ? 1 : 0;
@@ -179,6 +195,7 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
 #endif
   load_psp<DOF>(sm, b, inst);
   UWVK_STAMP(40);
+  double ds = 1.0, ids = 1.0;  // time scale of the Markov DOFs (Sigma = D Sigma~ D)
   bool ok = true, nan = false;
   uint32_t cnt[4] = {0, 0, 0, 0};
   MeasArgs ma{};
@@ -187,7 +204,8 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
   ProcCtx pc;
   for (int k = 0; k < 3; k++) pc.w[k] = w[k];
   pc.dt = ea.dt;
-  pc.off = sm.off;
+  pc.off = nullptr;
+  pc.off_lane = lane_offset<DOF>(b, inst, lane_id());
   // the next epoch's IMU inputs are prefetched one epoch ahead (their load
   // latency overlaps this epoch's arithmetic)
   uint32_t fl_n = 0;
@@ -214,11 +232,12 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
     }
     const PoseShared& sh = shared_for_epoch(b);
     UWVK_STAMP(41);
-    bool sok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, st);
+    if (((e - ea.first) & 1023) == 1023) psp_fold<DOF>(sm, ds, ids);  // keep d in range
+    bool sok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids, st);
     ok = ok && sok;
     if (fl & UWVK_EV_ACC) {
       if (all_finite(za, 3)) {
-        do_update<DOF, MK_ACC>(sm, sh, inst, za, ea.acc_cov, ma, &sok, st);
+        do_update<DOF, MK_ACC>(sm, sh, inst, za, ea.acc_cov, ma, &sok, ds, ids, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -227,7 +246,7 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + inst) * 3;
       if (all_finite(z, 3)) {
-        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, inst, z, ea.dvl_cov, ma, &sok, st);
+        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, inst, z, ea.dvl_cov, ma, &sok, ds, ids, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -236,7 +255,7 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
     if (fl & UWVK_EV_PRESSURE) {
       const double* z = ea.pressure + (int64_t)ea.p_index[e] * B + inst;
       if (all_finite(z, 1)) {
-        cnt[1] += do_update<DOF, MK_PRESSURE>(sm, sh, inst, z, &ea.p_cov, ma, &sok);
+        cnt[1] += do_update<DOF, MK_PRESSURE>(sm, sh, inst, z, &ea.p_cov, ma, &sok, ds, ids);
         ok = ok && sok;
       } else {
         nan = true;
@@ -249,7 +268,7 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
         double zz[2] = {z[0], z[1]}, R[4] = {ea.adcp_cov[0], ea.adcp_cov[1], ea.adcp_cov[2], ea.adcp_cov[3]};
         PWater<DOF> h;
         h.cw = ea.cw[c];
-        cnt[2] += psp_update<DOF>(sm, zz, R, 1, h, &sok);
+        cnt[2] += psp_update<DOF>(sm, zz, R, 1, h, &sok, ds, ids);
         ok = ok && sok;
       }
     }
@@ -263,6 +282,7 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
     if (ea.accept_counts)
       for (int k = 0; k < 4; k++) ea.accept_counts[inst * 4 + k] += cnt[k];
   }
+  psp_fold<DOF>(sm, ds, ids);
   store_psp<DOF>(sm, b, inst);
 }
 

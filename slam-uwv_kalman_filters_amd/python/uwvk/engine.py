@@ -14,7 +14,8 @@ from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(os.path.dirname(HERE))  # slam-uwv_kalman_filters_amd/
-LIB_PATH = os.path.join(PKG, "libuwvk.so")
+# UWVK_LIB selects an alternative build of the same ABI (A/B performance variants)
+LIB_PATH = os.environ.get("UWVK_LIB") or os.path.join(PKG, "libuwvk.so")
 
 # every symbol include/uwvk.h declares (checked by tests/test_abi.py)
 SYMBOLS = [
