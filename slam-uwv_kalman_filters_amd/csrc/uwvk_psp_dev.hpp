@@ -29,7 +29,13 @@
 
 // performance variants (A/B builds: make variant V=... VFLAGS=-D...)
 #ifndef PSP_RB
-#define PSP_RB 4          // rows per block of the row-block sweeps
+#define PSP_RB 8          // rows per block of the row-block sweeps
+#endif
+#ifndef PSP_PCHOL_LDS
+#define PSP_PCHOL_LDS 1   // partial Cholesky: 1 broadcast column through LDS, 0 readlane
+#endif
+#ifndef PSP_RANKM_LDS
+#define PSP_RANKM_LDS 1   // Sigma~ -= C~ K~^T: 1 C~_i by LDS broadcast, 0 by readlane
 #endif
 
 namespace uwvk {
@@ -41,7 +47,7 @@ struct PG {
   static constexpr int NSLOT = (NP + 63) / 64;       // flat slots per lane
   static constexpr int N = 2 * DOF + 1;              // ukfom sigma points
   static constexpr int KP = 15;                      // predict: nonlinear prefix (pos.x .. gyro bias)
-  static constexpr int STG = 120;                    // staged rows of L_a for the point lanes
+  static constexpr int STG = 160;                    // L_a rows for the point lanes / Cholesky column / C~
 
 };
 
@@ -189,14 +195,44 @@ UWVK_DEV void pchol_step(double (&a)[K], int r, bool& ok) {
 // acceleration and gravity keep d = 1.
 UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 
-// panel Sigma[r][0..K) = d_r d_c Sigma~[r][c] (dl: this lane's d)
+// variant: column J broadcast through a double-buffered LDS column (no readlanes)
+template <int K, int J>
+UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* colbuf) {
+  if constexpr (J < K) {
+    const double piv = readlane_d(a[J], J);
+    ok = ok && (piv > 0.0);
+    const double inv = rsqrt_f64(piv);
+    a[J] = (r == J) ? piv * inv : (r > J ? a[J] * inv : 0.0);
+    if constexpr (J + 1 < K) {
+      double* col = colbuf + (J & 1) * 64;
+      col[r] = a[J];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = J + 1; c < K; c++) a[c] -= a[J] * col[c];
+#pragma unroll
+      for (int c = J + 1; c < K; c++) asm volatile("" : "+v"(a[c]));
+    }
+    pchol_step_lds<K, J + 1>(a, r, ok, colbuf);
+  }
+}
+
+// panel Sigma[r][0..K) = d_r d_c Sigma~[r][c] (dl: this lane's d); colbuf:
+// 128 doubles of LDS scratch (PSP_PCHOL_LDS)
 template <int DOF, int K>
-UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl) {
+UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* colbuf) {
   const int rr = r < DOF ? r : DOF - 1;
 #pragma unroll
   for (int c = 0; c < K; c++) a[c] = S[pidx(rr, c)] * (scaled_dof(c) ? dl * readlane_d(dl, c) : dl);
   bool ok = true;
+#if PSP_PCHOL_LDS
+  pchol_step_lds<K, 0>(a, r, ok, colbuf);
+  psync();  // colbuf (stg) is reused right after
+#else
+  (void)colbuf;
   pchol_step<K, 0>(a, r, ok);
+#endif
   return ok;
 }
 
@@ -396,7 +432,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   const double wv_add = sh.p.water_velocity_scale * (vs0 * vs0 + vs1 * vs1 + vs2 * vs2) * dt;
   // partial Cholesky and row staging
   double a[K];
-  const bool ok = pchol<DOF, K>(sm.S, l, a, ds);
+  const bool ok = pchol<DOF, K>(sm.S, l, a, ds, sm.stg);
   stage_rows<PredRows, K>(sm.stg, l, a);
   psync();
   UWVK_STAMP(20);
@@ -693,7 +729,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double a[KA];
   bool cok = true;
   if constexpr (K > 0) {
-    cok = pchol<DOF, K>(sm.S, l, a, ds);
+    cok = pchol<DOF, K>(sm.S, l, a, ds, sm.stg);
     stage_rows<HM, K>(sm.stg, l, a);
     psync();
   }
@@ -838,6 +874,13 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     Kt[i] = Kg[i] * ids;
   }
   {
+#if PSP_RANKM_LDS
+    if (l < DOF) {  // C~ rows for the broadcast reads (stg is free here)
+#pragma unroll
+      for (int a2 = 0; a2 < M; a2++) sm.stg[M * l + a2] = Ct[a2];
+    }
+    psync();
+#endif
     // row blocks of RB: every load of a block is issued before its stores
     constexpr int RB = PSP_RB;
 #pragma unroll 1
@@ -853,7 +896,13 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
         const int i = i0 + r < DOF ? i0 + r : DOF - 1;
         double s2 = 0.0;
 #pragma unroll
-        for (int a2 = 0; a2 < M; a2++) s2 += readlane_d(Ct[a2], i) * Kt[a2];
+        for (int a2 = 0; a2 < M; a2++) {
+#if PSP_RANKM_LDS
+          s2 += sm.stg[M * i + a2] * Kt[a2];
+#else
+          s2 += readlane_d(Ct[a2], i) * Kt[a2];
+#endif
+        }
         if (i0 + r < DOF && l <= i) sm.S[i * (i + 1) / 2 + l] = sv[r] - s2;
       }
     }
