@@ -218,8 +218,8 @@ class PoseUKFBatch:
         return DevicePoseLog(log, self.device)
 
     def run_log(self, dlog, first=0, count=None, accept_counts=None, sync=True):
-        """Queue epochs [first, first+count) on the handle's stream (one fused
-        launch per epoch); sync=False leaves them in flight."""
+        """Queue epochs [first, first+count) on the handle's stream (PSP: one
+        launch per run of epochs without BodyEfforts); sync=False leaves them in flight."""
         count = dlog.epochs - first if count is None else count
         _chk(self.L.uwvk_pose_run_log(self.h, C.byref(dlog.s), C.c_int64(first), C.c_int64(count),
                                       accept_counts.ptr if accept_counts is not None else None), "run_log")

@@ -192,3 +192,26 @@ def test_nan_measurement_rejected(eng):
     x1, P1 = g.get_state()
     np.testing.assert_array_equal(x0, x1)
     np.testing.assert_array_equal(P0, P1)
+
+
+def test_run_log_long_single_launch(eng, orc):
+    """3000 C4 epochs in ONE run_log call: exercises the PSP kernel's periodic
+    fold of the time scale (every 1024 epochs) and the efforts-epoch split."""
+    cfg, uwv, log, o, g = _pair(eng, orc, 3, 53, "C4", 3000)
+    counts_o = o.run_log(log)
+    dlog = g.upload_log(log)
+    acc = eng.DeviceBuffer(np.zeros((3, 4), np.uint32))
+    g.run_log(dlog, accept_counts=acc)
+    np.testing.assert_array_equal(counts_o, acc.read(np.uint32, (3, 4)))
+    assert not g.get_status().any()
+    _check(o, g, 53, TOL_LOG)
+
+
+def test_run_log_device_flags_only(eng, orc):
+    """run_log without the host copy of the flags (the engine reads them back)."""
+    cfg, uwv, log, o, g = _pair(eng, orc, 3, 53, "C4", 600)
+    o.run_log(log)
+    dlog = g.upload_log(log)
+    dlog.s.host_flags = None
+    g.run_log(dlog)
+    _check(o, g, 53, TOL_LOG)
