@@ -124,11 +124,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # UWVK_BENCH_BACKEND=gloo: rehearsal of the N-rank path on one GPU (all ranks
+    # on device 0, statistics reduced on the host); the driver's runs use RCCL
+    backend = os.environ.get("UWVK_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = 0
+    stat_dev = "cuda" if backend == "nccl" else None
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     from uwvk import engine, ensemble, synth
 
     B = a.batch_per_gpu
@@ -163,13 +172,15 @@ def main():
     stats = f.ensemble_stats(truth)  # synchronous
     if dist is not None:
         # RCCL over xGMI: the only collective of the workload
-        stats = ensemble.allreduce_stats(stats, dist, device="cuda")
+        stats = ensemble.allreduce_stats(stats, dist, device=stat_dev)
     f.synchronize()
     barrier()
     wall = time.perf_counter() - t0
     if dist is not None:
         import torch
-        w = torch.tensor([wall], dtype=torch.float64).cuda()
+        w = torch.tensor([wall], dtype=torch.float64)
+        if stat_dev:
+            w = w.cuda()
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
     status = f.get_status()

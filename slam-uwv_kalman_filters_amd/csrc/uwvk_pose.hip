@@ -136,6 +136,15 @@ static hipError_t upload_shared(uwvk_pose* h, double dt) {
     int bw = 0;
     for (int i = 9; i < n; i++) bw = std::max(bw, i - h->sh.qlo[i]);
     h->sh.q_bw = bw;
+    // lane-resident Q (psp::LaneQ): no coupling of the rewritten rows (< 9) with
+    // anything but their own diagonal / the orientation block, band <= 2 below
+    bool simple = bw <= 2;
+    for (int i = 0; i < n && simple; i++)
+      for (int j = 0; j < i && simple; j++) {
+        const bool ori = i >= 3 && i < 6 && j >= 3 && j < 6;
+        if ((i < 9 || j < 9) && !ori && Qij(i, j) != 0.0) simple = false;
+      }
+    h->sh.q_simple = simple ? 1 : 0;
     e = hipMemcpyAsync(h->d_Qp, qp.data(), qp.size() * 8, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h->d_qband, band.data(), 128 * 8, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);  // qp, band are locals

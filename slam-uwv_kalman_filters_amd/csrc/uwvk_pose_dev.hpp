@@ -41,6 +41,7 @@ struct PoseShared {
   // at qb[qoff[i]...]; q_band = 0 when the band does not fit (global fallback)
   int qlo[56], qoff[56], q_band;
   int q_bw;  // max band width below the diagonal over rows >= 9 (PSP keeps <= 2 in registers)
+  int q_simple;  // PSP: lane-resident dt^2 Q suffices (see psp::LaneQ)
 };
 
 struct PoseBufs {

@@ -197,12 +197,15 @@ UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 
 // variant: column J broadcast through a double-buffered LDS column (no readlanes)
 template <int K, int J>
-UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* colbuf) {
+UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* colbuf, double piv) {
   if constexpr (J < K) {
-    const double piv = readlane_d(a[J], J);
     ok = ok && (piv > 0.0);
     const double inv = rsqrt_f64(piv);
     a[J] = (r == J) ? piv * inv : (r > J ? a[J] * inv : 0.0);
+    // look-ahead: the next pivot is lane J+1's a[J+1] - L[J+1][J]^2 (its own
+    // registers), so its rsqrt need not wait for the column broadcast
+    double pnext = 0.0;
+    if constexpr (J + 1 < K) pnext = readlane_d(a[J + 1] - a[J] * a[J], J + 1);
     if constexpr (J + 1 < K) {
       double* col = colbuf + (J & 1) * 64;
       col[r] = a[J];
@@ -214,7 +217,7 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* colbuf) {
 #pragma unroll
       for (int c = J + 1; c < K; c++) asm volatile("" : "+v"(a[c]));
     }
-    pchol_step_lds<K, J + 1>(a, r, ok, colbuf);
+    pchol_step_lds<K, J + 1>(a, r, ok, colbuf, pnext);
   }
 }
 
@@ -227,7 +230,7 @@ UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* c
   for (int c = 0; c < K; c++) a[c] = S[pidx(rr, c)] * (scaled_dof(c) ? dl * readlane_d(dl, c) : dl);
   bool ok = true;
 #if PSP_PCHOL_LDS
-  pchol_step_lds<K, 0>(a, r, ok, colbuf);
+  pchol_step_lds<K, 0>(a, r, ok, colbuf, readlane_d(a[0], 0));
   psync();  // colbuf (stg) is reused right after
 #else
   (void)colbuf;
@@ -402,11 +405,30 @@ struct PredRows {
 // ---------------------------------------------------------------------------
 // predictionStepImpl (PoseUKF.cpp:446-474) + ukf::predict, PSP form
 // ---------------------------------------------------------------------------
+// dt^2 Q entries a lane needs every predict, loaded once per launch (row l's
+// band: (l,l), (l,l-1), (l,l-2)); used when sh.q_simple (Q block-diagonal with
+// no coupling between the rewritten rows < 9 and the rest, band <= 2)
+struct LaneQ {
+  double q0, q1, q2;
+};
+template <int DOF>
+UWVK_DEV LaneQ lane_q(const double* fq, int l) {
+  const double2* f2 = reinterpret_cast<const double2*>(fq);
+  LaneQ q{0.0, 0.0, 0.0};
+  if (l < DOF) {
+    q.q0 = f2[pidx(l, l)].y;
+    if (l >= 1) q.q1 = f2[pidx(l, l - 1)].y;
+    if (l >= 2) q.q2 = f2[pidx(l, l - 2)].y;
+  }
+  return q;
+}
+
 // Q: process_noise_cov (DOF x DOF); fq: per packed entry {., dt^2 Q_ij} (host-made per dt)
 // ds, ids: this lane's time scale d_l and 1/d_l (updated: d' = A_ll d)
 template <int DOF>
 UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q,
-                          const double* fq, double& ds, double& ids, Stamper* st = nullptr) {
+                          const double* fq, double& ds, double& ids, const LaneQ& lq,
+                          Stamper* st = nullptr) {
   using L = Lay<DOF>;
   using G = PG<DOF>;
   constexpr int K = G::KP;
@@ -530,6 +552,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   UWVK_STAMP(24);
   // rewrite rows/cols < 9 (stored as Sigma / d'_l): A-coupled rows (pos, vel),
   // orientation rows (cross terms), ori x ori
+  const bool qs = sh.q_simple != 0;
   if (l < DOF && !(l >= 3 && l < 6)) {
     const bool jpv = jc >= 0;
     const double2* f2 = reinterpret_cast<const double2*>(fq);
@@ -537,12 +560,13 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     for (int q = 0; q < 6; q++)
       if (!jpv || l <= pv[q]) {
         const int e = pidx(pv[q], l);
-        sm.S[e] = (nv[q] + f2[e].y) * ids;
+        const double qq = qs ? (l == pv[q] ? lq.q0 : 0.0) : f2[e].y;
+        sm.S[e] = (nv[q] + qq) * ids;
       }
 #pragma unroll
     for (int i = 0; i < 3; i++) {
       const int e = pidx(3 + i, l);
-      sm.S[e] = (X[i] + f2[e].y) * ids;
+      sm.S[e] = (X[i] + (qs ? 0.0 : f2[e].y)) * ids;
     }
   }
   if (l < 9 && (l / 3) >= (l % 3)) {
@@ -563,7 +587,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       const int j = l - k;
       if (l >= R0 && l < DOF && j >= R0 && k <= bw) {
         const int e = pidx(l, j);
-        double q = f2[e].y;
+        double q = qs ? (k == 0 ? lq.q0 : (k == 1 ? lq.q1 : lq.q2)) : f2[e].y;
         if (k == 0 && l >= L::d_wv && l < L::d_wv + 4) q = dt2 * (sh.q_wv[l - L::d_wv] + wv_add);
         if (q != 0.0) sm.S[e] += q * (ids * idk);
       }
@@ -886,10 +910,18 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
 #pragma unroll 1
     for (int i0 = 0; i0 < DOF; i0 += RB) {
       double sv[RB];
+#if PSP_RANKM_LDS
+      double cv[RB][M];  // C~ rows of the block, broadcast loads issued up front
+#endif
 #pragma unroll
       for (int r = 0; r < RB; r++) {
         const int i = i0 + r;
         sv[r] = (i < DOF && l <= i) ? sm.S[i * (i + 1) / 2 + l] : 0.0;
+#if PSP_RANKM_LDS
+        const int ic = i < DOF ? i : DOF - 1;
+#pragma unroll
+        for (int a2 = 0; a2 < M; a2++) cv[r][a2] = sm.stg[M * ic + a2];
+#endif
       }
 #pragma unroll
       for (int r = 0; r < RB; r++) {
@@ -898,7 +930,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
 #pragma unroll
         for (int a2 = 0; a2 < M; a2++) {
 #if PSP_RANKM_LDS
-          s2 += sm.stg[M * i + a2] * Kt[a2];
+          s2 += cv[r][a2] * Kt[a2];
 #else
           s2 += readlane_d(Ct[a2], i) * Kt[a2];
 #endif

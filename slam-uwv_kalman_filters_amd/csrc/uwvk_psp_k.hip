@@ -142,7 +142,8 @@ __global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, d
   pc.off = nullptr;
   pc.off_lane = lane_offset<DOF>(b, inst, lane_id());
   double ds = 1.0, ids = 1.0;
-  const bool ok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids);
+  const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
+  const bool ok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq);
   if (!ok && lane_id() == 0) b.status[inst] |= UWVK_ST_NOTPD;
   psp_fold<DOF>(sm, ds, ids);
   store_psp<DOF>(sm, b, inst);
@@ -196,6 +197,7 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
   load_psp<DOF>(sm, b, inst);
   UWVK_STAMP(40);
   double ds = 1.0, ids = 1.0;  // time scale of the Markov DOFs (Sigma = D Sigma~ D)
+  const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
   bool ok = true, nan = false;
   uint32_t cnt[4] = {0, 0, 0, 0};
   MeasArgs ma{};
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
     const PoseShared& sh = shared_for_epoch(b);
     UWVK_STAMP(41);
     if (((e - ea.first) & 1023) == 1023) psp_fold<DOF>(sm, ds, ids);  // keep d in range
-    bool sok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids, st);
+    bool sok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, st);
     ok = ok && sok;
     if (fl & UWVK_EV_ACC) {
       if (all_finite(za, 3)) {
