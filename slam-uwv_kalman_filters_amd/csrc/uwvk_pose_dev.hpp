@@ -399,6 +399,8 @@ struct ProcCtx {
   double dt;
   const double* off;  // per-instance offsets (global, uniform address)
   double off_lane;    // PSP: the one offset storage component `lane` decays towards
+  double nt_lane;     // PSP: -1/tau of storage component `lane` (0: not a Markov state)
+  int vpart;          // PSP: storage index added times dt (pos <- vel, vel <- acc), or -1
 };
 
 template <int DOF>

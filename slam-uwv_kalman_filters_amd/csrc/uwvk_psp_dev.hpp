@@ -377,6 +377,15 @@ UWVK_DEV double proc_vect(int s, const double* mu, const PoseShared& sh, const P
   return x;  // acceleration, gravity
 }
 
+// the same, branch-free from the lane constants (psp::lane_proc, set once per
+// launch): x + dt * mu[vpart] | x + dt * (nt (x - off)) | x
+UWVK_DEV double proc_vect_lane(int s, const double* mu, const ProcCtx& c) {
+  const double x = mu[s];
+  const double y = mu[c.vpart >= 0 ? c.vpart : s];
+  const double d = c.vpart >= 0 ? y : c.nt_lane * (x - c.off_lane);
+  return (c.vpart >= 0 || c.nt_lane != 0.0) ? x + c.dt * d : x;
+}
+
 // Jacobian of the affine rows of f: A = diag(ad) + dt * (pos <- vel, vel <- acc)
 template <int DOF>
 UWVK_DEV double proc_diag(int d, const PoseShared& sh, double dt) {
@@ -605,7 +614,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   UWVK_STAMP(25);
   // new mean: vect parts f(mu), orientation the manifold mean
   double mv = 0.0;
-  if (l < L::store && !(l >= 3 && l < 7)) mv = proc_vect<DOF>(l, sm.mu, sh, pc);
+  if (l < L::store && !(l >= 3 && l < 7)) mv = proc_vect_lane(l, sm.mu, pc);
   psync();
   if (l < L::store && !(l >= 3 && l < 7)) sm.mu[l] = mv;
   if (l < 4) sm.mu[3 + l] = mq[l];

@@ -38,18 +38,28 @@ UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
   psync();
 }
 
-// the offset storage component `lane` decays towards (PoseUKF.cpp:43-59, 77-79)
+// per-lane process-model constants of storage component s (PoseUKF.cpp:24-79):
+// the state it integrates (pos <- vel, vel <- acc), or its Markov decay -1/tau
+// and the offset it decays towards
 template <int DOF>
-UWVK_DEV double lane_offset(const PoseBufs& b, int64_t inst, int s) {
+UWVK_DEV void lane_proc(const PoseBufs& b, const PoseShared& sh, int64_t inst, int s, ProcCtx& pc) {
   using L = Lay<DOF>;
+  const uwvk_pose_parameter& P = sh.p;
+  pc.vpart = s < 3 ? L::s_vel + s : ((s >= L::s_vel && s < L::s_vel + 3) ? L::s_acc + s - L::s_vel : -1);
+  pc.nt_lane = 0.0;
+  pc.off_lane = 0.0;
   int k = -1;
+  if (s >= L::s_bg && s < L::s_bg + 3) { pc.nt_lane = sh.ntau[0]; pc.off_lane = P.gyro_bias_offset[s - L::s_bg]; }
+  if (s >= L::s_ba && s < L::s_ba + 3) { pc.nt_lane = sh.ntau[1]; pc.off_lane = P.acc_bias_offset[s - L::s_ba]; }
   if constexpr (L::has_params) {
-    if (s >= L::s_inertia && s < L::s_inertia + 9) k = s - L::s_inertia;
-    if (s >= L::s_lin && s < L::s_lin + 9) k = 9 + s - L::s_lin;
-    if (s >= L::s_quad && s < L::s_quad + 9) k = 18 + s - L::s_quad;
+    if (s >= L::s_inertia && s < L::s_inertia + 9) { k = s - L::s_inertia; pc.nt_lane = sh.ntau[2]; }
+    if (s >= L::s_lin && s < L::s_lin + 9) { k = 9 + s - L::s_lin; pc.nt_lane = sh.ntau[3]; }
+    if (s >= L::s_quad && s < L::s_quad + 9) { k = 18 + s - L::s_quad; pc.nt_lane = sh.ntau[4]; }
   }
-  if (s == L::s_rho) k = 27;
-  return k >= 0 ? b.off[inst * 28 + k] : 0.0;
+  if (s >= L::s_wv && s < L::s_wv + 4) pc.nt_lane = sh.ntau[5];
+  if (s >= L::s_badcp && s < L::s_badcp + 2) pc.nt_lane = sh.ntau[6];
+  if (s == L::s_rho) { k = 27; pc.nt_lane = sh.ntau[7]; }
+  if (k >= 0) pc.off_lane = b.off[inst * 28 + k];
 }
 
 template <int DOF>
@@ -140,7 +150,7 @@ __global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, d
   for (int k = 0; k < 3; k++) pc.w[k] = b.rot[inst * 3 + k];
   pc.dt = dt;
   pc.off = nullptr;
-  pc.off_lane = lane_offset<DOF>(b, inst, lane_id());
+  lane_proc<DOF>(b, sh, inst, lane_id(), pc);
   double ds = 1.0, ids = 1.0;
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
   const bool ok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq);
@@ -207,7 +217,7 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
   for (int k = 0; k < 3; k++) pc.w[k] = w[k];
   pc.dt = ea.dt;
   pc.off = nullptr;
-  pc.off_lane = lane_offset<DOF>(b, inst, lane_id());
+  lane_proc<DOF>(b, *b.shared, inst, lane_id(), pc);
   // the next epoch's IMU inputs are prefetched one epoch ahead (their load
   // latency overlaps this epoch's arithmetic)
   uint32_t fl_n = 0;
