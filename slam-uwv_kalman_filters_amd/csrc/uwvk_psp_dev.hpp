@@ -31,8 +31,11 @@
 #ifndef PSP_RB
 #define PSP_RB 8          // rows per block of the row-block sweeps
 #endif
-#ifndef PSP_PCHOL_LDS
-#define PSP_PCHOL_LDS 1   // partial Cholesky: 1 broadcast column through LDS, 0 readlane
+// ablation knobs for timing analysis only (results are invalid when set):
+// PSP_ABL = bitmask: 1 mean 1 iteration, 2 no rank-m pass, 4 no L Delta / X,
+// 8 no predict Cholesky, 16 no predict points, 32 no update Cholesky, 64 no HG/C/S
+#ifndef PSP_ABL
+#define PSP_ABL 0
 #endif
 #ifndef PSP_RANKM_LDS
 #define PSP_RANKM_LDS 1   // Sigma~ -= C~ K~^T: 1 C~_i by LDS broadcast, 0 by readlane
@@ -174,30 +177,17 @@ UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
 // k-column partial Cholesky, lane r owns row r: a[c] = L[r][c] (0 above the
 // diagonal).  Right-looking; L[c][J] is broadcast from lane c's registers.
 // ---------------------------------------------------------------------------
-template <int K, int J>
-UWVK_DEV void pchol_step(double (&a)[K], int r, bool& ok) {
-  if constexpr (J < K) {
-    const double piv = readlane_d(a[J], J);
-    ok = ok && (piv > 0.0);
-    const double inv = rsqrt_f64(piv);
-    a[J] = (r == J) ? piv * inv : (r > J ? a[J] * inv : 0.0);
-#pragma unroll
-    for (int c = J + 1; c < K; c++) a[c] -= a[J] * readlane_d(a[J], c);
-#pragma unroll
-    for (int c = J + 1; c < K; c++) asm volatile("" : "+v"(a[c]));
-    pchol_step<K, J + 1>(a, r, ok);
-  }
-}
-
 // DOFs whose first-order Markov decay is carried by the time scale
 // (Sigma = D Sigma~ D, D = diag(d)): gyro/acc bias, model parameters, water
 // velocities, ADCP bias, density.  Position, orientation, velocity,
 // acceleration and gravity keep d = 1.
 UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 
-// variant: column J broadcast through a double-buffered LDS column (no readlanes)
+// column J broadcast through an LDS column (no readlanes); the rows the
+// sigma-point lanes need (RL::rows) are staged in the same step: lane r with
+// q = row_pos(r) writes L[r][J] to rows[q*K + J] (one write per column)
 template <int K, int J>
-UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* colbuf, double piv) {
+UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, double* rows, int q, double piv) {
   if constexpr (J < K) {
     ok = ok && (piv > 0.0);
     const double inv = rsqrt_f64(piv);
@@ -206,9 +196,9 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* colbuf, do
     // registers), so its rsqrt need not wait for the column broadcast
     double pnext = 0.0;
     if constexpr (J + 1 < K) pnext = readlane_d(a[J + 1] - a[J] * a[J], J + 1);
+    if (q >= 0) rows[q * K + J] = a[J];
     if constexpr (J + 1 < K) {
-      double* col = colbuf + (J & 1) * 64;
-      col[r] = a[J];
+      if (r < K) col[r] = a[J];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -217,25 +207,27 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* colbuf, do
 #pragma unroll
       for (int c = J + 1; c < K; c++) asm volatile("" : "+v"(a[c]));
     }
-    pchol_step_lds<K, J + 1>(a, r, ok, colbuf, pnext);
+    pchol_step_lds<K, J + 1>(a, r, ok, col, rows, q, pnext);
   }
 }
 
-// panel Sigma[r][0..K) = d_r d_c Sigma~[r][c] (dl: this lane's d); colbuf:
-// 128 doubles of LDS scratch (PSP_PCHOL_LDS)
-template <int DOF, int K>
-UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* colbuf) {
+// staged rows of L_a start here inside sm.stg (the column buffer is stg[0..32))
+constexpr int STG_ROWS = 32;
+
+// panel Sigma[r][0..K) = d_r d_c Sigma~[r][c] (dl: this lane's d); stg: the
+// staging area (column buffer + the rows of RL::rows, see STG_ROWS)
+template <int DOF, int K, class RL>
+UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* stg) {
   const int rr = r < DOF ? r : DOF - 1;
 #pragma unroll
   for (int c = 0; c < K; c++) a[c] = S[pidx(rr, c)] * (scaled_dof(c) ? dl * readlane_d(dl, c) : dl);
   bool ok = true;
-#if PSP_PCHOL_LDS
-  pchol_step_lds<K, 0>(a, r, ok, colbuf, readlane_d(a[0], 0));
-  psync();  // colbuf (stg) is reused right after
-#else
-  (void)colbuf;
-  pchol_step<K, 0>(a, r, ok);
-#endif
+  int q = -1;
+#pragma unroll
+  for (int k = 0; k < RL::NR; k++) q = (r == RL::rows[k]) ? k : q;
+  static_assert(K <= STG_ROWS && STG_ROWS + RL::NR * K <= 160, "staging area");
+  pchol_step_lds<K, 0>(a, r, ok, stg, stg + STG_ROWS, q, readlane_d(a[0], 0));
+  psync();  // the staged rows are read by the point lanes next
   return ok;
 }
 
@@ -245,18 +237,6 @@ UWVK_DEV constexpr int row_pos(const int (&rows)[NR], int d) {
   for (int q = 0; q < NR; q++)
     if (rows[q] == d) return q;
   return -1;
-}
-
-// lanes owning rows in ROWS write L[r][0..K) into stg[q*K + j]
-template <class RL, int K>
-UWVK_DEV void stage_rows(double* stg, int r, const double (&a)[K]) {
-#pragma unroll
-  for (int q = 0; q < RL::NR; q++) {
-    if (r == RL::rows[q]) {
-#pragma unroll
-      for (int j = 0; j < K; j++) stg[q * K + j] = a[j];
-    }
-  }
 }
 
 // point p (< 2K: column p>>1, sign + for even p; p == 2K: centre) restricted to
@@ -463,17 +443,24 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   const double wv_add = sh.p.water_velocity_scale * (vs0 * vs0 + vs1 * vs1 + vs2 * vs2) * dt;
   // partial Cholesky and row staging
   double a[K];
-  const bool ok = pchol<DOF, K>(sm.S, l, a, ds, sm.stg);
-  stage_rows<PredRows, K>(sm.stg, l, a);
-  psync();
+#if PSP_ABL & 8
+  bool ok = true;
+  for (int c = 0; c < K; c++) a[c] = sm.S[pidx(l < DOF ? l : DOF - 1, c)];
+#else
+  const bool ok = pchol<DOF, K, PredRows>(sm.S, l, a, ds, sm.stg);
+#endif
   UWVK_STAMP(20);
   // sigma points: lanes < 2K plus the centre lane 2K; orientation output only
   const bool pt = l < 2 * K, ctr = l == 2 * K;
   double o[4];
   {
     double x[L::store];
-    gen_rows<PredRows, DOF, K>(sm.mu, sm.stg, l, x);
+    gen_rows<PredRows, DOF, K>(sm.mu, sm.stg + STG_ROWS, l, x);
+#if PSP_ABL & 16
+    for (int i = 0; i < 4; i++) o[i] = x[3 + i];
+#else
     proc_orientation<DOF>(x, sh, pc, o);
+#endif
   }
   UWVK_STAMP(21);
   // manifold mean of the orientations (ukfom: ref = X_0, Gauss-Newton, |d| <= 1e-6)
@@ -500,7 +487,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #pragma unroll
       for (int i = 0; i < 4; i++) mq[i] = q[i];
       nrm = sqrt(nrm);
-    } while (nrm > 1e-6 && ++it < 10000);
+    } while (!(PSP_ABL & 1) && nrm > 1e-6 && ++it < 10000);
   }
   UWVK_STAMP(22);
   // deviations; ori x ori block; Delta_j = d_{j+} - d_{j-}
@@ -525,7 +512,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   {
     double Y[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-    for (int j = 0; j < K; j++)
+    for (int j = 0; j < ((PSP_ABL & 4) ? 0 : K); j++)
 #pragma unroll
       for (int i = 0; i < 3; i++) Y[i] += a[j] * readlane_d(dd[i], 2 * j);
     const int cp = proc_couple(l);
@@ -762,16 +749,18 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double a[KA];
   bool cok = true;
   if constexpr (K > 0) {
-    cok = pchol<DOF, K>(sm.S, l, a, ds, sm.stg);
-    stage_rows<HM, K>(sm.stg, l, a);
-    psync();
+#if PSP_ABL & 32
+    for (int c = 0; c < K; c++) a[c] = sm.S[pidx(l < DOF ? l : DOF - 1, c)];
+#else
+    cok = pchol<DOF, K, HM>(sm.S, l, a, ds, sm.stg);
+#endif
   }
   UWVK_STAMP(30);
   const bool pt = l < 2 * K;
   double zp[M];
   {
     double x[L::store];
-    gen_rows<HM, DOF, K>(sm.mu, sm.stg, l, x);
+    gen_rows<HM, DOF, K>(sm.mu, sm.stg + STG_ROWS, l, x);
     hm.eval(x, zp);
   }
   double zc[M], zb[M], e[M];
@@ -821,7 +810,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       double h = Hs[0][t];
 #pragma unroll
       for (int ii = 1; ii < M; ii++) h = (i == ii) ? Hs[ii][t] : h;
-      Pl += h * sm.stg[row_pos(HM::rows, HM::cols[t]) * K + j];
+      Pl += h * sm.stg[STG_ROWS + row_pos(HM::rows, HM::cols[t]) * K + j];
     }
   }
   const int rl = l < DOF ? l : DOF - 1;
@@ -917,7 +906,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     // row blocks of RB: every load of a block is issued before its stores
     constexpr int RB = PSP_RB;
 #pragma unroll 1
-    for (int i0 = 0; i0 < DOF; i0 += RB) {
+    for (int i0 = 0; i0 < ((PSP_ABL & 2) ? 0 : DOF); i0 += RB) {
       double sv[RB];
 #if PSP_RANKM_LDS
       double cv[RB][M];  // C~ rows of the block, broadcast loads issued up front
