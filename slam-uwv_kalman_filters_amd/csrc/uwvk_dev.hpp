@@ -119,6 +119,16 @@ UWVK_DEV void qboxminus(const double a[4], const double b[4], double o[3]) {
 // ---------------------------------------------------------------------------
 UWVK_DEV int lane_id() { return threadIdx.x & 63; }
 
+// filter instance of this workgroup (one workgroup per instance).  Workgroups
+// are dealt round-robin to the 8 XCDs (workgroup w runs on XCD w % 8), so XCD
+// x is given the contiguous instances [x n, (x+1) n): neighbouring instances'
+// per-epoch input rows (24 B, five to a 128-B line) then meet in one L2
+// instead of being fetched once per XCD.  The tail past 8n maps to itself.
+UWVK_DEV int64_t xcd_instance(int64_t batch) {
+  const int64_t w = blockIdx.x, n = batch >> 3;
+  return w < (n << 3) ? (w & 7) * n + (w >> 3) : w;
+}
+
 UWVK_DEV double shfl_d(double v, int src) {
   int lo = __double2loint(v), hi = __double2hiint(v);
   lo = __shfl(lo, src, 64);

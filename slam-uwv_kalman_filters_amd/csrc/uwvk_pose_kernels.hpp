@@ -187,7 +187,7 @@ UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, 
 template <int DOF>
 __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_predict(PoseBufs b, PoseShared sh, double dt) {
   __shared__ Smem<DOF> sm;
-  const int64_t i = blockIdx.x;
+  const int64_t i = xcd_instance(b.batch);
   load_instance<DOF>(sm, b, i);
   ProcCtx pc;
   for (int k = 0; k < 3; k++) pc.w[k] = b.rot[i * 3 + k];
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_predict(PoseBufs b, PoseSh
 template <int DOF, int K>
 __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_update(PoseBufs b, PoseShared sh, MeasArgs ma, int m) {
   __shared__ Smem<DOF> sm;
-  const int64_t i = blockIdx.x;
+  const int64_t i = xcd_instance(b.batch);
   if (ma.mask && !ma.mask[i]) {
     if (ma.accepted && tid() == 0) ma.accepted[i] = 0;
     return;
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_update(PoseBufs b, PoseSha
 template <int DOF>
 __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_epoch(PoseBufs b, PoseShared sh, EpochArgs ea) {
   __shared__ Smem<DOF> sm;
-  const int64_t i = blockIdx.x, B = b.batch;
+  const int64_t B = b.batch, i = xcd_instance(B);
 #ifdef UWVK_STAMPS
   Stamper stamper;
   Stamper* st = &stamper;

@@ -167,6 +167,14 @@ UWVK_DEV void qboxminus_psp(const double a[4], const double b[4], double o[3]) {
 // value of lane l ^ 1 (quad_perm [1,0,3,2])
 UWVK_DEV double swap_pair_d(double v) { return dpp_d<0xb1, 0xf, 0xf>(v); }
 
+// v_i for a lane-varying i as a select chain on scalars (a dynamically
+// indexed private array would be placed in scratch memory, and a select
+// chain over array elements is folded back into such an indexed load)
+UWVK_DEV double sel3(double v0, double v1, double v2, int i) { return i == 0 ? v0 : (i == 1 ? v1 : v2); }
+UWVK_DEV double sel6(double v0, double v1, double v2, double v3, double v4, double v5, int i) {
+  return i < 3 ? sel3(v0, v1, v2, i) : sel3(v3, v4, v5, i - 3);
+}
+
 UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_barrier();
@@ -429,13 +437,19 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     double R[9];
     qmatrix(sm.mu + L::s_quat, R);
     const int r = l / 3, c = l % 3;
+    double Rr[3], Rc[3];
+#pragma unroll
+    for (int m = 0; m < 3; m++) {
+      Rr[m] = sel3(R[m], R[3 + m], R[6 + m], r);
+      Rc[m] = sel3(R[m], R[3 + m], R[6 + m], c);
+    }
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       double u = 0.0;
 #pragma unroll
-      for (int m = 0; m < 3; m++) u += R[r * 3 + m] * sh.q_ori[m * 3 + k];
-      s += u * R[c * 3 + k];
+      for (int m = 0; m < 3; m++) u += Rr[m] * sh.q_ori[m * 3 + k];
+      s += u * Rc[k];
     }
     qo_lane = s;
   }
@@ -567,7 +581,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   }
   if (l < 9 && (l / 3) >= (l % 3)) {
     const int a2 = l / 3, b2 = l % 3;
-    sm.S[pidx(3 + a2, 3 + b2)] = oo[a2 * (a2 + 1) / 2 + b2] + dt2 * qo_lane;
+    sm.S[pidx(3 + a2, 3 + b2)] = sel6(oo[0], oo[1], oo[2], oo[3], oo[4], oo[5], a2 * (a2 + 1) / 2 + b2) + dt2 * qo_lane;
   }
   // rows/cols >= 9: A Sigma A^T = D' Sigma~ D' leaves Sigma~ unchanged; only
   // dt^2 Q / (d'_i d'_j) is added on Q's band.  Lane l owns row l's band
@@ -963,8 +977,8 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       for (int u = 0; u < 3; u++) {
         double t = 0.0;
 #pragma unroll
-        for (int v = 0; v < 3; v++) t += sm.S[pidx(3 + u, 3 + v)] * R[c * 3 + v];
-        s += R[r * 3 + u] * t;
+        for (int v = 0; v < 3; v++) t += sm.S[pidx(3 + u, 3 + v)] * sel3(R[v], R[3 + v], R[6 + v], c);
+        s += sel3(R[u], R[3 + u], R[6 + u], r) * t;
       }
       nb = s;
     }

@@ -64,19 +64,15 @@ UWVK_DEV void lane_proc(const PoseBufs& b, const PoseShared& sh, int64_t inst, i
 
 template <int DOF>
 UWVK_DEV void store_psp(const PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
-  using G = PG<DOF>;
+  // the full symmetric matrix in row-major order, 64 consecutive entries per
+  // store instruction (a mirrored write of the packed triangle would scatter
+  // column-strided 8-B stores)
   const int l = lane_id();
   double* gs = b.sigma + inst * (int64_t)(DOF * DOF);
 #pragma unroll 4
-  for (int t = 0; t < G::NSLOT; t++) {
-    const int e = l + 64 * t;
-    if (e < G::NP) {
-      int i, j;
-      unpack(e, i, j);
-      const double s = sm.S[e];
-      gs[i * DOF + j] = s;
-      if (i != j) gs[j * DOF + i] = s;
-    }
+  for (int e = l; e < DOF * DOF; e += 64) {
+    const int i = e / DOF, j = e - i * DOF;
+    gs[e] = sm.S[pidx(i, j)];
   }
   if (l < Lay<DOF>::store) b.mu[inst * Lay<DOF>::store + l] = sm.mu[l];
 }
@@ -144,7 +140,7 @@ UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, co
 template <int DOF>
 __global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, double dt) {
   __shared__ PspSmem<DOF> sm;
-  const int64_t inst = blockIdx.x;
+  const int64_t inst = xcd_instance(b.batch);
   load_psp<DOF>(sm, b, inst);
   ProcCtx pc;
   for (int k = 0; k < 3; k++) pc.w[k] = b.rot[inst * 3 + k];
@@ -162,7 +158,7 @@ __global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, d
 template <int DOF, int KIND>
 __global__ __launch_bounds__(64) void k_psp_update(PoseBufs b, PoseShared sh, MeasArgs ma, int m) {
   __shared__ PspSmem<DOF> sm;
-  const int64_t inst = blockIdx.x;
+  const int64_t inst = xcd_instance(b.batch);
   if (ma.mask && !ma.mask[inst]) {
     if (ma.accepted && lane_id() == 0) ma.accepted[inst] = 0;
     return;
@@ -197,7 +193,7 @@ UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
 template <int DOF>
 __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
-  const int64_t inst = blockIdx.x, B = b.batch;
+  const int64_t B = b.batch, inst = xcd_instance(B);
 #ifdef UWVK_STAMPS
   Stamper stamper;
   Stamper* st = &stamper;
