@@ -338,6 +338,51 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
 uwvk_status uwvk_pose_timer_start(uwvk_pose* h);
 uwvk_status uwvk_pose_timer_stop(uwvk_pose* h, float* elapsed_ms);
 
+/* ---- recorded-mission ingestion (host only, no device needed) ---------- */
+/* The reference is driven by its caller's stream aligner (Rock orogen task,
+ * outside the repository): RotationRate + predictionStep +
+ * Acceleration per IMU sample (PoseUKF.cpp:446-496), the lower-rate sensors
+ * integrated as their samples arrive (PoseUKF.cpp:476-611).  This turns the
+ * per-sensor sample stamps of a recording into the epoch-indexed flags and
+ * row indices of uwvk_pose_log (the payload arrays keep sample order).
+ * Semantics: DESIGN.md §11 (fixed-step replay, lag < dt, per-sensor queue). */
+typedef struct uwvk_stream_times { /* seconds, ascending per sensor; NULL when n = 0 */
+  const double* imu;      int64_t n_imu;  /* one epoch per IMU sample */
+  const double* dvl;      int64_t n_dvl;
+  const double* pressure; int64_t n_pressure;
+  const double* adcp;     int64_t n_adcp;  /* one sample = all cells of one ADCP ping */
+  const double* efforts;  int64_t n_efforts;
+  const uint8_t* efforts_velocity_only;    /* [n_efforts], nullable: only_affect_velocity */
+} uwvk_stream_times;
+
+typedef struct uwvk_schedule {
+  /* caller-allocated HOST arrays of n_imu entries (index arrays may be NULL
+   * when that sensor has no samples) */
+  uint32_t* flags;         /* UWVK_EV_* per epoch */
+  int32_t* dvl_index;      /* row of the sample integrated at that epoch, -1 = none */
+  int32_t* pressure_index;
+  int32_t* adcp_index;
+  int32_t* efforts_index;
+  /* outputs */
+  double dt;               /* mean IMU interval (0 for a single sample) */
+  int64_t epochs;
+  int64_t kept[4];         /* DVL, pressure, ADCP, efforts samples placed */
+  int64_t dropped[4];      /* before the first IMU stamp / queued past the last epoch */
+} uwvk_schedule;
+
+/* dt_tolerance: allowed |interval - dt| / dt of the IMU stream (non-uniform ->
+ * UWVK_EINVAL); time_epsilon: stamp slack in seconds. */
+uwvk_status uwvk_schedule_streams(const uwvk_stream_times* in, double dt_tolerance, double time_epsilon,
+                                  uwvk_schedule* out);
+
+/* ADCP cell weighting for integrateMeasurement(WaterVelocityMeasurement,
+ * cell_weighting) (PoseUKF.cpp:133-151,604-611) from cell_size and
+ * first_cell_blank (PoseUKFConfig.hpp:34-38): 0 at the nearest cell centre,
+ * 1 at the farthest, linear in range.  valid[i] (nullable) = correlation[i] >=
+ * minimum_correlation (PoseUKFConfig.hpp:40-41), all 1 when correlation is NULL. */
+uwvk_status uwvk_adcp_cell_weighting(const uwvk_water_velocity* wv, int32_t cells, const double* correlation,
+                                     double* weighting, uint8_t* valid);
+
 /* ======================================================================== */
 /* VelocityUKF (src/VelocityUKF.hpp:231-266)                                 */
 /* ======================================================================== */

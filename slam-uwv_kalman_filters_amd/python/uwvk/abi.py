@@ -80,6 +80,18 @@ class VelLog(C.Structure):  # uwvk_vel_log (device pointers)
                 ("pressure_index", P), ("pressure", P), ("pressure_cov", D)]
 
 
+class StreamTimes(C.Structure):  # uwvk_stream_times (host pointers)
+    _fields_ = [("imu", P), ("n_imu", C.c_int64), ("dvl", P), ("n_dvl", C.c_int64),
+                ("pressure", P), ("n_pressure", C.c_int64), ("adcp", P), ("n_adcp", C.c_int64),
+                ("efforts", P), ("n_efforts", C.c_int64), ("efforts_velocity_only", P)]
+
+
+class Schedule(C.Structure):  # uwvk_schedule (host pointers)
+    _fields_ = [("flags", P), ("dvl_index", P), ("pressure_index", P), ("adcp_index", P),
+                ("efforts_index", P), ("dt", D), ("epochs", C.c_int64),
+                ("kept", _arr(C.c_int64, 4)), ("dropped", _arr(C.c_int64, 4))]
+
+
 # event flags (include/uwvk.h)
 EV_ACC = 0x1
 EV_DVL = 0x2

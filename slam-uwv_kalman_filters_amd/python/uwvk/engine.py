@@ -32,6 +32,7 @@ SYMBOLS = [
     "uwvk_vel_create", "uwvk_vel_destroy", "uwvk_vel_stream", "uwvk_vel_init", "uwvk_vel_setup_motion_model",
     "uwvk_vel_set_gyro", "uwvk_vel_set_efforts", "uwvk_vel_predict", "uwvk_vel_update_dvl",
     "uwvk_vel_update_pressure", "uwvk_vel_get_state", "uwvk_vel_get_model_state", "uwvk_vel_run_log",
+    "uwvk_schedule_streams", "uwvk_adcp_cell_weighting",
 ]
 
 _LIB = None
