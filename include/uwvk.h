@@ -121,7 +121,7 @@ typedef struct uwvk_hydrostatics { /* HydrostaticConfiguration, PoseUKFConfig.hp
   double pressure_std;
 } uwvk_hydrostatics;
 
-typedef struct uwvk_pose_config { /* PoseUKFConfig, PoseUKFConfig.hpp:159-194 (visual landmarks: out of scope) */
+typedef struct uwvk_pose_config { /* PoseUKFConfig, PoseUKFConfig.hpp:159-194 (visual-landmark config: passed per call) */
   uwvk_inertial_noise acceleration;
   uwvk_inertial_noise rotation_rate;
   uwvk_model_noise model_noise_parameters;
@@ -254,6 +254,24 @@ uwvk_status uwvk_pose_update_geographic(uwvk_pose* h, const double* mu, const do
 uwvk_status uwvk_pose_update_delayed_xy(uwvk_pose* h, const double* mu, const double* cov,
                                         const double* shared_cov, const double* delayed_xy,
                                         const uint8_t* mask, uint8_t* accepted);
+/* integrateMeasurement(vector<VisualFeatureMeasurement>, feature_positions, marker_pose,
+ * cov_marker_pose, camera_config, camera_in_IMU) (PoseUKF.cpp:613-654): the state is
+ * augmented with the marker pose (PoseStateWithMarker, :221-229), one S2-valued
+ * update per feature (measurementVisualLandmark, :231-244; accept any Mahalanobis
+ * distance), then reset to the leading block.  Per instance n_features features:
+ *   features           [batch][nf][2] undistorted image coordinates (px)
+ *   feature_cov        [batch][nf][4] (feature_cov_per_instance) or [nf][4], px^2
+ *   feature_positions  [nf][3] in the marker frame (shared)
+ *   marker_pose        [batch][7] (marker_pose_per_instance) or [7]: t(3), q(w,x,y,z)
+ *   cov_marker_pose    [36] (shared), camera {fx, fy, cx, cy}, camera_in_imu t(3) q(4)
+ * A NaN feature fails the whole call with UWVK_ENAN and changes nothing (the
+ * reference throws before its ukf.reset). */
+uwvk_status uwvk_pose_update_visual_landmark(uwvk_pose* h, int32_t n_features, const double* features,
+                                             const double* feature_cov, int feature_cov_per_instance,
+                                             const double* feature_positions, const double* marker_pose,
+                                             int marker_pose_per_instance, const double cov_marker_pose[36],
+                                             const double camera[4], const double camera_in_imu[7],
+                                             const uint8_t* mask);
 /* resetFilterWithExternalPose (PoseUKF.cpp:685-691): pose batch*7 {t, q(w,x,y,z)} */
 uwvk_status uwvk_pose_reset_with_external_pose(uwvk_pose* h, const double* pose);
 
@@ -426,6 +444,68 @@ typedef struct uwvk_vel_log {
   double pressure_cov;
 } uwvk_vel_log;
 uwvk_status uwvk_vel_run_log(uwvk_vel* h, const uwvk_vel_log* log, int64_t first, int64_t count);
+
+/* ======================================================================== */
+/* BottomUKF (src/BottomUKF.hpp:26-53, BottomUKF.cpp:1-71)                  */
+/* State {distance, normal}: 3 DOF, stored as 4 scalars {d, nx, ny, nz}      */
+/* (the normal is an MTK::S2 unit vector).             */
+/* ======================================================================== */
+#define UWVK_BOTTOM_DOF 3
+typedef struct uwvk_bottom uwvk_bottom;
+uwvk_status uwvk_bottom_create(int64_t batch, int device, uwvk_bottom** out);
+void uwvk_bottom_destroy(uwvk_bottom* h);
+void* uwvk_bottom_stream(const uwvk_bottom* h);
+/* BottomUKF(initial_state, state_cov) (BottomUKF.cpp:43-49): x batch*4 (normal
+ * normalised here, as MTK::S2 does), P batch*9; process noise = identity. */
+uwvk_status uwvk_bottom_init(uwvk_bottom* h, const double* x, const double* P);
+/* setProcessNoiseCovariance [EXT base]: 3x3, shared by the batch */
+uwvk_status uwvk_bottom_set_process_noise(uwvk_bottom* h, const double Q[9]);
+/* setVelocity (BottomUKF.cpp:69-72): batch*3 */
+uwvk_status uwvk_bottom_set_velocity(uwvk_bottom* h, const double* velocity);
+/* predictionStep -> predictionStepImpl (BottomUKF.cpp:51-57) */
+uwvk_status uwvk_bottom_predict(uwvk_bottom* h, double dt);
+/* integrateMeasurement(RangeMeasurement, unit_direction, origin) (BottomUKF.cpp:59-64):
+ * mu batch, cov batch (NULL = shared_cov); beam direction / origin shared. */
+uwvk_status uwvk_bottom_update_range(uwvk_bottom* h, const double* mu, const double* cov, double shared_cov,
+                                     const double unit_direction[3], const double origin[3], const uint8_t* mask);
+/* integrateMeasurement(NormalType, cov) (BottomUKF.cpp:66-70): mu batch*3 (normalised),
+ * cov batch*4 (NULL = shared_cov[4]) */
+uwvk_status uwvk_bottom_update_normal(uwvk_bottom* h, const double* mu, const double* cov, const double* shared_cov,
+                                      const uint8_t* mask);
+uwvk_status uwvk_bottom_get_state(uwvk_bottom* h, double* x, double* P);
+uwvk_status uwvk_bottom_get_status(uwvk_bottom* h, uint32_t* status, int clear);
+
+/* ======================================================================== */
+/* IndirectPoseUKF (src/IndirectPoseUKF.hpp:28-86, IndirectPoseUKF.cpp:1-147) */
+/* State {position_error, orientation_error}: 6 DOF, stored t(3) q(w,x,y,z).  */
+/* ======================================================================== */
+#define UWVK_IPOSE_DOF 6
+typedef struct uwvk_ipose uwvk_ipose;
+uwvk_status uwvk_ipose_create(int64_t batch, int device, uwvk_ipose** out);
+void uwvk_ipose_destroy(uwvk_ipose* h);
+void* uwvk_ipose_stream(const uwvk_ipose* h);
+/* IndirectPoseUKF(position_error_std, orientation_error_std, orientation_error_tau,
+ * initial_position_error, initial_position_error_std) (IndirectPoseUKF.cpp:66-91):
+ * stds shared; initial_position_error batch*3 (NULL = zero); initial std NULL = ones. */
+uwvk_status uwvk_ipose_init(uwvk_ipose* h, const double position_error_std[3], const double orientation_error_std[3],
+                            double orientation_error_tau, const double* initial_position_error,
+                            const double initial_position_error_std[3]);
+/* updatePoseReference (IndirectPoseUKF.cpp:144-147): batch*7 body in world, t(3) q(4) */
+uwvk_status uwvk_ipose_set_pose_reference(uwvk_ipose* h, const double* pose);
+/* predictionStep -> predictionStepImpl (IndirectPoseUKF.cpp:93-106) */
+uwvk_status uwvk_ipose_predict(uwvk_ipose* h, double dt);
+/* integrateMeasurement(marker_features, feature_positions, marker_pose, cov_marker_pose,
+ * camera_config, camera_in_body) (IndirectPoseUKF.cpp:108-140); arrays as for
+ * uwvk_pose_update_visual_landmark. */
+uwvk_status uwvk_ipose_update_visual(uwvk_ipose* h, int32_t n_features, const double* features,
+                                     const double* feature_cov, int feature_cov_per_instance,
+                                     const double* feature_positions, const double* marker_pose,
+                                     int marker_pose_per_instance, const double cov_marker_pose[36],
+                                     const double camera[4], const double camera_in_body[7], const uint8_t* mask);
+/* getCorrectedPose (IndirectPoseUKF.cpp:137-142): pose_ref * pose_error, batch*7 */
+uwvk_status uwvk_ipose_get_corrected_pose(uwvk_ipose* h, double* out);
+uwvk_status uwvk_ipose_get_state(uwvk_ipose* h, double* x, double* P);
+uwvk_status uwvk_ipose_get_status(uwvk_ipose* h, uint32_t* status, int clear);
 
 #ifdef __cplusplus
 }

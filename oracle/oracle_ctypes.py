@@ -259,3 +259,140 @@ class OracleVelBatch:
             if f & abi.EV_PRESSURE:
                 self.update_pressure(log["pressure"][log["pressure_index"][e]], log["pressure_cov"])
         return B
+
+
+# ---- BottomUKF / IndirectPoseUKF / visual landmarks (uwvk_small_oracle.c) ----
+def _per(a, batch, tail):
+    """shared [*tail] or per-instance [batch, *tail] -> [batch, *tail]"""
+    a = np.asarray(a, dtype=np.float64)
+    if a.shape == tuple(tail):
+        a = np.broadcast_to(a, (batch,) + tuple(tail))
+    return np.ascontiguousarray(a)
+
+
+def _pose_visual(L, fn, ptr, batch, features, feature_cov, feature_pos, marker_pose, cov_marker, cam, cam_in):
+    f = _f64(features)
+    nf = f.shape[1]
+    fc = _per(feature_cov, batch, (nf, 2, 2))
+    mp = _per(marker_pose, batch, (7,))
+    fp, cm, cc, ci = _f64(feature_pos), _f64(cov_marker), _f64(cam), _f64(cam_in)
+    for i in range(batch):
+        e = fn(ptr(i), C.c_int(nf), dp(f[i]), dp(fc[i]), dp(fp), dp(mp[i]), dp(cm), dp(cc), dp(ci))
+        if e:
+            raise RuntimeError("oracle visual update failed: %s" % abi.STATUS.get(e, e))
+
+
+def _pose_update_visual(self, features, feature_cov, feature_pos, marker_pose, cov_marker, cam, cam_in_imu):
+    """PoseUKF::integrateMeasurement(vector<VisualFeatureMeasurement>, ...) (PoseUKF.cpp:613-654)."""
+    _pose_visual(self.L, self.L.or_pose_update_visual, self.ptr, self.batch, features, feature_cov, feature_pos,
+                 marker_pose, cov_marker, cam, cam_in_imu)
+
+
+OraclePoseBatch.update_visual = _pose_update_visual
+
+
+class _SmallBatch:
+    SIZEOF = None
+
+    def __init__(self, batch):
+        self.L = lib()
+        getattr(self.L, self.SIZEOF).restype = C.c_size_t
+        self.batch = batch
+        self.sz = getattr(self.L, self.SIZEOF)()
+        self.buf = (C.c_char * (self.sz * batch))()
+
+    def ptr(self, i):
+        return C.cast(C.addressof(self.buf) + i * self.sz, C.c_void_p)
+
+    def _struct(self, i, n):
+        return np.frombuffer(self.buf, np.float64, count=n, offset=i * self.sz)
+
+
+class OracleBottomBatch(_SmallBatch):
+    """`batch` oracle BottomUKF instances (BottomUKF.hpp:26-53)."""
+    SIZEOF = "or_bottom_sizeof"
+
+    def init(self, x, P):
+        x, P = _f64(x), _f64(P)
+        for i in range(self.batch):
+            self.L.or_bottom_init(self.ptr(i), dp(x[i]), dp(P[i]))
+
+    def set_process_noise(self, Q):
+        for i in range(self.batch):
+            self.L.or_bottom_set_process_noise(self.ptr(i), dp(Q))
+
+    def set_velocity(self, v):
+        v = _per(v, self.batch, (3,))
+        for i in range(self.batch):
+            self.L.or_bottom_set_velocity(self.ptr(i), dp(v[i]))
+
+    def predict(self, dt):
+        for i in range(self.batch):
+            e = self.L.or_bottom_predict(self.ptr(i), C.c_double(dt))
+            if e:
+                raise RuntimeError("oracle bottom predict: %s" % abi.STATUS.get(e, e))
+
+    def update_range(self, mu, cov, direction, origin, mask=None):
+        mu, cov = _per(mu, self.batch, ()), _per(cov, self.batch, ())
+        for i in range(self.batch):
+            if mask is not None and not mask[i]:
+                continue
+            e = self.L.or_bottom_update_range(self.ptr(i), C.c_double(mu[i]), C.c_double(cov[i]), dp(direction),
+                                              dp(origin))
+            if e:
+                raise RuntimeError("oracle range update: %s" % abi.STATUS.get(e, e))
+
+    def update_normal(self, mu, cov):
+        mu, cov = _per(mu, self.batch, (3,)), _per(cov, self.batch, (2, 2))
+        for i in range(self.batch):
+            e = self.L.or_bottom_update_normal(self.ptr(i), dp(mu[i]), dp(cov[i]))
+            if e:
+                raise RuntimeError("oracle normal update: %s" % abi.STATUS.get(e, e))
+
+    def get_state(self):
+        x = np.empty((self.batch, 4))
+        P = np.empty((self.batch, 3, 3))
+        for i in range(self.batch):
+            s = self._struct(i, 13)
+            x[i], P[i] = s[:4], s[4:13].reshape(3, 3)
+        return x, P
+
+
+class OracleIndirectPoseBatch(_SmallBatch):
+    """`batch` oracle IndirectPoseUKF instances (IndirectPoseUKF.hpp:28-86)."""
+    SIZEOF = "or_ipose_sizeof"
+
+    def init(self, pos_std, ori_std, tau, init_pos_err=None, init_pos_std=None):
+        ipe = None if init_pos_err is None else _per(init_pos_err, self.batch, (3,))
+        for i in range(self.batch):
+            self.L.or_ipose_init(self.ptr(i), dp(pos_std), dp(ori_std), C.c_double(tau),
+                                 None if ipe is None else dp(ipe[i]), dp(init_pos_std))
+
+    def set_pose_reference(self, pose):
+        pose = _per(pose, self.batch, (7,))
+        for i in range(self.batch):
+            self.L.or_ipose_set_pose_reference(self.ptr(i), dp(pose[i]))
+
+    def predict(self, dt):
+        for i in range(self.batch):
+            e = self.L.or_ipose_predict(self.ptr(i), C.c_double(dt))
+            if e:
+                raise RuntimeError("oracle ipose predict: %s" % abi.STATUS.get(e, e))
+
+    def update_visual(self, features, feature_cov, feature_pos, marker_pose, cov_marker, cam, cam_in_body):
+        _pose_visual(self.L, self.L.or_ipose_update_visual, self.ptr, self.batch, features, feature_cov,
+                     feature_pos, marker_pose, cov_marker, cam, cam_in_body)
+
+    def get_corrected_pose(self):
+        out = np.empty((self.batch, 7))
+        for i in range(self.batch):
+            self.L.or_ipose_get_corrected_pose(self.ptr(i), dp(out[i]))
+        return out
+
+    def get_state(self):
+        x = np.empty((self.batch, 7))
+        P = np.empty((self.batch, 6, 6))
+        for i in range(self.batch):
+            s = self._struct(i, 43)
+            x[i], P[i] = s[:7], s[7:43].reshape(6, 6)
+        return x, P

@@ -123,6 +123,44 @@ void or_model_rk4(const uwvk_uwv_params* p, const double Minv[36], const double 
                   const double s_in[13], double s_out[13]);
 int or_invert(int n, const double* A, double* Ainv);
 
+/* ---- BottomUKF / IndirectPoseUKF / visual landmarks (uwvk_small_oracle.c) */
+typedef struct or_bottom {  /* BottomUKF.hpp:15-53: {distance, normal (S2, unit 3-vector)} */
+  double mu[4];
+  double sigma[9];
+  double Q[9];
+  double velocity[3];
+} or_bottom;
+void or_bottom_init(or_bottom* f, const double x[4], const double P[9]);
+void or_bottom_set_process_noise(or_bottom* f, const double Q[9]);
+void or_bottom_set_velocity(or_bottom* f, const double v[3]);
+int or_bottom_predict(or_bottom* f, double dt);
+int or_bottom_update_range(or_bottom* f, double mu, double cov, const double dir[3], const double origin[3]);
+int or_bottom_update_normal(or_bottom* f, const double mu[3], const double cov[4]);
+size_t or_bottom_sizeof(void);
+
+typedef struct or_ipose {  /* IndirectPoseUKF.hpp:18-86: {position_error, orientation_error} */
+  double mu[7];
+  double sigma[36];
+  double Q[36];
+  double pose_ref[7]; /* t(3), q(4) */
+  double tau;
+} or_ipose;
+void or_ipose_init(or_ipose* f, const double pos_std[3], const double ori_std[3], double tau,
+                   const double init_pos_err[3], const double init_pos_std[3]);
+void or_ipose_set_pose_reference(or_ipose* f, const double pose[7]);
+int or_ipose_predict(or_ipose* f, double dt);
+int or_ipose_update_visual(or_ipose* f, int nf, const double* features, const double* feature_cov,
+                           const double* feature_pos, const double marker_pose[7], const double cov_marker[36],
+                           const double cam_cfg[4], const double cam_in_body[7]);
+void or_ipose_get_corrected_pose(const or_ipose* f, double out[7]);
+size_t or_ipose_sizeof(void);
+int or_pose_update_visual(or_pose* f, int nf, const double* features, const double* feature_cov,
+                          const double* feature_pos, const double marker_pose[7], const double cov_marker[36],
+                          const double cam_cfg[4], const double cam_in_imu[7]);
+void or_s2_boxplus(const double x[3], const double d[2], double s, double o[3]);
+void or_s2_boxminus(const double y[3], const double x[3], double o[2]);
+void or_s2_from_vector(const double v[3], double o[3]);
+
 /* ---- batched log runners (cpu_baseline leg + golden fixtures) ----------- */
 /* Host-array version of uwvk_pose_log; arrays are host pointers. */
 typedef struct or_pose_run_args {

@@ -10,6 +10,11 @@
 #include "uwvk_pose_kernels.hpp"
 #include "uwvk_psp.hpp"
 #include "uwvk_host.hpp"
+#include "uwvk_aug_dev.hpp"
+
+namespace uwvk {
+hipError_t launch_pose_visual(int dof, hipStream_t st, const PoseBufs& b, const aug::VisArgs& va);
+}
 
 #include <algorithm>
 #include <cmath>
@@ -44,6 +49,7 @@ struct uwvk_pose {
   bool has_state = false, has_Q = false;
   int dense = 0;  // UWVK_OPT_DENSE_SIGMA
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  aug::VisStage vis;  // visual-landmark update staging
 };
 
 // literal (all 2n+1 sigma points) kernels requested?
@@ -213,6 +219,7 @@ void uwvk_pose_destroy(uwvk_pose* h) {
                   (void*)h->d_model, (void*)h->d_uwv, (void*)h->d_status, (void*)h->d_meas, (void*)h->d_mask,
                   (void*)h->d_accepted, (void*)h->d_scratch, (void*)h->d_shared, (void*)h->d_Qp, (void*)h->d_qband})
     if (p) (void)hipFree(p);
+  h->vis.release();
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -412,6 +419,29 @@ uwvk_status uwvk_pose_update_geographic(uwvk_pose* h, const double* mu, const do
   const double zero[3] = {0, 0, 0};
   return launch_update<MK_GEO>(h, 2, mu, cov, sc, mask, acc, nullptr, 0, gps_in_body ? gps_in_body : zero, 0);
 }
+// integrateMeasurement(vector<VisualFeatureMeasurement>, feature_positions, marker_pose,
+// cov_marker_pose, camera_config, camera_in_IMU) (PoseUKF.cpp:613-654)
+uwvk_status uwvk_pose_update_visual_landmark(uwvk_pose* h, int32_t n_features, const double* features,
+                                             const double* feature_cov, int feature_cov_per_instance,
+                                             const double* feature_positions, const double* marker_pose,
+                                             int marker_pose_per_instance, const double cov_marker_pose[36],
+                                             const double camera[4], const double camera_in_imu[7],
+                                             const uint8_t* mask) {
+  if (!h) return UWVK_EINVAL;
+  if (!h->has_state) return UWVK_ENOTINIT;
+  aug::VisArgs va{};
+  const int st = aug::stage_visual(h->stream, h->batch, n_features, features, feature_cov, feature_cov_per_instance,
+                                   feature_positions, marker_pose, marker_pose_per_instance, cov_marker_pose, camera,
+                                   camera_in_imu, mask, &va, &h->vis);
+  if (st != 0 || va.nf == 0) {
+    (void)hipStreamSynchronize(h->stream);
+    return (uwvk_status)st;
+  }
+  const hipError_t e = launch_pose_visual(h->dof, h->stream, bufs(h), va);
+  if (hipStreamSynchronize(h->stream) != hipSuccess || e != hipSuccess) return UWVK_EDEVICE;
+  return UWVK_OK;
+}
+
 uwvk_status uwvk_pose_update_delayed_xy(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
                                         const double* delayed_xy, const uint8_t* mask, uint8_t* acc) {
   if (!delayed_xy) return UWVK_EINVAL;

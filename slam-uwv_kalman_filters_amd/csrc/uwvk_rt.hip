@@ -28,7 +28,7 @@ int uwvk_device_available(int device) {
   if (hipMalloc(&d, sizeof(int)) != hipSuccess) return 0;
   hipLaunchKernelGGL(uwvk_probe_kernel, dim3(1), dim3(64), 0, 0, d);
   bool ok = hipGetLastError() == hipSuccess && hipMemcpy(&h, d, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess;
-  hipFree(d);
+  (void)hipFree(d);
   return ok && h == 0x5a5a;
 }
 

@@ -32,7 +32,13 @@ SYMBOLS = [
     "uwvk_vel_create", "uwvk_vel_destroy", "uwvk_vel_stream", "uwvk_vel_init", "uwvk_vel_setup_motion_model",
     "uwvk_vel_set_gyro", "uwvk_vel_set_efforts", "uwvk_vel_predict", "uwvk_vel_update_dvl",
     "uwvk_vel_update_pressure", "uwvk_vel_get_state", "uwvk_vel_get_model_state", "uwvk_vel_run_log",
-    "uwvk_schedule_streams", "uwvk_adcp_cell_weighting",
+    "uwvk_schedule_streams", "uwvk_adcp_cell_weighting", "uwvk_pose_update_visual_landmark",
+    "uwvk_bottom_create", "uwvk_bottom_destroy", "uwvk_bottom_stream", "uwvk_bottom_init",
+    "uwvk_bottom_set_process_noise", "uwvk_bottom_set_velocity", "uwvk_bottom_predict", "uwvk_bottom_update_range",
+    "uwvk_bottom_update_normal", "uwvk_bottom_get_state", "uwvk_bottom_get_status",
+    "uwvk_ipose_create", "uwvk_ipose_destroy", "uwvk_ipose_stream", "uwvk_ipose_init",
+    "uwvk_ipose_set_pose_reference", "uwvk_ipose_predict", "uwvk_ipose_update_visual",
+    "uwvk_ipose_get_corrected_pose", "uwvk_ipose_get_state", "uwvk_ipose_get_status",
 ]
 
 _LIB = None
@@ -191,6 +197,15 @@ class PoseUKFBatch:
         self._keep = (mu, cov, msk)
         _chk(fn(*args), "update_" + kind)
         return acc
+
+    def update_visual(self, features, feature_cov, feature_positions, marker_pose, cov_marker_pose, camera,
+                      camera_in_imu, mask=None):
+        """integrateMeasurement(vector<VisualFeatureMeasurement>, ...) (PoseUKF.cpp:613-654).
+        features [batch, nf, 2]; feature_cov [batch, nf, 2, 2] or [nf, 2, 2];
+        feature_positions [nf, 3]; marker_pose [batch, 7] or [7]; camera (fx, fy, cx, cy)."""
+        args = visual_args(self.batch, features, feature_cov, feature_positions, marker_pose, cov_marker_pose,
+                           camera, camera_in_imu, mask)
+        _chk(self.L.uwvk_pose_update_visual_landmark(self.h, *args[0]), "update_visual_landmark")
 
     def reset_with_external_pose(self, pose):
         pose = _f64(pose)
@@ -367,6 +382,24 @@ class DeviceVelLog:
         s.pressure_cov = float(log["pressure_cov"])
         self.s = s
         self.epochs = s.epochs
+
+
+def visual_args(batch, features, feature_cov, feature_positions, marker_pose, cov_marker_pose, camera, cam_in,
+                mask=None):
+    """ctypes arguments of uwvk_*_update_visual*: (args, keep-alive arrays)."""
+    f = _f64(features)
+    nf = f.shape[1] if f.ndim == 3 else 0
+    fc = _f64(np.asarray(feature_cov, np.float64).reshape(-1, nf, 4) if nf else np.zeros(4))
+    fc_pi = int(fc.shape[0] == batch and (batch > 1 or np.asarray(feature_cov).ndim == 4))
+    mp = _f64(marker_pose)
+    mp_pi = int(mp.ndim == 2)
+    fp = _f64(np.asarray(feature_positions, np.float64).reshape(-1, 3) if nf else np.zeros(3))
+    keep = [f, fc, mp, fp, _f64(cov_marker_pose), _f64(camera), _f64(cam_in)]
+    msk = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    keep.append(msk)
+    args = [C.c_int32(nf), _p(f), _p(fc), C.c_int(fc_pi), _p(fp), _p(mp), C.c_int(mp_pi), _p(keep[4]),
+            _p(keep[5]), _p(keep[6]), _p(msk)]
+    return args, keep
 
 
 def device_available(device=0):
