@@ -1,0 +1,83 @@
+// IndirectPoseUKF.hpp — C++ host facade for the batched IndirectPoseUKF
+// (uwvk_ipose_* C ABI).
+//
+// Mirrors src/IndirectPoseUKF.hpp:28-86: state {position_error,
+// orientation_error}, stored per instance as t(3) q(w,x,y,z); 6x6 covariance.
+#pragma once
+#include "PoseUKF.hpp"
+
+namespace uwv_kalman_filters_amd {
+
+class IndirectPoseUKF {
+ public:
+  // IndirectPoseUKF(position_error_std, orientation_error_std, orientation_error_tau,
+  // initial_position_error, initial_position_error_std) (IndirectPoseUKF.cpp:66-91).
+  // initial_position_error: empty (zero) or batch*3.
+  IndirectPoseUKF(int64_t batch, const std::array<double, 3>& position_error_std,
+                  const std::array<double, 3>& orientation_error_std, double orientation_error_tau,
+                  const std::vector<double>& initial_position_error = {},
+                  const std::array<double, 3>& initial_position_error_std = {{1.0, 1.0, 1.0}}, int device = 0)
+      : batch_(batch) {
+    check(uwvk_ipose_create(batch, device, &h_), "uwvk_ipose_create");
+    if (!initial_position_error.empty() && initial_position_error.size() != (size_t)batch * 3) {
+      uwvk_ipose_destroy(h_);
+      throw std::invalid_argument("IndirectPoseUKF: initial_position_error size");
+    }
+    check(uwvk_ipose_init(h_, position_error_std.data(), orientation_error_std.data(), orientation_error_tau,
+                          initial_position_error.empty() ? nullptr : initial_position_error.data(),
+                          initial_position_error_std.data()),
+          "IndirectPoseUKF");
+  }
+  IndirectPoseUKF(const IndirectPoseUKF&) = delete;
+  IndirectPoseUKF& operator=(const IndirectPoseUKF&) = delete;
+  virtual ~IndirectPoseUKF() { uwvk_ipose_destroy(h_); }
+
+  int64_t batch() const { return batch_; }
+  // updatePoseReference (IndirectPoseUKF.cpp:144-147): batch poses {t, q}
+  void updatePoseReference(const std::vector<Pose7>& pose_ref) {
+    if (pose_ref.size() != (size_t)batch_) throw std::invalid_argument("updatePoseReference: wrong size");
+    std::vector<double> p;
+    p.reserve((size_t)batch_ * 7);
+    for (const auto& x : pose_ref) {
+      p.insert(p.end(), x.t.begin(), x.t.end());
+      p.insert(p.end(), x.q.begin(), x.q.end());
+    }
+    check(uwvk_ipose_set_pose_reference(h_, p.data()), "updatePoseReference");
+  }
+  void predictionStep(double delta_t) { check(uwvk_ipose_predict(h_, delta_t), "predictionStep"); }
+  // integrateMeasurement(marker_features, feature_positions, marker_pose, cov_marker_pose,
+  // camera_config, camera_in_body) (IndirectPoseUKF.cpp:108-140)
+  void integrateMeasurement(const std::vector<VisualFeatureMeasurement>& marker_features,
+                            const std::vector<std::array<double, 3>>& feature_positions,
+                            const std::vector<Pose7>& marker_pose, const std::array<double, 36>& cov_marker_pose,
+                            const CameraConfiguration& camera_config, const Pose7& camera_in_body,
+                            const std::vector<uint8_t>& mask = {}) {
+    detail::VisualPack v(batch_, marker_features, feature_positions, marker_pose, camera_config, camera_in_body);
+    check(uwvk_ipose_update_visual(h_, v.nf, v.features.data(), v.fcov.data(), v.fcov_pi, v.fpos.data(),
+                                   v.marker.data(), v.marker_pi, cov_marker_pose.data(), v.cam, v.cam_in.data(),
+                                   mask.empty() ? nullptr : mask.data()),
+          "integrateMeasurement(VisualFeatureMeasurement)");
+  }
+  // getCorrectedPose (IndirectPoseUKF.cpp:137-142)
+  std::vector<Pose7> getCorrectedPose() {
+    std::vector<double> o((size_t)batch_ * 7);
+    check(uwvk_ipose_get_corrected_pose(h_, o.data()), "getCorrectedPose");
+    std::vector<Pose7> r((size_t)batch_);
+    for (size_t i = 0; i < r.size(); i++) {
+      for (int k = 0; k < 3; k++) r[i].t[k] = o[i * 7 + k];
+      for (int k = 0; k < 4; k++) r[i].q[k] = o[i * 7 + 3 + k];
+    }
+    return r;
+  }
+  void getState(std::vector<double>& x, std::vector<double>* P = nullptr) {
+    x.resize((size_t)batch_ * 7);
+    if (P) P->resize((size_t)batch_ * 36);
+    check(uwvk_ipose_get_state(h_, x.data(), P ? P->data() : nullptr), "getState");
+  }
+
+ private:
+  int64_t batch_;
+  uwvk_ipose* h_ = nullptr;
+};
+
+}  // namespace uwv_kalman_filters_amd

@@ -51,6 +51,66 @@ struct Velocity : BatchMeasurement<3> {};
 struct BodyEffortsMeasurement : BatchMeasurement<6> {};
 struct WaterVelocityMeasurement : BatchMeasurement<2> {};
 
+// VisualFeatureMeasurement (PoseUKF.hpp:88, IndirectPoseUKF.hpp:35): ONE feature
+// for every instance: mu batch*2 undistorted image coordinates (px), cov
+// batch*4 (px^2) or empty for shared_cov.
+struct VisualFeatureMeasurement : BatchMeasurement<2> {};
+// CameraConfiguration (PoseUKFConfig.hpp:125-131)
+struct CameraConfiguration {
+  double fx = 0, fy = 0, cx = 0, cy = 0;
+};
+// Affine3d stand-in: translation + quaternion (w, x, y, z)
+struct Pose7 {
+  std::array<double, 3> t{};
+  std::array<double, 4> q{{1.0, 0.0, 0.0, 0.0}};
+};
+
+namespace detail {
+// Packs a reference-style feature list into the C ABI's [batch][nf][...] arrays.
+struct VisualPack {
+  std::vector<double> features, fcov, fpos, marker, cam_in;
+  int fcov_pi = 0, marker_pi = 0, nf = 0;
+  double cam[4] = {0, 0, 0, 0};
+  VisualPack(int64_t batch, const std::vector<VisualFeatureMeasurement>& f,
+             const std::vector<std::array<double, 3>>& positions, const std::vector<Pose7>& marker_pose,
+             const CameraConfiguration& cc, const Pose7& cam_in_body) {
+    if (f.size() != positions.size())
+      throw std::invalid_argument("integrateMeasurement(VisualFeature): features / positions size mismatch");
+    if (marker_pose.size() != 1 && marker_pose.size() != (size_t)batch)
+      throw std::invalid_argument("integrateMeasurement(VisualFeature): marker_pose size");
+    nf = (int)f.size();
+    const size_t B = (size_t)batch;
+    fcov_pi = 0;
+    for (const auto& m : f) {
+      if (m.mu.size() != B * 2) throw std::invalid_argument("VisualFeatureMeasurement: mu size");
+      if (!m.cov.empty()) fcov_pi = 1;
+    }
+    features.assign(B * nf * 2, 0.0);
+    fcov.assign(fcov_pi ? B * nf * 4 : (size_t)nf * 4, 0.0);
+    for (int i = 0; i < nf; i++) {
+      for (size_t b = 0; b < B; b++) {
+        features[(b * nf + i) * 2] = f[i].mu[b * 2];
+        features[(b * nf + i) * 2 + 1] = f[i].mu[b * 2 + 1];
+        if (fcov_pi)
+          for (int k = 0; k < 4; k++)
+            fcov[(b * nf + i) * 4 + k] = f[i].cov.empty() ? f[i].shared_cov[k] : f[i].cov.at(b * 4 + k);
+      }
+      if (!fcov_pi)
+        for (int k = 0; k < 4; k++) fcov[(size_t)i * 4 + k] = f[i].shared_cov[k];
+      for (int k = 0; k < 3; k++) fpos.push_back(positions[i][k]);
+    }
+    marker_pi = marker_pose.size() == B && B > 1;
+    for (size_t b = 0; b < (marker_pi ? B : 1); b++) {
+      for (int k = 0; k < 3; k++) marker.push_back(marker_pose[b].t[k]);
+      for (int k = 0; k < 4; k++) marker.push_back(marker_pose[b].q[k]);
+    }
+    cam[0] = cc.fx; cam[1] = cc.fy; cam[2] = cc.cx; cam[3] = cc.cy;
+    for (int k = 0; k < 3; k++) cam_in.push_back(cam_in_body.t[k]);
+    for (int k = 0; k < 4; k++) cam_in.push_back(cam_in_body.q[k]);
+  }
+};
+}  // namespace detail
+
 using PoseUKFConfig = uwvk_pose_config;
 using UWVParameters = uwvk_uwv_params;
 using LocationConfiguration = uwvk_location;
@@ -148,6 +208,20 @@ class PoseUKF {
     check(uwvk_pose_update_delayed_xy(h_, m.mu.data(), covp(m), m.shared_cov.data(), delayed_position.data(),
                                       maskp(m), acc()),
           "integrateDelayedPositionMeasurement");
+  }
+  // integrateMeasurement(marker_features, feature_positions, marker_pose, cov_marker_pose,
+  // camera_config, camera_in_IMU) (PoseUKF.hpp:174-177, PoseUKF.cpp:613-654).
+  // marker_pose: one pose shared by the batch, or one per instance.
+  void integrateMeasurement(const std::vector<VisualFeatureMeasurement>& marker_features,
+                            const std::vector<std::array<double, 3>>& feature_positions,
+                            const std::vector<Pose7>& marker_pose, const std::array<double, 36>& cov_marker_pose,
+                            const CameraConfiguration& camera_config, const Pose7& camera_in_IMU,
+                            const std::vector<uint8_t>& mask = {}) {
+    detail::VisualPack v(batch(), marker_features, feature_positions, marker_pose, camera_config, camera_in_IMU);
+    check(uwvk_pose_update_visual_landmark(h_, v.nf, v.features.data(), v.fcov.data(), v.fcov_pi, v.fpos.data(),
+                                           v.marker.data(), v.marker_pi, cov_marker_pose.data(), v.cam,
+                                           v.cam_in.data(), mask.empty() ? nullptr : mask.data()),
+          "integrateMeasurement(VisualFeatureMeasurement)");
   }
   // resetFilterWithExternalPose (PoseUKF.hpp:187): per instance {tx,ty,tz,qw,qx,qy,qz}
   void resetFilterWithExternalPose(const std::vector<double>& imu_in_nav) {

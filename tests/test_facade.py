@@ -10,23 +10,33 @@ ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 
 
-def _build(tmp):
-    exe = os.path.join(tmp, "facade_test")
+def _build(tmp, name="facade_test"):
+    exe = os.path.join(tmp, name)
     cmd = ["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(PKG, "include"),
-           os.path.join(HERE, "cpp", "facade_test.cpp"), "-o", exe,
+           os.path.join(HERE, "cpp", name + ".cpp"), "-o", exe,
            "-L", PKG, "-luwvk", "-Wl,-rpath," + PKG,
            "-L", os.path.join(ROOT, "oracle"), "-loracle", "-Wl,-rpath," + os.path.join(ROOT, "oracle"), "-lm"]
     subprocess.run(cmd, check=True)
     return exe
 
 
-def test_facade_compiles(tmp_path):
-    _build(str(tmp_path))
+@pytest.mark.parametrize("name", ["facade_test", "facade_small_test"])
+def test_facade_compiles(tmp_path, name):
+    _build(str(tmp_path), name)
 
 
 @pytest.mark.gpu
 def test_facade_matches_oracle(tmp_path):
     exe = _build(str(tmp_path))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_facade_small_filters_match_oracle(tmp_path):
+    """BottomUKF / IndirectPoseUKF facades (incl. the visual update's feature packing)."""
+    exe = _build(str(tmp_path), "facade_small_test")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
