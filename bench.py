@@ -64,14 +64,26 @@ PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector = matrix) spec; probe measured 7
 PEAK_HBM_GBS = 8000.0
 
 
+# VelocityUKF (config C2) work per step, frozen from the kernel's code
+# (uwvk_vel.hip): one RK4 step of the Fossen model = 4 derivative evaluations
+# x ~530 flop (rotations 90, Coriolis 102, damping 186, restoring 90, M^-1 72)
+# + stage sums / normalisation ~170 = 2,290 flop; a predict integrates the 9
+# sigma points and the side model (10 RK4) plus ~900 flop of 4-DOF UKF algebra;
+# DVL (5 Hz) and pressure (10 Hz) updates add ~20 flop per step on average.
+F_VEL_RK4 = 2_290
+F_VEL_STEP = 10 * F_VEL_RK4 + 900 + 20  # 23,820
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200, help="timed epochs")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch-per-gpu", type=int, default=65536)
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="0: 65536 (C3/C4), 4096 (C2)")
     ap.add_argument("--dof", type=int, default=53)
-    ap.add_argument("--mode", default="C3", choices=["C3", "C4"])
+    ap.add_argument("--mode", default="C3", choices=["C2", "C3", "C4"],
+                    help="C3 (headline) / C4: PoseUKF; C2: VelocityUKF (secondary line)")
+    ap.add_argument("--vel-groups", type=int, default=-1, help="C2: -1 auto, 0 lane per filter, 1 16-lane rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true", help="literal kernels (all 2n+1 sigma points)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
@@ -140,7 +152,9 @@ def main():
             dist.init_process_group("gloo")
     from uwvk import engine, ensemble, synth
 
-    B = a.batch_per_gpu
+    if a.mode == "C2":
+        return bench_vel(a, engine, synth, world, rank, local, dist)
+    B = a.batch_per_gpu or 65536
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, a.mode, a.dof, first_instance=rank * B)
     f = engine.PoseUKFBatch(B, a.dof, device=local)
@@ -228,6 +242,76 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(synth, cfg, uwv, a.mode, a.dof, threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_vel(a, engine, synth, world, rank, local, dist):
+    """Config C2: VelocityUKF (VelocityUKF.cpp:79-130), batch 4096 per GPU,
+    1 kHz gyro + efforts, 5 Hz DVL, 10 Hz pressure.  One step = one epoch of
+    one instance (gyro/efforts store, predict, due updates)."""
+    B = a.batch_per_gpu or 4096
+    log = synth.make_vel_log(B, a.warmup + a.steps, first_instance=rank * B)
+    f = engine.VelocityUKFBatch(B, device=local)
+    f.set_lane_groups(a.vel_groups)
+    f.init(log["x0"], log["P0"])
+    f.set_gyro(log["gyro"][0])
+    f.setup_motion_model(synth.default_uwv())
+    d = f.upload_log(log)
+    f.run_log(d, 0, a.warmup)
+    if dist is not None:
+        dist.barrier()
+    f.synchronize()
+    t0 = time.perf_counter()
+    f.timer_start()
+    f.run_log(d, a.warmup, a.steps, sync=False)
+    kernel_ms = f.timer_stop()
+    f.synchronize()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        w = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w.item())
+    groups = a.vel_groups if a.vel_groups >= 0 else int(B <= 24576)  # uwvk_vel.hip kVelGroupsMaxBatch
+    launches = (a.steps + 4095) // 4096
+    flops = B * F_VEL_STEP * a.steps
+    tf = flops / (kernel_ms * 1e-3) / 1e12
+    kname = "k_vel_epoch_g" if groups else "k_vel_epoch"
+    out = {
+        "metric": "VelocityUKF predict+update steps/sec at batch=%d (config C2)" % B, "value": B * world * a.steps / wall,
+        "unit": "steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "C2: VelocityUKF 4-DOF, batch %d per GPU, 1 kHz gyro + efforts, 5 Hz DVL, 10 Hz depth"
+                               % B, "global_batch": B * world, "batch_per_gpu": B,
+                   "layout": "16 lanes per filter" if groups else "one filter per lane", "kernel": kname},
+        "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                     "frac": tf / PEAK_FP64_TFLOPS, "traffic": None, "kernel": kname, "launches": launches,
+                     "kernel_ms_per_launch": kernel_ms / launches, "algorithmic_flop_per_step": F_VEL_STEP},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_ctypes as O
+        # bounded sample (~10 s on 16 cores): the 2000-epoch log replayed `passes` times
+        nb, ne, passes = 64 * threads, 2000, 30
+        clog = synth.make_vel_log(nb, ne)
+        o = O.OracleVelBatch(nb)
+        o.init(clog["x0"], clog["P0"])
+        o.set_gyro(clog["gyro"][0])
+        o.setup_motion_model(synth.default_uwv())
+        c0 = time.perf_counter()
+        for _ in range(passes):
+            o.run_log(clog, nthreads=threads)
+        cdt = time.perf_counter() - c0
+        out["cpu_baseline"] = {"value": nb * ne * passes / cdt, "unit": "steps/s", "cores": threads, "kind": "port",
+                               "sample": "%d VelocityUKF instances x %d epochs x %d passes (C2), %d pthreads, %.2f s wall"
+                                         % (nb, ne, passes, threads, cdt)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -443,7 +443,19 @@ typedef struct uwvk_vel_log {
   const double* pressure;   /* [n_pressure][batch] (z position) */
   double pressure_cov;
 } uwvk_vel_log;
+/* Runs epochs [first, first + count): one launch per 4096 epochs, state in
+ * registers across the launch.  Asynchronous on the handle's stream (the
+ * getters and uwvk_vel_synchronize wait). */
 uwvk_status uwvk_vel_run_log(uwvk_vel* h, const uwvk_vel_log* log, int64_t first, int64_t count);
+/* UWVK_VEL_OPT_LANE_GROUPS: -1 (default) auto by batch size, 0 one filter per
+ * lane (9 sigma points in one lane's registers), 1 one filter per 16-lane DPP
+ * row (one sigma point per lane; fills the chip at small batches, e.g. C2's 4096). */
+#define UWVK_VEL_OPT_LANE_GROUPS 1
+uwvk_status uwvk_vel_set_option(uwvk_vel* h, int option, int value);
+uwvk_status uwvk_vel_synchronize(uwvk_vel* h);
+/* HIP events on the handle's stream around queued work (bench timing) */
+uwvk_status uwvk_vel_timer_start(uwvk_vel* h);
+uwvk_status uwvk_vel_timer_stop(uwvk_vel* h, float* elapsed_ms);
 
 /* ======================================================================== */
 /* BottomUKF (src/BottomUKF.hpp:26-53, BottomUKF.cpp:1-71)                  */

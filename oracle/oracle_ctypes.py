@@ -59,6 +59,13 @@ class RunArgs(C.Structure):
                 ("efforts_index", P), ("efforts", P), ("efforts_cov", C.c_double * 36)]
 
 
+class VelRunArgs(C.Structure):
+    P = C.c_void_p
+    _fields_ = [("batch", C.c_int64), ("epochs", C.c_int64), ("dt", C.c_double), ("flags", P), ("gyro", P),
+                ("efforts", P), ("dvl_index", P), ("dvl", P), ("dvl_cov", C.c_double * 9), ("pressure_index", P),
+                ("pressure", P), ("pressure_cov", C.c_double)]
+
+
 class OraclePoseBatch:
     """`batch` independent oracle PoseUKF instances in one contiguous buffer."""
 
@@ -246,9 +253,36 @@ class OracleVelBatch:
                                     ms[i].ctypes.data_as(DP))
         return (x, P, ms) if model else (x, P)
 
-    def run_log(self, log, first=0, count=None):
+    def run_log(self, log, first=0, count=None, nthreads=1):
+        """Native driver loop (or_vel_run_log): gyro, efforts, predict, DVL, pressure per epoch."""
         count = log["epochs"] - first if count is None else count
-        B = self.batch
+        a = VelRunArgs()
+        a.batch, a.epochs, a.dt = self.batch, log["epochs"], log["dt"]
+        keep = {}
+
+        def put(name, arr, dtype):
+            arr = np.ascontiguousarray(arr, dtype=dtype)
+            keep[name] = arr
+            return arr.ctypes.data
+
+        a.flags = put("flags", log["flags"], np.uint32)
+        a.gyro = put("gyro", log["gyro"], np.float64)
+        a.efforts = put("efforts", log["efforts"], np.float64)
+        a.dvl_index = put("dvl_index", log["dvl_index"], np.int32)
+        a.dvl = put("dvl", log["dvl"] if log["dvl"].size else np.zeros(3), np.float64)
+        abi.fill(a.dvl_cov, np.asarray(log["dvl_cov"]).ravel())
+        a.pressure_index = put("pressure_index", log["pressure_index"], np.int32)
+        a.pressure = put("pressure", log["pressure"] if log["pressure"].size else np.zeros(1), np.float64)
+        a.pressure_cov = float(log["pressure_cov"])
+        e = self.L.or_vel_run_log(C.cast(C.addressof(self.buf), C.c_void_p), C.byref(a), C.c_int64(first),
+                                  C.c_int64(count), C.c_int(nthreads))
+        if e:
+            raise RuntimeError("oracle vel run_log: %s" % abi.STATUS.get(e, e))
+        return self.batch
+
+    def run_log_steps(self, log, first=0, count=None):
+        """The same loop through the per-call API (cross-check of run_log)."""
+        count = log["epochs"] - first if count is None else count
         for e in range(first, first + count):
             self.set_gyro(log["gyro"][e])
             self.set_efforts(log["efforts"][e])
@@ -258,7 +292,7 @@ class OracleVelBatch:
                 self.update_dvl(log["dvl"][log["dvl_index"][e]], log["dvl_cov"])
             if f & abi.EV_PRESSURE:
                 self.update_pressure(log["pressure"][log["pressure_index"][e]], log["pressure_cov"])
-        return B
+        return self.batch
 
 
 # ---- BottomUKF / IndirectPoseUKF / visual landmarks (uwvk_small_oracle.c) ----

@@ -1134,6 +1134,61 @@ int or_pose_run_log(or_pose* filters, const or_pose_run_args* a, int64_t first, 
   return err;
 }
 
+typedef struct vel_job {
+  or_vel* filters;
+  const or_vel_run_args* a;
+  int64_t first, count, i0, i1;
+  int err;
+} vel_job;
+
+/* the epoch order of the reference's users (VelocityUKF.cpp:79-130) */
+static void* vel_worker(void* p) {
+  vel_job* j = (vel_job*)p;
+  const or_vel_run_args* a = j->a;
+  const int64_t B = a->batch;
+  for (int64_t i = j->i0; i < j->i1 && !j->err; i++) {
+    or_vel* f = &j->filters[i];
+    for (int64_t e = j->first; e < j->first + j->count; e++) {
+      int r = or_vel_set_gyro(f, a->gyro + (e * B + i) * 3, NULL);
+      if (!r) r = or_vel_set_efforts(f, a->efforts + (e * B + i) * 6, NULL);
+      if (!r) r = or_vel_predict(f, a->dt);
+      if (!r && (a->flags[e] & UWVK_EV_DVL))
+        r = or_vel_update_dvl(f, a->dvl + ((int64_t)a->dvl_index[e] * B + i) * 3, a->dvl_cov);
+      if (!r && (a->flags[e] & UWVK_EV_PRESSURE)) {
+        const double pc[1] = {a->pressure_cov};
+        r = or_vel_update_pressure(f, a->pressure + (int64_t)a->pressure_index[e] * B + i, pc);
+      }
+      if (r) {
+        j->err = r;
+        break;
+      }
+    }
+  }
+  return NULL;
+}
+
+int or_vel_run_log(or_vel* filters, const or_vel_run_args* a, int64_t first, int64_t count, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > a->batch) nthreads = (int)a->batch;
+  vel_job* jobs = (vel_job*)calloc((size_t)nthreads, sizeof(vel_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t].filters = filters; jobs[t].a = a; jobs[t].first = first; jobs[t].count = count;
+    jobs[t].i0 = a->batch * t / nthreads;
+    jobs[t].i1 = a->batch * (t + 1) / nthreads;
+    if (nthreads == 1) vel_worker(&jobs[t]);
+    else pthread_create(&th[t], NULL, vel_worker, &jobs[t]);
+  }
+  int err = 0;
+  for (int t = 0; t < nthreads; t++) {
+    if (nthreads > 1) pthread_join(th[t], NULL);
+    if (jobs[t].err && !err) err = jobs[t].err;
+  }
+  free(jobs);
+  free(th);
+  return err;
+}
+
 size_t or_pose_sizeof(void) { return sizeof(or_pose); }
 size_t or_vel_sizeof(void) { return sizeof(or_vel); }
 

@@ -192,6 +192,23 @@ typedef struct or_pose_run_args {
 int or_pose_run_log(or_pose* filters, const or_pose_run_args* a, int64_t first, int64_t count, int nthreads,
                     uint32_t* accept_counts);
 size_t or_pose_sizeof(void);
+/* VelocityUKF log (config C2), host arrays; layout as uwvk_vel_log */
+typedef struct or_vel_run_args {
+  int64_t batch, epochs;
+  double dt;
+  const uint32_t* flags;
+  const double* gyro;    /* [epochs][batch][3] */
+  const double* efforts; /* [epochs][batch][6] */
+  const int32_t* dvl_index;
+  const double* dvl;
+  double dvl_cov[9];
+  const int32_t* pressure_index;
+  const double* pressure;
+  double pressure_cov;
+} or_vel_run_args;
+/* VelocityUKF driver loop per epoch (gyro, efforts, predict, DVL, pressure),
+ * instances split over nthreads pthreads.  Returns 0 or the first error. */
+int or_vel_run_log(or_vel* filters, const or_vel_run_args* a, int64_t first, int64_t count, int nthreads);
 void or_pose_get_state(const or_pose* f, double* x, double* P);
 void or_vel_get_state(const or_vel* f, double* x, double* P, double* model_state);
 size_t or_vel_sizeof(void);

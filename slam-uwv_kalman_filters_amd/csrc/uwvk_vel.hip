@@ -5,6 +5,7 @@
 // VGPRs; the kernel is bound by the fp64 model evaluation (9 x RK4 per predict).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -430,6 +431,255 @@ __global__ __launch_bounds__(64) void k_vel_epoch(VelBufs b, VelShared P, VelEpo
   v_store(b, i, mu, S);
 }
 
+// ---------------------------------------------------------------------------
+// Lane-group epoch kernel: 16 lanes (one DPP row) per filter, ONE SIGMA POINT
+// PER LANE (lanes 0..8), lane 9 advances the side motion model
+// (motion_model->sendEffort, VelocityUKF.cpp:126-127) in the same RK4 pass.
+// mu / Sigma are replicated in every lane of the row and kept bitwise
+// identical: the cross-point sums are butterfly reductions inside the row
+// (quad_perm / half-mirror / mirror DPP), whose result is the same in every
+// lane.  4 filters per wave: batch 4096 fills 1024 waves, one per SIMD,
+// where the lane-per-filter kernel occupies 64.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+UWVK_DEV double vdpp(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+// sum over the 16 lanes of this lane's DPP row, identical in every lane
+UWVK_DEV double row_sum16(double v) {
+  v = v + vdpp<0xb1>(v);   // quad_perm [1,0,3,2]
+  v = v + vdpp<0x4e>(v);   // quad_perm [2,3,0,1]
+  v = v + vdpp<0x141>(v);  // row_half_mirror
+  v = v + vdpp<0x140>(v);  // row_mirror
+  return v;
+}
+// value of row lane src (0..15) in every lane of the row
+UWVK_DEV double row_bcast(double v, int src) {
+  const int ba = (((int)threadIdx.x & ~15) + src) * 4;
+  const int lo = __builtin_amdgcn_ds_bpermute(ba, __double2loint(v));
+  const int hi = __builtin_amdgcn_ds_bpermute(ba, __double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+// sigma point g of (mu, L) [EXT ukfom]: 0 = mu, 2j+1 = mu + L_j, 2j+2 = mu - L_j
+UWVK_DEV void vg_point(const double mu[4], const double L[16], int g, double x[4]) {
+  const int j = g >= 1 && g < 9 ? (g - 1) >> 1 : 0;
+  const double sg = (g >= 1 && g < 9) ? ((g & 1) ? 1.0 : -1.0) : 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    double c = L[k * 4];
+#pragma unroll
+    for (int jj = 1; jj < 4; jj++) c = (j == jj) ? L[k * 4 + jj] : c;
+    x[k] = sg == 0.0 ? mu[k] : mu[k] + sg * c;
+  }
+}
+
+// iterative vect mean over the 9 point lanes (ref = X_0, |delta| <= 1e-6)
+template <int M>
+UWVK_DEV void vg_mean(const double x[M], bool pt, double ref[M]) {
+#pragma unroll
+  for (int k = 0; k < M; k++) ref[k] = row_bcast(x[k], 0);
+  int it = 0;
+  double nrm;
+  do {
+    double d[M];
+    nrm = 0.0;
+#pragma unroll
+    for (int k = 0; k < M; k++) {
+      d[k] = row_sum16(pt ? x[k] - ref[k] : 0.0) / 9.0;
+      nrm += d[k] * d[k];
+    }
+#pragma unroll
+    for (int k = 0; k < M; k++) ref[k] = ref[k] + 1.0 * d[k];
+    nrm = sqrt(nrm);
+  } while (nrm > 1e-6 && ++it < 10000);
+}
+
+// Sigma = 1/2 sum_p d_p d_p^T over the point lanes (+ add)
+UWVK_DEV void vg_cov(const double x[4], const double mean[4], bool pt, double S[16]) {
+  double d[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) d[k] = pt ? x[k] - mean[k] : 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j <= i; j++) {
+      const double s = 0.5 * row_sum16(d[i] * d[j]);
+      S[i * 4 + j] = s;
+      S[j * 4 + i] = s;
+    }
+}
+
+// update with h = x[OFF..OFF+M) (VelocityUKF.cpp:100-124), accept any
+template <int M, int OFF>
+UWVK_DEV bool vg_update(double mu[4], double S[16], const double z[M], const double R[M * M], int g) {
+  const bool pt = g < 9;
+  double L[16], x[4];
+  bool ok = v_chol(S, L);
+  vg_point(mu, L, g, x);
+  double zp[M], zm[M];
+#pragma unroll
+  for (int a = 0; a < M; a++) zp[a] = x[OFF + a];
+  vg_mean<M>(zp, pt, zm);
+  double dz[M], dx[4];
+#pragma unroll
+  for (int a = 0; a < M; a++) dz[a] = pt ? zp[a] - zm[a] : 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) dx[k] = pt ? x[k] - mu[k] : 0.0;
+  double Sz[M * M], C[4 * M], Si[M * M], K[4 * M], nu[M];
+#pragma unroll
+  for (int a = 0; a < M; a++)
+#pragma unroll
+    for (int b = 0; b <= a; b++) {
+      const double s = row_sum16(dz[a] * dz[b]);
+      Sz[a * M + b] = 0.5 * s + R[a * M + b];
+      Sz[b * M + a] = 0.5 * s + R[b * M + a];
+    }
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int a = 0; a < M; a++) C[i * M + a] = 0.5 * row_sum16(dx[i] * dz[a]);
+  if constexpr (M == 1) {
+    Si[0] = 1.0 / Sz[0];
+  } else {
+    const double* A = Sz;
+    const double c00 = A[4] * A[8] - A[5] * A[7];
+    const double c01 = A[5] * A[6] - A[3] * A[8];
+    const double c02 = A[3] * A[7] - A[4] * A[6];
+    const double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+    const double id = 1.0 / det;
+    Si[0] = c00 * id;
+    Si[1] = (A[2] * A[7] - A[1] * A[8]) * id;
+    Si[2] = (A[1] * A[5] - A[2] * A[4]) * id;
+    Si[3] = c01 * id;
+    Si[4] = (A[0] * A[8] - A[2] * A[6]) * id;
+    Si[5] = (A[2] * A[3] - A[0] * A[5]) * id;
+    Si[6] = c02 * id;
+    Si[7] = (A[1] * A[6] - A[0] * A[7]) * id;
+    Si[8] = (A[0] * A[4] - A[1] * A[3]) * id;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int a = 0; a < M; a++) {
+      double s = 0.0;
+#pragma unroll
+      for (int b = 0; b < M; b++) s += C[i * M + b] * Si[b * M + a];
+      K[i * M + a] = s;
+    }
+#pragma unroll
+  for (int a = 0; a < M; a++) nu[a] = z[a] - zm[a];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      double s = 0.0;
+#pragma unroll
+      for (int a = 0; a < M; a++) s += C[i * M + a] * K[j * M + a];
+      S[i * 4 + j] -= s;
+    }
+  double delta[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    double s = 0.0;
+#pragma unroll
+    for (int a = 0; a < M; a++) s += K[i * M + a] * nu[a];
+    delta[i] = s;
+  }
+  // apply_delta: re-spread about mu, shift every point and mu by delta
+  ok = v_chol(S, L) && ok;
+  vg_point(mu, L, g, x);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    mu[k] = mu[k] + 1.0 * delta[k];
+    x[k] = x[k] + 1.0 * delta[k];
+  }
+  vg_cov(x, mu, pt, S);
+  return ok;
+}
+
+constexpr int VG = 16;  // lanes per filter
+
+__global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P, VelEpochArgs ea) {
+  const int g = (int)threadIdx.x & (VG - 1);
+  const int64_t B = b.batch, inst = (int64_t)blockIdx.x * (64 / VG) + (int)threadIdx.x / VG;
+  const bool live = inst < B;
+  const int64_t i = live ? inst : B - 1;  // dead groups compute on a copy and store nothing
+  const bool pt = g < 9, side = g == 9;
+  double mu[4], S[16], m[13], w[3], tau[6];
+  v_load(b, i, mu, S);
+#pragma unroll
+  for (int k = 0; k < 13; k++) m[k] = b.model[i * 13 + k];
+  double q[4] = {m[3], m[4], m[5], m[6]};
+  bool ok = true;
+  for (int64_t e = ea.first; e < ea.first + ea.count; e++) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) { w[k] = ea.gyro[(e * B + i) * 3 + k]; m[10 + k] = w[k]; }
+#pragma unroll
+    for (int k = 0; k < 6; k++) tau[k] = ea.efforts[(e * B + i) * 6 + k];
+    // predict (VelocityUKF.cpp:115-128): point lanes integrate their sigma
+    // point, lane 9 the side model, in one RK4 pass
+    double L[16], x[4];
+    ok = v_chol(S, L) && ok;
+    vg_point(mu, L, g, x);
+    double s13[13], n13[13];
+#pragma unroll
+    for (int k = 0; k < 13; k++) s13[k] = m[k];
+    if (!side) {
+      s13[0] = s13[1] = s13[2] = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) s13[3 + k] = q[k];
+#pragma unroll
+      for (int k = 0; k < 3; k++) s13[7 + k] = x[k];
+    }
+    v_rk4(P, tau, ea.dt, s13, n13);
+    {  // processMotionModel tail (VelocityUKF.cpp:22-32)
+      double t[3], r[3];
+#pragma unroll
+      for (int k = 0; k < 3; k++) t[k] = x[k] + (n13[7 + k] - x[k]);
+      qrot(q, t, r);
+      x[3] = x[3] + ea.dt * r[2];
+      x[0] = t[0]; x[1] = t[1]; x[2] = t[2];
+    }
+    vg_mean<4>(x, pt, mu);
+    vg_cov(x, mu, pt, S);
+#pragma unroll
+    for (int k = 0; k < 16; k++) S[k] += ea.dt * P.Q0[k];
+    if (side) {
+#pragma unroll
+      for (int k = 0; k < 13; k++) m[k] = n13[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) q[k] = row_bcast(side ? m[3 + k] : 0.0, 9);
+    const uint32_t fl = ea.flags[e];
+    if (fl & UWVK_EV_DVL) {
+      const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + i) * 3;
+      const double zz[3] = {z[0], z[1], z[2]};
+      ok = vg_update<3, 0>(mu, S, zz, ea.dvl_cov, g) && ok;
+    }
+    if (fl & UWVK_EV_PRESSURE) {
+      const double zz[1] = {ea.pressure[(int64_t)ea.p_index[e] * B + i]};
+      const double R[1] = {ea.p_cov};
+      ok = vg_update<1, 3>(mu, S, zz, R, g) && ok;
+    }
+  }
+  if (!live) return;
+  if (side) {
+    if (ea.count > 0) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) b.gyro[i * 3 + k] = w[k];
+#pragma unroll
+      for (int k = 0; k < 6; k++) b.efforts[i * 6 + k] = tau[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 13; k++) b.model[i * 13 + k] = m[k];
+    if (!ok) b.status[i] |= UWVK_ST_NOTPD;
+    v_store(b, i, mu, S);
+  }
+}
+
 __global__ void k_vel_setup(VelBufs b) {  // setupMotionModel pose (VelocityUKF.cpp:65-74)
   const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= b.batch) return;
@@ -457,7 +707,14 @@ struct uwvk_vel {
   uint32_t* d_status = nullptr;
   VelShared P{};
   bool has_state = false, has_model = false;
+  int groups = -1;  // UWVK_VEL_OPT_LANE_GROUPS: -1 auto, 0 lane per filter, 1 16 lanes per filter
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
+// auto: lane groups below the measured crossover (C2 on MI355X: the lane-per-
+// filter kernel's epoch latency is flat at ~38-40 us up to batch 65536, one
+// wave per SIMD; the lane-group kernel takes 7.4 us at 4096 and ~1.74 ns per
+// instance once the chip is full, 114 us at 65536)
+static constexpr int64_t kVelGroupsMaxBatch = 24576;
 
 static VelBufs vbufs(const uwvk_vel* h) {
   VelBufs b;
@@ -521,8 +778,38 @@ void uwvk_vel_destroy(uwvk_vel* h) {
   for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_gyro, (void*)h->d_eff, (void*)h->d_model,
                   (void*)h->d_meas, (void*)h->d_mask, (void*)h->d_status})
     if (p) (void)hipFree(p);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
+}
+
+uwvk_status uwvk_vel_set_option(uwvk_vel* h, int option, int value) {
+  if (!h) return UWVK_EINVAL;
+  if (option != UWVK_VEL_OPT_LANE_GROUPS || value < -1 || value > 1) return UWVK_EINVAL;
+  h->groups = value;
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_vel_synchronize(uwvk_vel* h) {
+  if (!h) return UWVK_EINVAL;
+  return hipStreamSynchronize(h->stream) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
+}
+
+uwvk_status uwvk_vel_timer_start(uwvk_vel* h) {
+  if (!h) return UWVK_EINVAL;
+  if (!h->ev0 && hipEventCreate(&h->ev0) != hipSuccess) return UWVK_EDEVICE;
+  if (!h->ev1 && hipEventCreate(&h->ev1) != hipSuccess) return UWVK_EDEVICE;
+  HIPCHK(hipEventRecord(h->ev0, h->stream));
+  return UWVK_OK;
+}
+
+uwvk_status uwvk_vel_timer_stop(uwvk_vel* h, float* ms) {
+  if (!h || !ms || !h->ev0 || !h->ev1) return UWVK_EINVAL;
+  HIPCHK(hipEventRecord(h->ev1, h->stream));
+  HIPCHK(hipEventSynchronize(h->ev1));
+  HIPCHK(hipEventElapsedTime(ms, h->ev0, h->ev1));
+  return UWVK_OK;
 }
 
 void* uwvk_vel_stream(const uwvk_vel* h) { return h ? (void*)h->stream : nullptr; }
@@ -653,10 +940,17 @@ uwvk_status uwvk_vel_run_log(uwvk_vel* h, const uwvk_vel_log* log, int64_t first
   std::memcpy(ea.dvl_cov, log->dvl_cov, sizeof(ea.dvl_cov));
   ea.p_index = log->pressure_index; ea.pressure = log->pressure; ea.p_cov = log->pressure_cov;
   ea.dt = log->dt;
-  for (int64_t e = first; e < first + count; e++) {
+  // one launch per chunk of epochs (state stays in registers across the chunk)
+  const bool groups = h->groups > 0 || (h->groups < 0 && h->batch <= kVelGroupsMaxBatch);
+  constexpr int64_t kChunk = 4096;
+  for (int64_t e = first; e < first + count; e += kChunk) {
     ea.first = e;
-    ea.count = 1;
-    hipLaunchKernelGGL(k_vel_epoch, dim3(vgrid(h->batch)), dim3(64), 0, h->stream, vbufs(h), h->P, ea);
+    ea.count = std::min<int64_t>(kChunk, first + count - e);
+    if (groups)
+      hipLaunchKernelGGL(k_vel_epoch_g, dim3((unsigned)((h->batch + 3) / 4)), dim3(64), 0, h->stream, vbufs(h), h->P,
+                         ea);
+    else
+      hipLaunchKernelGGL(k_vel_epoch, dim3(vgrid(h->batch)), dim3(64), 0, h->stream, vbufs(h), h->P, ea);
     HIPCHK(hipGetLastError());
   }
   return UWVK_OK;

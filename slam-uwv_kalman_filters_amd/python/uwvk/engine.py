@@ -32,6 +32,7 @@ SYMBOLS = [
     "uwvk_vel_create", "uwvk_vel_destroy", "uwvk_vel_stream", "uwvk_vel_init", "uwvk_vel_setup_motion_model",
     "uwvk_vel_set_gyro", "uwvk_vel_set_efforts", "uwvk_vel_predict", "uwvk_vel_update_dvl",
     "uwvk_vel_update_pressure", "uwvk_vel_get_state", "uwvk_vel_get_model_state", "uwvk_vel_run_log",
+    "uwvk_vel_set_option", "uwvk_vel_synchronize", "uwvk_vel_timer_start", "uwvk_vel_timer_stop",
     "uwvk_schedule_streams", "uwvk_adcp_cell_weighting", "uwvk_pose_update_visual_landmark",
     "uwvk_bottom_create", "uwvk_bottom_destroy", "uwvk_bottom_stream", "uwvk_bottom_init",
     "uwvk_bottom_set_process_noise", "uwvk_bottom_set_velocity", "uwvk_bottom_predict", "uwvk_bottom_update_range",
@@ -354,10 +355,26 @@ class VelocityUKFBatch:
     def upload_log(self, log):
         return DeviceVelLog(log, self.device)
 
-    def run_log(self, dlog, first=0, count=None):
+    def run_log(self, dlog, first=0, count=None, sync=True):
         count = dlog.epochs - first if count is None else count
         _chk(self.L.uwvk_vel_run_log(self.h, C.byref(dlog.s), C.c_int64(first), C.c_int64(count)), "vel_run_log")
-        self.get_state()  # synchronises the handle's stream
+        if sync:
+            self.synchronize()
+
+    def set_lane_groups(self, value):
+        """-1 auto, 0 one filter per lane, 1 one filter per 16 lanes (UWVK_VEL_OPT_LANE_GROUPS)."""
+        _chk(self.L.uwvk_vel_set_option(self.h, 1, int(value)), "vel_set_option")
+
+    def synchronize(self):
+        _chk(self.L.uwvk_vel_synchronize(self.h), "vel_synchronize")
+
+    def timer_start(self):
+        _chk(self.L.uwvk_vel_timer_start(self.h), "vel_timer_start")
+
+    def timer_stop(self):
+        ms = C.c_float(0)
+        _chk(self.L.uwvk_vel_timer_stop(self.h, C.byref(ms)), "vel_timer_stop")
+        return ms.value
 
 
 class DeviceVelLog:

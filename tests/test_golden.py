@@ -103,12 +103,14 @@ def test_engine_reproduces_fixture(path, engine_path):
 
 
 @pytest.mark.gpu
-def test_engine_reproduces_vel_fixture():
+@pytest.mark.parametrize("groups", [0, 1])
+def test_engine_reproduces_vel_fixture(groups):
     from uwvk import engine
     g = np.load(os.path.join(HERE, "golden", "vel_c2.npz"), allow_pickle=False)
     log = {k: g[k] for k in g.files}
     log["epochs"], log["dt"] = int(g["epochs"]), float(g["dt"])
     f = engine.VelocityUKFBatch(g["x0"].shape[0])
+    f.set_lane_groups(groups)
     f.init(g["x0"], g["P0"])
     f.set_gyro(g["gyro"][0])
     f.setup_motion_model(synth.default_uwv())
@@ -120,3 +122,18 @@ def test_engine_reproduces_vel_fixture():
         assert np.max(np.abs(x - g["mu"][k]) / sd) < TOL_GPU
         assert cov_err(P, g["cov"][k]).max() < TOL_GPU
         assert np.max(np.abs(m - g["model"][k])) < 1e-9
+
+
+def test_oracle_vel_runner_matches_step_api():
+    """or_vel_run_log (threaded native loop, the C2 cpu_baseline) == the per-call API loop, bitwise."""
+    log = synth.make_vel_log(6, 450)
+    uwv = synth.default_uwv()
+    a, b = O.OracleVelBatch(6), O.OracleVelBatch(6)
+    for f in (a, b):
+        f.init(log["x0"], log["P0"])
+        f.set_gyro(log["gyro"][0])
+        f.setup_motion_model(uwv)
+    a.run_log(log, nthreads=3)
+    b.run_log_steps(log)
+    for u, v in zip(a.get_state(model=True), b.get_state(model=True)):
+        np.testing.assert_array_equal(u, v)

@@ -131,13 +131,16 @@ def test_run_log(eng, orc, dof, mode, epochs, path):
     _check(o, g, dof, TOL_LOG)
 
 
-def test_velocity_ukf(eng, orc):
+@pytest.mark.parametrize("groups,B", [(0, 16), (1, 16), (1, 13), (-1, 70)])
+def test_velocity_ukf(eng, orc, groups, B):
+    """run_log on both kernel layouts: one filter per lane (0) and one per
+    16-lane row (1, incl. a batch that leaves a partial wave); -1 = auto."""
     from uwvk import synth
-    B = 16
     log = synth.make_vel_log(B, 600)
     uwv = synth.default_uwv()
     o = orc.OracleVelBatch(B)
     g = eng.VelocityUKFBatch(B)
+    g.set_lane_groups(groups)
     for f in (o, g):
         f.init(log["x0"], log["P0"])
         f.set_gyro(log["gyro"][0])
