@@ -337,6 +337,21 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
  * truth: host store-vector (nullable -> zeros).  out: host doubles, 3*store+1. */
 uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* out);
 
+/* Multi-GPU ensembles: one process (or thread) per GPU owns a
+ * contiguous instance range; the only collective is this statistics sum over
+ * RCCL.  `comm` is an RCCL communicator (ncclComm_t) as void*, from
+ * uwvk_comm_init or the caller's own RCCL setup; NULL = this handle only (same
+ * as uwvk_pose_ensemble_stats).  The sum runs on the handle's stream. */
+uwvk_status uwvk_pose_ensemble_allreduce(uwvk_pose* h, const double* truth, double* out, void* comm);
+/* RCCL communicator helpers (no RCCL headers needed by the caller): rank 0
+ * calls uwvk_comm_unique_id and ships the uwvk_comm_unique_id_bytes() bytes to
+ * the other ranks out of band; every rank then calls uwvk_comm_init. */
+int uwvk_comm_unique_id_bytes(void);
+uwvk_status uwvk_comm_unique_id(char* id);
+uwvk_status uwvk_comm_init(int nranks, const char* id, int rank, int device, void** comm);
+void uwvk_comm_destroy(void* comm);
+uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n, void* stream);
+
 /* Engine options (not part of the reference surface).
  * UWVK_OPT_LITERAL_APPLY_DELTA: 0 (default) applies ukfom's apply_delta through
  *   its exact nav-frame identity mu <- mu [+] d, Sigma <- T Sigma T^T

@@ -549,6 +549,10 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
 }
 
 uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* out) {
+  return uwvk_pose_ensemble_allreduce(h, truth, out, nullptr);
+}
+
+uwvk_status uwvk_pose_ensemble_allreduce(uwvk_pose* h, const double* truth, double* out, void* comm) {
   if (!h || !out) return UWVK_EINVAL;
   const int s = h->store;
   const int nout = 3 * s + 1;
@@ -563,6 +567,10 @@ uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* 
   const unsigned nb = (unsigned)((h->batch + 63) / 64);
   (void)nb;
   HIPCHK(launch_pose_stats(h->dof, h->stream, b, d_truth, d_out));
+  if (comm) {  // RCCL sum across the ranks' shards, stream-ordered after the stats kernel
+    const uwvk_status st = uwvk_comm_allreduce_sum_device(comm, d_out, nout, (void*)h->stream);
+    if (st != UWVK_OK) return st;
+  }
   HIPCHK(hipMemcpyAsync(out, d_out, nout * 8, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return UWVK_OK;

@@ -240,6 +240,13 @@ class PoseUKF {
     if (P) P->resize((size_t)batch() * dof() * dof());
     check(uwvk_pose_get_state(h_, x.data(), P ? P->data() : nullptr), "getState");
   }
+  // Ensemble statistics (layout: uwvk_pose_ensemble_stats); with an RCCL
+  // communicator (uwvk_comm_init, void* ncclComm_t) summed over all ranks.
+  std::vector<double> ensembleStats(const double* truth = nullptr, void* comm = nullptr) {
+    std::vector<double> out(3 * store() + 1);
+    check(uwvk_pose_ensemble_allreduce(h_, truth, out.data(), comm), "ensembleStats");
+    return out;
+  }
   // Gate decisions of the last update (1 = accepted), one byte per instance.
   const std::vector<uint8_t>& lastAccepted() const { return accepted_; }
   std::vector<uint32_t> status(bool clear = false) {

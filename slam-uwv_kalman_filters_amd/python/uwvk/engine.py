@@ -33,6 +33,8 @@ SYMBOLS = [
     "uwvk_vel_set_gyro", "uwvk_vel_set_efforts", "uwvk_vel_predict", "uwvk_vel_update_dvl",
     "uwvk_vel_update_pressure", "uwvk_vel_get_state", "uwvk_vel_get_model_state", "uwvk_vel_run_log",
     "uwvk_vel_set_option", "uwvk_vel_synchronize", "uwvk_vel_timer_start", "uwvk_vel_timer_stop",
+    "uwvk_pose_ensemble_allreduce", "uwvk_comm_unique_id_bytes", "uwvk_comm_unique_id", "uwvk_comm_init",
+    "uwvk_comm_destroy", "uwvk_comm_allreduce_sum_device",
     "uwvk_schedule_streams", "uwvk_adcp_cell_weighting", "uwvk_pose_update_visual_landmark",
     "uwvk_bottom_create", "uwvk_bottom_destroy", "uwvk_bottom_stream", "uwvk_bottom_init",
     "uwvk_bottom_set_process_noise", "uwvk_bottom_set_velocity", "uwvk_bottom_predict", "uwvk_bottom_update_range",
@@ -66,6 +68,7 @@ def lib(path=None):
         L.uwvk_vel_stream.argtypes = [VP]
         L.uwvk_pose_destroy.argtypes = [VP]
         L.uwvk_vel_destroy.argtypes = [VP]
+        L.uwvk_comm_destroy.argtypes = [VP]
         L.uwvk_device_free.argtypes = [VP]
         L.uwvk_memcpy_h2d.argtypes = [VP, VP, C.c_size_t]
         L.uwvk_memcpy_d2h.argtypes = [VP, VP, C.c_size_t]
@@ -243,10 +246,15 @@ class PoseUKFBatch:
         if sync:
             self.synchronize()
 
-    def ensemble_stats(self, truth=None):
+    def ensemble_stats(self, truth=None, comm=None):
+        """Ensemble statistics of this handle's instances; with an RcclComm,
+        summed over every rank's shard by RCCL (uwvk_pose_ensemble_allreduce)."""
         out = np.zeros(3 * self.lay["store"] + 1)
         t = _f64(truth)
-        _chk(self.L.uwvk_pose_ensemble_stats(self.h, _p(t), _p(out)), "ensemble_stats")
+        if comm is None:
+            _chk(self.L.uwvk_pose_ensemble_stats(self.h, _p(t), _p(out)), "ensemble_stats")
+        else:
+            _chk(self.L.uwvk_pose_ensemble_allreduce(self.h, _p(t), _p(out), comm.ptr), "ensemble_allreduce")
         return out
 
     def timer_start(self):
@@ -399,6 +407,35 @@ class DeviceVelLog:
         s.pressure_cov = float(log["pressure_cov"])
         self.s = s
         self.epochs = s.epochs
+
+
+class RcclComm:
+    """An RCCL communicator made through the C ABI (uwvk_comm_*).  Rank 0 makes
+    the id (RcclComm.unique_id()) and ships it to the other ranks out of band."""
+
+    @staticmethod
+    def unique_id():
+        L = lib()
+        n = L.uwvk_comm_unique_id_bytes()
+        buf = C.create_string_buffer(n)
+        _chk(L.uwvk_comm_unique_id(buf), "comm_unique_id")
+        return buf.raw
+
+    def __init__(self, nranks, uid, rank, device=0):
+        self.L = lib()
+        self.ptr = VP()
+        _chk(self.L.uwvk_comm_init(nranks, C.c_char_p(uid), rank, device, C.byref(self.ptr)), "comm_init")
+
+    def close(self):
+        if self.ptr:
+            self.L.uwvk_comm_destroy(self.ptr)
+            self.ptr = VP()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def visual_args(batch, features, feature_cov, feature_positions, marker_pose, cov_marker_pose, camera, cam_in,

@@ -86,3 +86,22 @@ def test_ensemble_stats_kernel_matches_host():
     x, P = f.get_state()
     np.testing.assert_allclose(f.ensemble_stats(truth), ensemble.ensemble_stats_host(x, P, truth), rtol=1e-9,
                                atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_rccl_allreduce_through_c_abi():
+    """uwvk_pose_ensemble_allreduce over an RCCL communicator made by the C ABI
+    (uwvk_comm_*): with one rank the RCCL sum equals the local statistics
+    (the N-rank case runs in the driver's 8-GPU bench)."""
+    sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+    from uwvk import engine, synth
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(70, 30, "C3")
+    f = engine.PoseUKFBatch(70)
+    f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    f.set_process_noise_from_config(cfg, log["dt"])
+    f.run_log(f.upload_log(log))
+    truth = log["truth"].state(30)
+    comm = engine.RcclComm(1, engine.RcclComm.unique_id(), 0, 0)
+    np.testing.assert_array_equal(f.ensemble_stats(truth, comm), f.ensemble_stats(truth))
+    comm.close()
