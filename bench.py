@@ -125,9 +125,36 @@ def cpu_baseline(synth, cfg, uwv, mode, dof, threads):
     t0 = time.perf_counter()
     o.run_log(log, nthreads=threads)
     dt = time.perf_counter() - t0
+    # one instance on one core, the same log's first instance
+    o1 = O.OraclePoseBatch(1, dof)
+    log1 = {k: (v[:, :1] if k in ("gyro", "acc", "dvl", "pressure", "efforts") and hasattr(v, "ndim") and v.ndim >= 2
+                else v) for k, v in log.items()}
+    log1["adcp"] = log["adcp"][:, :, :1] if log["adcp"].size else log["adcp"]
+    for k in ("pos0", "pos_cov", "rot0", "rot_cov"):
+        log1[k] = log[k][:1]
+    log1["batch"] = 1
+    o1.init_from_config(log1["pos0"], log1["pos_cov"], log1["rot0"], log1["rot_cov"], cfg, uwv)
+    o1.set_process_noise_from_config(cfg, log["dt"])
+    t1 = time.perf_counter()
+    o1.run_log(log1, nthreads=1)
+    dt1 = time.perf_counter() - t1
     return {"value": batch * epochs / dt, "unit": "steps/s", "cores": threads, "kind": "port",
             "sample": "%d PoseUKF instances x %d epochs (%s, incl. %d DVL updates each), %d pthreads, %.2f s wall"
-                      % (batch, epochs, mode, int(((log["flags"] & 2) != 0).sum()), threads, dt)}
+                      % (batch, epochs, mode, int(((log["flags"] & 2) != 0).sum()), threads, dt),
+            "single_core": {"value": epochs / dt1, "unit": "steps/s", "cores": 1,
+                            "sample": "1 PoseUKF instance x %d epochs, %.2f s" % (epochs, dt1)},
+            "host": {"cpu": _cpu_model(), "logical_cpus": os.cpu_count()}}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main():
