@@ -467,6 +467,9 @@ uwvk_status uwvk_vel_run_log(uwvk_vel* h, const uwvk_vel_log* log, int64_t first
  * row (one sigma point per lane; fills the chip at small batches, e.g. C2's 4096). */
 #define UWVK_VEL_OPT_LANE_GROUPS 1
 uwvk_status uwvk_vel_set_option(uwvk_vel* h, int option, int value);
+/* setProcessNoiseCovariance [EXT pose_estimation base]: 4x4, shared by the
+ * batch (default: VelocityUKF.cpp:54-55, velocity diag 1e-4); predict adds dt * Q. */
+uwvk_status uwvk_vel_set_process_noise(uwvk_vel* h, const double Q[16]);
 uwvk_status uwvk_vel_synchronize(uwvk_vel* h);
 /* HIP events on the handle's stream around queued work (bench timing) */
 uwvk_status uwvk_vel_timer_start(uwvk_vel* h);
@@ -517,6 +520,10 @@ void* uwvk_ipose_stream(const uwvk_ipose* h);
 uwvk_status uwvk_ipose_init(uwvk_ipose* h, const double position_error_std[3], const double orientation_error_std[3],
                             double orientation_error_tau, const double* initial_position_error,
                             const double initial_position_error_std[3]);
+/* setProcessNoiseCovariance [EXT pose_estimation base]: 6x6, shared by the
+ * batch (uwvk_ipose_init sets diag(position_error_std^2, orientation_error_std^2),
+ * IndirectPoseUKF.cpp:76-80); predict shapes it as predictionStepImpl (:93-106). */
+uwvk_status uwvk_ipose_set_process_noise(uwvk_ipose* h, const double Q[36]);
 /* updatePoseReference (IndirectPoseUKF.cpp:144-147): batch*7 body in world, t(3) q(4) */
 uwvk_status uwvk_ipose_set_pose_reference(uwvk_ipose* h, const double* pose);
 /* predictionStep -> predictionStepImpl (IndirectPoseUKF.cpp:93-106) */

@@ -214,6 +214,10 @@ class OracleVelBatch:
         for i in range(self.batch):
             self.L.or_vel_init(self.ptr(i), dp(x[i]), dp(P[i]))
 
+    def set_process_noise(self, Q):
+        for i in range(self.batch):
+            self.L.or_vel_set_process_noise(self.ptr(i), dp(Q))
+
     def setup_motion_model(self, uwv):
         for i in range(self.batch):
             self.L.or_vel_setup_motion_model(self.ptr(i), C.byref(uwv))
@@ -406,6 +410,10 @@ class OracleIndirectPoseBatch(_SmallBatch):
         pose = _per(pose, self.batch, (7,))
         for i in range(self.batch):
             self.L.or_ipose_set_pose_reference(self.ptr(i), dp(pose[i]))
+
+    def set_process_noise(self, Q):
+        for i in range(self.batch):
+            self.L.or_ipose_set_process_noise(self.ptr(i), dp(Q))
 
     def predict(self, dt):
         for i in range(self.batch):

@@ -987,6 +987,9 @@ void or_vel_init(or_vel* f, const double x[4], const double P[16]) { /* Velocity
   for (int i = 0; i < 3; i++) f->Q[i * 4 + i] = 0.0001;
 }
 
+/* setProcessNoiseCovariance [EXT pose_estimation base] */
+void or_vel_set_process_noise(or_vel* f, const double Q[16]) { memcpy(f->Q, Q, 16 * sizeof(double)); }
+
 void or_vel_setup_motion_model(or_vel* f, const uwvk_uwv_params* uwv) { /* VelocityUKF.cpp:58-77 */
   f->uwv = *uwv;
   or_invert(6, uwv->inertia_matrix, f->Minv);

@@ -116,6 +116,7 @@ void or_vel_setup_motion_model(or_vel* f, const uwvk_uwv_params* uwv);
 int or_vel_set_gyro(or_vel* f, const double w[3], const double* cov);
 int or_vel_set_efforts(or_vel* f, const double tau[6], const double* cov);
 int or_vel_predict(or_vel* f, double dt);
+void or_vel_set_process_noise(or_vel* f, const double Q[16]);
 int or_vel_update_dvl(or_vel* f, const double mu[3], const double cov[9]);
 int or_vel_update_pressure(or_vel* f, const double mu[1], const double cov[1]);
 /* one RK4 step of the [EXT] ModelSimulation (state: p q v w), exposed for tests */
@@ -148,6 +149,7 @@ typedef struct or_ipose {  /* IndirectPoseUKF.hpp:18-86: {position_error, orient
 void or_ipose_init(or_ipose* f, const double pos_std[3], const double ori_std[3], double tau,
                    const double init_pos_err[3], const double init_pos_std[3]);
 void or_ipose_set_pose_reference(or_ipose* f, const double pose[7]);
+void or_ipose_set_process_noise(or_ipose* f, const double Q[36]);
 int or_ipose_predict(or_ipose* f, double dt);
 int or_ipose_update_visual(or_ipose* f, int nf, const double* features, const double* feature_cov,
                            const double* feature_pos, const double marker_pose[7], const double cov_marker[36],

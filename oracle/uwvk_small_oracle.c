@@ -286,6 +286,9 @@ void or_bottom_init(or_bottom* f, const double x[4], const double P[9]) {
 
 void or_bottom_set_process_noise(or_bottom* f, const double Q[9]) { memcpy(f->Q, Q, sizeof(double) * 9); }
 
+/* setProcessNoiseCovariance [EXT pose_estimation base] */
+void or_ipose_set_process_noise(or_ipose* f, const double Q[36]) { memcpy(f->Q, Q, sizeof(double) * 36); }
+
 void or_bottom_set_velocity(or_bottom* f, const double v[3]) { memcpy(f->velocity, v, sizeof(double) * 3); }
 
 /* processModel, BottomUKF.cpp:5-16 */

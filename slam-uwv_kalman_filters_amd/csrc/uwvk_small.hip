@@ -497,6 +497,13 @@ uwvk_status uwvk_ipose_init(uwvk_ipose* h, const double position_error_std[3], c
   return UWVK_OK;
 }
 
+uwvk_status uwvk_ipose_set_process_noise(uwvk_ipose* h, const double Q[36]) {
+  if (!h || !Q) return UWVK_EINVAL;
+  if (!finite_all(Q, 36)) return UWVK_ENAN;
+  std::memcpy(h->Q.v, Q, sizeof(h->Q.v));
+  return UWVK_OK;
+}
+
 uwvk_status uwvk_ipose_set_pose_reference(uwvk_ipose* h, const double* pose) {
   if (!h || !pose) return UWVK_EINVAL;
   if (!finite_all(pose, (size_t)h->batch * 7)) return UWVK_ENAN;

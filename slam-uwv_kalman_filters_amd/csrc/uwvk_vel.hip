@@ -791,6 +791,13 @@ uwvk_status uwvk_vel_set_option(uwvk_vel* h, int option, int value) {
   return UWVK_OK;
 }
 
+uwvk_status uwvk_vel_set_process_noise(uwvk_vel* h, const double Q[16]) {
+  if (!h || !Q) return UWVK_EINVAL;
+  if (!vfinite(Q, 16)) return UWVK_ENAN;
+  std::memcpy(h->P.Q0, Q, sizeof(h->P.Q0));
+  return UWVK_OK;
+}
+
 uwvk_status uwvk_vel_synchronize(uwvk_vel* h) {
   if (!h) return UWVK_EINVAL;
   return hipStreamSynchronize(h->stream) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;

@@ -33,6 +33,10 @@ class IndirectPoseUKF {
   virtual ~IndirectPoseUKF() { uwvk_ipose_destroy(h_); }
 
   int64_t batch() const { return batch_; }
+  // setProcessNoiseCovariance [EXT pose_estimation base]: 6x6 shared by the batch
+  void setProcessNoiseCovariance(const std::array<double, 36>& Q) {
+    check(uwvk_ipose_set_process_noise(h_, Q.data()), "setProcessNoiseCovariance");
+  }
   // updatePoseReference (IndirectPoseUKF.cpp:144-147): batch poses {t, q}
   void updatePoseReference(const std::vector<Pose7>& pose_ref) {
     if (pose_ref.size() != (size_t)batch_) throw std::invalid_argument("updatePoseReference: wrong size");

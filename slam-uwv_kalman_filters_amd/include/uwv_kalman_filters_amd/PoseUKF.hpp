@@ -316,6 +316,10 @@ class VelocityUKF {
   virtual ~VelocityUKF() { uwvk_vel_destroy(h_); }
 
   void setupMotionModel(const UWVParameters& p) { check(uwvk_vel_setup_motion_model(h_, &p), "setupMotionModel"); }
+  // setProcessNoiseCovariance [EXT pose_estimation base]: 4x4 shared by the batch
+  void setProcessNoiseCovariance(const std::array<double, 16>& Q) {
+    check(uwvk_vel_set_process_noise(h_, Q.data()), "setProcessNoiseCovariance");
+  }
   void predictionStep(double dt) { check(uwvk_vel_predict(h_, dt), "predictionStep"); }
   void integrateMeasurement(const GyroMeasurement& m) {
     check(uwvk_vel_set_gyro(h_, m.mu.data(), m.cov.empty() ? nullptr : m.cov.data()), "integrateMeasurement(Gyro)");

@@ -34,7 +34,8 @@ SYMBOLS = [
     "uwvk_vel_update_pressure", "uwvk_vel_get_state", "uwvk_vel_get_model_state", "uwvk_vel_run_log",
     "uwvk_vel_set_option", "uwvk_vel_synchronize", "uwvk_vel_timer_start", "uwvk_vel_timer_stop",
     "uwvk_pose_ensemble_allreduce", "uwvk_comm_unique_id_bytes", "uwvk_comm_unique_id", "uwvk_comm_init",
-    "uwvk_comm_destroy", "uwvk_comm_allreduce_sum_device",
+    "uwvk_comm_destroy", "uwvk_comm_allreduce_sum_device", "uwvk_vel_set_process_noise",
+    "uwvk_ipose_set_process_noise",
     "uwvk_schedule_streams", "uwvk_adcp_cell_weighting", "uwvk_pose_update_visual_landmark",
     "uwvk_bottom_create", "uwvk_bottom_destroy", "uwvk_bottom_stream", "uwvk_bottom_init",
     "uwvk_bottom_set_process_noise", "uwvk_bottom_set_velocity", "uwvk_bottom_predict", "uwvk_bottom_update_range",
@@ -368,6 +369,11 @@ class VelocityUKFBatch:
         _chk(self.L.uwvk_vel_run_log(self.h, C.byref(dlog.s), C.c_int64(first), C.c_int64(count)), "vel_run_log")
         if sync:
             self.synchronize()
+
+    def set_process_noise(self, Q):
+        """setProcessNoiseCovariance [EXT base]: 4x4 shared by the batch."""
+        Q = _f64(Q)
+        _chk(self.L.uwvk_vel_set_process_noise(self.h, _p(Q)), "vel_set_process_noise")
 
     def set_lane_groups(self, value):
         """-1 auto, 0 one filter per lane, 1 one filter per 16 lanes (UWVK_VEL_OPT_LANE_GROUPS)."""

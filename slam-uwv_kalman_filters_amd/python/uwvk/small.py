@@ -104,6 +104,11 @@ class IndirectPoseUKFBatch(_Small):
         a, b = _f64(pos_std), _f64(ori_std)
         _chk(self._fn("init")(self.h, _p(a), _p(b), C.c_double(tau), _p(ipe), _p(ips)), "ipose_init")
 
+    def set_process_noise(self, Q):
+        """setProcessNoiseCovariance [EXT base]: 6x6 shared by the batch."""
+        Q = _f64(Q)
+        _chk(self._fn("set_process_noise")(self.h, _p(Q)), "ipose_set_process_noise")
+
     def set_pose_reference(self, pose):
         pose = _per(pose, self.batch, (7,))
         _chk(self._fn("set_pose_reference")(self.h, _p(pose)), "ipose_set_pose_reference")

@@ -155,6 +155,29 @@ def test_velocity_ukf(eng, orc, groups, B):
     assert np.max(np.abs(mg - mo)) < 1e-9
 
 
+@pytest.mark.parametrize("groups", [0, 1])
+def test_velocity_ukf_process_noise(eng, orc, groups):
+    """setProcessNoiseCovariance [EXT base] with a full 4x4 Q (incl. z and couplings)."""
+    from uwvk import synth
+    B = 9
+    log = synth.make_vel_log(B, 300)
+    A = np.array([[2e-2, 1e-3, 0, 0], [0, 1e-2, 2e-3, 0], [0, 0, 1e-2, 0], [1e-3, 0, 0, 5e-3]])
+    Q = A @ A.T
+    o, g = orc.OracleVelBatch(B), eng.VelocityUKFBatch(B)
+    g.set_lane_groups(groups)
+    for f in (o, g):
+        f.init(log["x0"], log["P0"])
+        f.set_process_noise(Q)
+        f.set_gyro(log["gyro"][0])
+        f.setup_motion_model(synth.default_uwv())
+    o.run_log(log)
+    g.run_log(g.upload_log(log))
+    (xo, Po), (xg, Pg) = o.get_state(), g.get_state()
+    sd = np.sqrt(np.diagonal(Po, axis1=1, axis2=2))
+    assert np.max(np.abs(xg - xo) / sd) < TOL_LOG
+    assert cov_err(Pg, Po).max() < TOL_LOG
+
+
 def test_velocity_ukf_api(eng, orc):
     from uwvk import synth
     B = 8

@@ -333,3 +333,23 @@ def test_gpu_pose_visual_landmark(dof):
         g.update_visual(px, fcov, fpos, marker, cm, cam, cib)
     assert e.value.code == 2
     np.testing.assert_array_equal(g.get_state()[0], xg)
+
+
+@pytest.mark.gpu
+def test_gpu_ipose_process_noise():
+    """setProcessNoiseCovariance [EXT base] with cross terms between position and orientation error."""
+    B = 7
+    ref, p_err, q_err, marker, px = ipose_scene(B)
+    g, o = IndirectPoseUKFBatch(B), O.OracleIndirectPoseBatch(B)
+    A = np.random.default_rng(4).normal(0, 1, (6, 6)) * np.r_[[0.1] * 3, [0.01] * 3][:, None]
+    Q = A @ A.T + np.diag([1e-3] * 3 + [1e-5] * 3)
+    for f in (g, o):
+        f.init([0.1, 0.1, 0.2], [0.01, 0.01, 0.02], 20.0, None, [0.5, 0.5, 0.5])
+        f.set_process_noise(Q)
+        f.set_pose_reference(ref)
+    for step in range(5):
+        for f in (g, o):
+            f.predict(0.1)
+    (xg, Pg), (xo, Po) = g.get_state(), o.get_state()
+    assert cov_err(Pg, Po).max() < TOL
+    assert float(np.max(qlog_err(xg[:, 3:], xo[:, 3:]))) < 1e-12
