@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--dof", type=int, default=53)
     ap.add_argument("--mode", default="C3", choices=["C2", "C3", "C4"],
                     help="C3 (headline) / C4: PoseUKF; C2: VelocityUKF (secondary line)")
+    ap.add_argument("--c4-cycle", default="30,10",
+                    help="C4 DVL drop-out cycle 'on,off' in s; e.g. 0.3,0.1 keeps every event rate of the 30/10 "
+                         "cycle (0.25%% efforts epochs) inside a 2000-epoch window")
     ap.add_argument("--vel-groups", type=int, default=-1, help="C2: -1 auto, 0 lane per filter, 1 16-lane rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true", help="literal kernels (all 2n+1 sigma points)")
@@ -90,14 +93,15 @@ def parse():
     return ap.parse_args()
 
 
-def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance):
+def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance, c4_cycle=(30.0, 10.0)):
     """Log of warmup+steps epochs whose 5 Hz DVL schedule puts at least one DVL
     epoch inside the timed window (exactly the 1-in-200 rate when steps >= 200)."""
     total = warmup + steps
     # shift the start so that a DVL epoch (k % 200 == 0) lands mid-window
     target = warmup + min(steps, 200) // 2
     shift = (200 - (target + 1) % 200) % 200
-    log = synth.make_pose_log(batch, total + shift, mode=mode, dof=dof, first_instance=first_instance)
+    log = synth.make_pose_log(batch, total + shift, mode=mode, dof=dof, first_instance=first_instance,
+                              dropout_on=c4_cycle[0], dropout_off=c4_cycle[1])
     return log, shift
 
 
@@ -183,7 +187,8 @@ def main():
         return bench_vel(a, engine, synth, world, rank, local, dist)
     B = a.batch_per_gpu or 65536
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
-    log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, a.mode, a.dof, first_instance=rank * B)
+    cyc = tuple(float(v) for v in a.c4_cycle.split(","))
+    log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, a.mode, a.dof, first_instance=rank * B, c4_cycle=cyc)
     f = engine.PoseUKFBatch(B, a.dof, device=local)
     if a.dense:
         f.set_dense_sigma(True)
@@ -252,7 +257,10 @@ def main():
                                % (a.mode, a.dof, B, " + ADCP x4 + DVL drop-out/efforts + pressure"
                                   if a.mode == "C4" else ""),
                    "global_batch": B * world, "batch_per_gpu": B, "step": "one IMU epoch per instance",
-                   "dvl_epochs_in_window": n_dvl, "parallelism": "instance-sharded x%d (no data-path collective)"
+                   "dvl_epochs_in_window": n_dvl,
+                   "efforts_epochs_in_window": n_eff,
+                   "adcp_epochs_in_window": int(((window & 8) != 0).sum()),
+                   "c4_cycle_s": list(cyc) if a.mode == "C4" else None, "parallelism": "instance-sharded x%d (no data-path collective)"
                                                                   % world,
                    "path": "dense (all 2n+1 sigma points)" if a.dense else "PSP (partitioned sigma points)",
                    "kernel": kname},
