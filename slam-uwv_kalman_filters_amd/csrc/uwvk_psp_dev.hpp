@@ -37,9 +37,6 @@
 #ifndef PSP_ABL
 #define PSP_ABL 0
 #endif
-#ifndef PSP_RANKM_LDS
-#define PSP_RANKM_LDS 1   // Sigma~ -= C~ K~^T: 1 C~_i by LDS broadcast, 0 by readlane
-#endif
 
 namespace uwvk {
 namespace psp {
@@ -749,6 +746,30 @@ struct PZ {  // measurementZPosition, PoseUKF.cpp:100-105: linear (k = 0)
   UWVK_DEV void jac(const double*, double (&H)[M][NC]) const { H[0][0] = 1; }
 };
 
+// Sigma~ -= C~ K~^T on rows [i0, i0 + R): lane l owns column l (entries
+// (i, l), i >= l).  The packed offset of (i0 + r, 0) is uniform (scalar ALU),
+// so a row costs one address add, the mask compare, M FMAs and the store;
+// C~_i is an LDS broadcast (stg[M i ..]).  Rows are loaded before any store.
+// Lanes l > i load a neighbouring entry of the same PspSmem (never stored).
+template <int R, int M>
+UWVK_DEV void rankm_rows(double* S, const double* stg, int i0, int l, const double (&Kt)[M]) {
+  const int tri = i0 * (i0 + 1) / 2;
+  double sv[R], cv[R][M];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    sv[r] = S[tri + r * i0 + r * (r + 1) / 2 + l];
+#pragma unroll
+    for (int a = 0; a < M; a++) cv[r][a] = stg[M * (i0 + r) + a];
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    double s2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < M; a++) s2 += cv[r][a] * Kt[a];
+    if (l <= i0 + r) S[tri + r * i0 + r * (r + 1) / 2 + l] = sv[r] - s2;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // ukf::update [EXT], PSP form.  gate: 0 accept any, 1 d2p95.  Returns the gate
 // decision; *ok = false on a non-positive pivot of the partial Cholesky.
@@ -895,9 +916,8 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   const bool accept = gate == 0 ? true : !(d2 > kD2P95);
   if (!accept) return false;
   UWVK_STAMP(33);
-  // Sigma -= C K^T: row sweep, lane = column j holds K_j; C_i arrives as a
-  // uniform (readlane) value; the next row's load precedes this row's store.
-  // delta = K nu (lane r).
+  // Sigma -= C K^T: row sweep (rankm_rows), lane = column j holds K_j, C_i is
+  // an LDS broadcast; each block's loads precede its stores.  delta = K nu (lane r).
   psync();
   double dl = 0.0;  // delta = K nu, lane r
 #pragma unroll
@@ -910,45 +930,17 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     Kt[i] = Kg[i] * ids;
   }
   {
-#if PSP_RANKM_LDS
     if (l < DOF) {  // C~ rows for the broadcast reads (stg is free here)
 #pragma unroll
       for (int a2 = 0; a2 < M; a2++) sm.stg[M * l + a2] = Ct[a2];
     }
     psync();
-#endif
-    // row blocks of RB: every load of a block is issued before its stores
-    constexpr int RB = PSP_RB;
+    constexpr int RB = PSP_RB, NB = DOF / RB, REM = DOF - NB * RB;
+    static_assert(63 < 56 + PG<DOF>::STG, "row over-read (lanes l > i, last rows) stays inside PspSmem");
+    if (!(PSP_ABL & 2)) {
 #pragma unroll 1
-    for (int i0 = 0; i0 < ((PSP_ABL & 2) ? 0 : DOF); i0 += RB) {
-      double sv[RB];
-#if PSP_RANKM_LDS
-      double cv[RB][M];  // C~ rows of the block, broadcast loads issued up front
-#endif
-#pragma unroll
-      for (int r = 0; r < RB; r++) {
-        const int i = i0 + r;
-        sv[r] = (i < DOF && l <= i) ? sm.S[i * (i + 1) / 2 + l] : 0.0;
-#if PSP_RANKM_LDS
-        const int ic = i < DOF ? i : DOF - 1;
-#pragma unroll
-        for (int a2 = 0; a2 < M; a2++) cv[r][a2] = sm.stg[M * ic + a2];
-#endif
-      }
-#pragma unroll
-      for (int r = 0; r < RB; r++) {
-        const int i = i0 + r < DOF ? i0 + r : DOF - 1;
-        double s2 = 0.0;
-#pragma unroll
-        for (int a2 = 0; a2 < M; a2++) {
-#if PSP_RANKM_LDS
-          s2 += cv[r][a2] * Kt[a2];
-#else
-          s2 += readlane_d(Ct[a2], i) * Kt[a2];
-#endif
-        }
-        if (i0 + r < DOF && l <= i) sm.S[i * (i + 1) / 2 + l] = sv[r] - s2;
-      }
+      for (int b = 0; b < NB; b++) rankm_rows<RB, M>(sm.S, sm.stg, b * RB, l, Kt);
+      if constexpr (REM > 0) rankm_rows<REM, M>(sm.S, sm.stg, NB * RB, l, Kt);
     }
   }
   psync();
