@@ -37,6 +37,17 @@
 #ifndef PSP_ABL
 #define PSP_ABL 0
 #endif
+// instruction-count trims (A/B bitmask): 1 lane-limited wave sums, 2 manifold
+// mean without sqrt / division, 4 rank-m rows as one FMA chain, 8 reciprocal
+// by v_rcp_f64 + Newton in the small-angle SO3 log, 16 one product for the
+// Cholesky column incl. its diagonal, 32 v_rcp_f64 + Newton for 1/d, 64 the
+// Cholesky panel read with immediate offsets from the row start.
+// Measured on the C3 bench (kernel ms per 200-epoch launch): none 103.2,
+// 1-8 97.5, +16 95.4, +32 within noise, +64 94.3.  Rejected: Delta_j as LDS
+// broadcasts instead of v_readlane (105.9), the same for Dz / P (no change).
+#ifndef PSP_FAST
+#define PSP_FAST 127
+#endif
 
 namespace uwvk {
 namespace psp {
@@ -91,13 +102,22 @@ UWVK_DEV double dpp_d(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW, BANK, true);
   return __hiloint2double(hi, lo);
 }
+// NL: lanes that may hold a non-zero term (the others must pass 0).  Sums over
+// <= 16 lanes stop at the row total (lane 15), <= 32 lanes after row_bcast:15.
+template <int NL = 64>
 UWVK_DEV double wave_sum_dpp(double v) {
   double s = v + dpp_d<0x111, 0xf, 0xf>(v);   // row_shr:1
   s = s + dpp_d<0x112, 0xf, 0xf>(v);          // row_shr:2
   s = s + dpp_d<0x113, 0xf, 0xf>(v);          // row_shr:3
   s = s + dpp_d<0x114, 0xf, 0xe>(s);          // row_shr:4, banks 1-3
   s = s + dpp_d<0x118, 0xf, 0xc>(s);          // row_shr:8, banks 2-3
+#if PSP_FAST & 1
+  if constexpr (NL <= 16) return readlane_d(s, 15);
+#endif
   s = s + dpp_d<0x142, 0xa, 0xf>(s);          // row_bcast:15, rows 1,3
+#if PSP_FAST & 1
+  if constexpr (NL <= 32) return readlane_d(s, 31);
+#endif
   s = s + dpp_d<0x143, 0xc, 0xf>(s);          // row_bcast:31, rows 2,3
   return readlane_d(s, 63);
 }
@@ -137,7 +157,13 @@ UWVK_DEV void so3_log_psp(const double q[4], double o[3]) {
   if (w < 0) { w = -w; x = -x; y = -y; z = -z; }
   const double n2 = x * x + y * y + z * z, w2 = w * w;
   if (n2 < 0.0025 * w2) {  // r = |v|/w < 0.05 (rotation < 0.1 rad)
+#if PSP_FAST & 8
+    double iw = __builtin_amdgcn_rcp(w);  // w in (0.99, 1]: two Newton steps -> correctly rounded to ~1 ulp
+    iw = fma(iw, fma(-w, iw, 1.0), iw);
+    iw = fma(iw, fma(-w, iw, 1.0), iw);
+#else
     const double iw = 1.0 / w;
+#endif
     const double r2 = n2 * (iw * iw);
     // atan(r)/r = sum (-r^2)^k / (2k+1), k <= 8
     double a = 1.0 / 17.0;
@@ -196,7 +222,13 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
   if constexpr (J < K) {
     ok = ok && (piv > 0.0);
     const double inv = rsqrt_f64(piv);
+#if PSP_FAST & 16
+    // lane J's own a[J] is the pivot (the look-ahead below evaluates the same
+    // fma as the column update), so one product serves the diagonal too
+    a[J] = (r >= J) ? a[J] * inv : 0.0;
+#else
     a[J] = (r == J) ? piv * inv : (r > J ? a[J] * inv : 0.0);
+#endif
     // look-ahead: the next pivot is lane J+1's a[J+1] - L[J+1][J]^2 (its own
     // registers), so its rsqrt need not wait for the column broadcast
     double pnext = 0.0;
@@ -224,8 +256,17 @@ constexpr int STG_ROWS = 32;
 template <int DOF, int K, class RL>
 UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* stg) {
   const int rr = r < DOF ? r : DOF - 1;
+#if PSP_FAST & 64
+  // row rr from its packed start with immediate offsets: for c > rr this reads
+  // a later (finite) entry of Sigma~, which the column steps never use (they
+  // zero L[r][c] for r < c before it is read)
+  const double* Sr = S + rr * (rr + 1) / 2;
+#pragma unroll
+  for (int c = 0; c < K; c++) a[c] = Sr[c] * (scaled_dof(c) ? dl * readlane_d(dl, c) : dl);
+#else
 #pragma unroll
   for (int c = 0; c < K; c++) a[c] = S[pidx(rr, c)] * (scaled_dof(c) ? dl * readlane_d(dl, c) : dl);
+#endif
   bool ok = true;
   int q = -1;
 #pragma unroll
@@ -489,7 +530,11 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       nrm = 0.0;
 #pragma unroll
       for (int i = 0; i < 3; i++) {
-        d[i] = wave_sum_dpp(w * d[i]) / (double)G::N;
+#if PSP_FAST & 2
+        d[i] = wave_sum_dpp<2 * K + 1>(w * d[i]) * (1.0 / (double)G::N);
+#else
+        d[i] = wave_sum_dpp<2 * K + 1>(w * d[i]) / (double)G::N;
+#endif
         nrm += d[i] * d[i];
       }
       double e[4], q[4];
@@ -497,8 +542,12 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       qmul(e, mq, q);
 #pragma unroll
       for (int i = 0; i < 4; i++) mq[i] = q[i];
+#if PSP_FAST & 2
+    } while (!(PSP_ABL & 1) && nrm > 1e-12 && ++it < 10000);  // |delta| > 1e-6
+#else
       nrm = sqrt(nrm);
     } while (!(PSP_ABL & 1) && nrm > 1e-6 && ++it < 10000);
+#endif
   }
   UWVK_STAMP(22);
   // deviations; ori x ori block; Delta_j = d_{j+} - d_{j-}
@@ -511,7 +560,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
-      for (int j = 0; j <= i; j++) oo[k++] = 0.5 * wave_sum_dpp(w * d[i] * d[j]);
+      for (int j = 0; j <= i; j++) oo[k++] = 0.5 * wave_sum_dpp<2 * K + 1>(w * d[i] * d[j]);
   }
   // Delta_j = d_{j+} - d_{j-} lives in lane 2j; it is read back as a uniform
   // (SGPR) value below, no LDS staging
@@ -553,7 +602,13 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   // new time scale d' = A_ll d (A_ll = 1 on the unscaled DOFs)
   if (l < DOF && scaled_dof(l)) {
     ds = aj * ds;
+#if PSP_FAST & 32
+    double rc = __builtin_amdgcn_rcp(ds);  // d in (0, 1]: two Newton steps
+    rc = fma(rc, fma(-ds, rc, 1.0), rc);
+    ids = fma(rc, fma(-ds, rc, 1.0), rc);
+#else
     ids = 1.0 / ds;
+#endif
   }
   psync();
   UWVK_STAMP(24);
@@ -763,10 +818,17 @@ UWVK_DEV void rankm_rows(double* S, const double* stg, int i0, int l, const doub
   }
 #pragma unroll
   for (int r = 0; r < R; r++) {
+#if PSP_FAST & 4
+    double s2 = sv[r];
+#pragma unroll
+    for (int a = 0; a < M; a++) s2 = fma(-cv[r][a], Kt[a], s2);
+    if (l <= i0 + r) S[tri + r * i0 + r * (r + 1) / 2 + l] = s2;
+#else
     double s2 = 0.0;
 #pragma unroll
     for (int a = 0; a < M; a++) s2 += cv[r][a] * Kt[a];
     if (l <= i0 + r) S[tri + r * i0 + r * (r + 1) / 2 + l] = sv[r] - s2;
+#endif
   }
 }
 
@@ -804,8 +866,12 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   // zbar = z_0 + (1/N) sum_{2K} (z_p - z_0)  (the linear pairs cancel)
 #pragma unroll
   for (int i = 0; i < M; i++) {
-    const double s = K > 0 ? wave_sum_dpp(pt ? zp[i] - zc[i] : 0.0) : 0.0;
+    const double s = K > 0 ? wave_sum_dpp<2 * K>(pt ? zp[i] - zc[i] : 0.0) : 0.0;
+#if PSP_FAST & 2
+    zb[i] = zc[i] + s * (1.0 / (double)G::N);
+#else
     zb[i] = zc[i] + s / (double)G::N;
+#endif
     e[i] = zc[i] - zb[i];
   }
   double dz[M];
@@ -817,7 +883,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   for (int i = 0; i < M; i++)
 #pragma unroll
     for (int j = 0; j <= i; j++) {
-      const double s = K > 0 ? wave_sum_dpp(pt ? dz[i] * dz[j] : 0.0) : 0.0;
+      const double s = K > 0 ? wave_sum_dpp<2 * K>(pt ? dz[i] * dz[j] : 0.0) : 0.0;
       S[i * M + j] = 0.5 * (s + wc * e[i] * e[j]);
     }
   // Delta z_j = z_{j+} - z_{j-} lives in lane 2j (read back as uniform values)
@@ -854,8 +920,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   for (int i = 0; i < M; i++) Gr[i] = 0.0;
 #pragma unroll
   for (int t = 0; t < NC; t++) {
-    constexpr int dummy = 0;
-    (void)dummy;
     double s = sm.S[pidx(rl, HM::cols[t])];
     if (scaled_dof(HM::cols[t])) s = s * readlane_d(ds, HM::cols[t]);
 #pragma unroll
