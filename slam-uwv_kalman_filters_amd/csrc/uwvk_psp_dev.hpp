@@ -41,12 +41,16 @@
 // mean without sqrt / division, 4 rank-m rows as one FMA chain, 8 reciprocal
 // by v_rcp_f64 + Newton in the small-angle SO3 log, 16 one product for the
 // Cholesky column incl. its diagonal, 32 v_rcp_f64 + Newton for 1/d, 64 the
-// Cholesky panel read with immediate offsets from the row start.
+// Cholesky panel read with immediate offsets from the row start, 256 the
+// update's z-bar and S sums as one LDS-transposed round (lds_sums), 512 the
+// same for the predict's ori x ori sums.
 // Measured on the C3 bench (kernel ms per 200-epoch launch): none 103.2,
-// 1-8 97.5, +16 95.4, +32 within noise, +64 94.3.  Rejected: Delta_j as LDS
-// broadcasts instead of v_readlane (105.9), the same for Dz / P (no change).
+// 1-8 97.5, +16 95.4, +32 within noise, +64 94.3, +256/512 92.0.  Rejected:
+// Delta_j as LDS broadcasts instead of v_readlane (105.9), the same for Dz / P
+// (no change), lds_sums in the manifold-mean loop (+0.7%), s_setprio around
+// the Cholesky column chain (within noise).
 #ifndef PSP_FAST
-#define PSP_FAST 127
+#define PSP_FAST 895
 #endif
 
 namespace uwvk {
@@ -196,6 +200,36 @@ UWVK_DEV double swap_pair_d(double v) { return dpp_d<0xb1, 0xf, 0xf>(v); }
 UWVK_DEV double sel3(double v0, double v1, double v2, int i) { return i == 0 ? v0 : (i == 1 ? v1 : v2); }
 UWVK_DEV double sel6(double v0, double v1, double v2, double v3, double v4, double v5, int i) {
   return i < 3 ? sel3(v0, v1, v2, i) : sel3(v3, v4, v5, i - 3);
+}
+
+UWVK_DEV void wsync() {  // LDS ordering point between the lanes of one wave
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// R sums over NL contributors at once (instead of R DPP reductions): lane
+// l = STRIDE * c (c < NL) writes v[i] to buf[i * NL + c]; lane i < R adds row
+// i by a pairwise tree; out[i] is read back as a uniform value.
+template <int R, int NL, int STRIDE>
+UWVK_DEV void lds_sums(const double (&v)[R], double* buf, int l, double (&out)[R]) {
+  static_assert(NL % 2 == 0 && R * NL <= 160, "transpose buffer");
+  const int c = l / STRIDE;
+  if (l % STRIDE == 0 && c < NL) {
+#pragma unroll
+    for (int i = 0; i < R; i++) buf[i * NL + c] = v[i];
+  }
+  wsync();
+  const double* row = buf + (l < R ? l : 0) * NL;  // 8-B aligned only (ds_read2_b64 pairs)
+  double p[NL / 2];
+#pragma unroll
+  for (int k = 0; k < NL / 2; k++) p[k] = row[2 * k] + row[2 * k + 1];
+#pragma unroll
+  for (int w = 1; w < NL / 2; w *= 2)
+#pragma unroll
+    for (int k = 0; k + w < NL / 2; k += 2 * w) p[k] += p[k + w];
+#pragma unroll
+  for (int i = 0; i < R; i++) out[i] = readlane_d(p[0], i);
 }
 
 UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
@@ -556,11 +590,29 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   double oo[6];
   {
     const double w = pt ? 1.0 : (ctr ? wc : 0.0);
+#if PSP_FAST & 512
+    // six sums over lanes 0..2K: pair sums by one DPP swap, then the 16 even
+    // lanes' values transposed through LDS (stg is free after the points)
+    double v[6];
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j <= i; j++) {
+        const double t = w * d[i] * d[j];
+        v[k++] = t + swap_pair_d(t);
+      }
+    static_assert(2 * K + 1 <= 32, "pair sums over two DPP rows");
+    lds_sums<6, 16, 2>(v, sm.stg, l, oo);
+#pragma unroll
+    for (int i = 0; i < 6; i++) oo[i] = 0.5 * oo[i];
+#else
     int k = 0;
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
       for (int j = 0; j <= i; j++) oo[k++] = 0.5 * wave_sum_dpp<2 * K + 1>(w * d[i] * d[j]);
+#endif
   }
   // Delta_j = d_{j+} - d_{j-} lives in lane 2j; it is read back as a uniform
   // (SGPR) value below, no LDS staging
@@ -863,6 +915,70 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double zc[M], zb[M], e[M];
 #pragma unroll
   for (int i = 0; i < M; i++) zc[i] = readlane_d(zp[i], 2 * K);
+  constexpr double wc = 1.0 + 2.0 * (DOF - K);
+  double S[M * M];
+#if PSP_FAST & 256
+  // H and P first: P reads the staged rows, after which stg holds the
+  // transposed sums.  One round of M + M(M+1)/2 sums over the 2K point lanes:
+  // u = z_p - z_0, s = sum u, m = s / N; sum dz dz^T = sum u u^T - m s^T - s m^T + 2K m m^T
+  double Hs[M][NC];
+  {
+    double H[M][NC];
+    hm.jac(sm.mu, H);
+#pragma unroll
+    for (int i = 0; i < M; i++)
+#pragma unroll
+      for (int t = 0; t < NC; t++) Hs[i][t] = readlane_d(H[i][t], 0);
+  }
+  double Pl = 0.0;
+  if constexpr (K > 0) {
+    const int q = l < M * K ? l : 0;
+    const int i = q / K, j = q - (q / K) * K;
+#pragma unroll
+    for (int t = 0; t < NC; t++) {
+      double h = Hs[0][t];
+#pragma unroll
+      for (int ii = 1; ii < M; ii++) h = (i == ii) ? Hs[ii][t] : h;
+      Pl += h * sm.stg[STG_ROWS + row_pos(HM::rows, HM::cols[t]) * K + j];
+    }
+    constexpr int R = M + M * (M + 1) / 2;
+    double v[R], sums[R];
+#pragma unroll
+    for (int i2 = 0; i2 < M; i2++) v[i2] = zp[i2] - zc[i2];
+    int k = M;
+#pragma unroll
+    for (int i2 = 0; i2 < M; i2++)
+#pragma unroll
+      for (int j2 = 0; j2 <= i2; j2++) v[k++] = v[i2] * v[j2];
+    lds_sums<R, 2 * K, 1>(v, sm.stg, l, sums);
+    double m[M];
+#pragma unroll
+    for (int i2 = 0; i2 < M; i2++) {
+      m[i2] = sums[i2] * (1.0 / (double)G::N);
+      zb[i2] = zc[i2] + m[i2];
+      e[i2] = zc[i2] - zb[i2];
+    }
+    k = M;
+#pragma unroll
+    for (int i2 = 0; i2 < M; i2++)
+#pragma unroll
+      for (int j2 = 0; j2 <= i2; j2++) {
+        const double s = sums[k++] - m[i2] * sums[j2] - m[j2] * sums[i2] + (2.0 * K) * m[i2] * m[j2];
+        S[i2 * M + j2] = 0.5 * (s + wc * e[i2] * e[j2]);
+      }
+  } else {
+#pragma unroll
+    for (int i2 = 0; i2 < M; i2++) {
+      zb[i2] = zc[i2];
+      e[i2] = 0.0;
+#pragma unroll
+      for (int j2 = 0; j2 <= i2; j2++) S[i2 * M + j2] = 0.0;
+    }
+  }
+  double zd[M];
+#pragma unroll
+  for (int i = 0; i < M; i++) zd[i] = K > 0 ? zp[i] - swap_pair_d(zp[i]) : 0.0;
+#else
   // zbar = z_0 + (1/N) sum_{2K} (z_p - z_0)  (the linear pairs cancel)
 #pragma unroll
   for (int i = 0; i < M; i++) {
@@ -877,8 +993,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double dz[M];
 #pragma unroll
   for (int i = 0; i < M; i++) dz[i] = zp[i] - zb[i];
-  constexpr double wc = 1.0 + 2.0 * (DOF - K);
-  double S[M * M];
 #pragma unroll
   for (int i = 0; i < M; i++)
 #pragma unroll
@@ -890,7 +1004,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double zd[M];
 #pragma unroll
   for (int i = 0; i < M; i++) zd[i] = K > 0 ? zp[i] - swap_pair_d(zp[i]) : 0.0;
-  UWVK_STAMP(31);
   // affine part.  H at mu: every lane evaluates it, the values become uniform
   // (SGPR) copies; P = H L_a lane-parallel (lane i*K + j); G = Sigma H^T (lane r).
   double Hs[M][NC];
@@ -914,6 +1027,8 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       Pl += h * sm.stg[STG_ROWS + row_pos(HM::rows, HM::cols[t]) * K + j];
     }
   }
+#endif
+  UWVK_STAMP(31);
   const int rl = l < DOF ? l : DOF - 1;
   double Gr[M];
 #pragma unroll
