@@ -105,16 +105,38 @@ def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance, c4_c
     return log, shift
 
 
-def roofline_traffic(workload):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
+def pmc_entry(workload):
+    """The committed rocprofv3 PMC summary of this workload's kernel (or {})."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        e = d.get(workload)
-        return None if e is None else float(e["bytes_per_launch"])
-    except (OSError, ValueError, KeyError):
+            return json.load(f).get(workload) or {}
+    except (OSError, ValueError):
+        return {}
+
+
+def roofline_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
+    e = pmc_entry(workload)
+    return float(e["bytes_per_launch"]) if "bytes_per_launch" in e else None
+
+
+# VALU issue roof: 256 CUs x 4 SIMDs, a wave64 VALU instruction occupies its
+# 16-lane SIMD for 4 cycles (fp64 FMA included), 2.4 GHz peak engine clock
+N_SIMD, CYC_PER_VALU, CLOCK_HZ = 1024, 4, 2.4e9
+
+
+def valu_issue(workload, kernel_ms_per_launch, epochs_per_launch):
+    """Fraction of the chip's VALU issue slots the kernel fills: the committed
+    SQ_INSTS_VALU count per epoch (rocprofv3 --pmc, profiles/pmc_traffic.json)
+    scaled to this launch, divided by the launch's SIMD cycles."""
+    e = pmc_entry(workload)
+    if "valu_insts_per_epoch" not in e:
         return None
+    insts = float(e["valu_insts_per_epoch"]) * epochs_per_launch
+    slots = N_SIMD * (kernel_ms_per_launch * 1e-3) * CLOCK_HZ / CYC_PER_VALU
+    return {"valu_insts_per_launch": insts, "frac": insts / slots,
+            "valu_insts_per_wave_epoch": e.get("valu_insts_per_wave_epoch"), "source": e.get("valu_source")}
 
 
 def cpu_baseline(synth, cfg, uwv, mode, dof, threads):
@@ -271,7 +293,8 @@ def main():
                      "algorithmic_flop_per_step": F_STEP,
                      "executed_flop_per_step": (F_STEP_EXEC if a.dense else F_STEP_PSP),
                      "executed_tflops": exec_tf, "executed_frac": exec_tf / PEAK_FP64_TFLOPS,
-                     "hbm_frac_algorithmic": (B * B_STEP * a.steps / (kernel_ms * 1e-3)) / (PEAK_HBM_GBS * 1e9)},
+                     "hbm_frac_algorithmic": (B * B_STEP * a.steps / (kernel_ms * 1e-3)) / (PEAK_HBM_GBS * 1e9),
+                     "valu_issue": None if a.dense or launches != 1 else valu_issue(workload, per_launch_ms, a.steps)},
         "ensemble": {"nees_mean_pos_ori_vel": float(stats[-1] / (B * world))},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -92,7 +92,7 @@ UWVK_DEV void unpack(int e, int& i, int& j) {
 UWVK_DEV int olane() {
   int l = (int)threadIdx.x;
   asm volatile("" : "+v"(l));
-  return l;
+  return l;  // (restoring the range with l & 63 measured 1% slower)
 }
 
 // ---------------------------------------------------------------------------

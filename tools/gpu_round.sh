@@ -17,4 +17,5 @@ cat "$OUT/bench_dense.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps $SP --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1 || { tail -30 "$OUT/prof.log"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps $SP --warmup 2 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1 || { tail -30 "$OUT/pmc_fetch.log"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps $SP --warmup 2 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1 || { tail -30 "$OUT/pmc_write.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VALU_FMA_F64 SQ_WAVES --output-format csv -d "$OUT/pmc_sq" -o run -- python3 bench.py --steps $SP --warmup 2 --no-cpu-baseline > "$OUT/pmc_sq.log" 2>&1 || { tail -30 "$OUT/pmc_sq.log"; exit 1; }
 find "$OUT" -name "*.csv" | head -20
