@@ -517,8 +517,10 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     }
     return UWVK_OK;
   }
-  // PSP: one launch per run of epochs without BodyEfforts; efforts epochs
-  // go through the literal fused kernel (same HBM state layout)
+  // PSP: one launch per run of epochs up to and including the next BodyEfforts
+  // epoch (its predict and other updates); that epoch's efforts update alone
+  // then goes through the literal kernel (same HBM state layout).  Efforts is
+  // the last update of an epoch (the fused literal order), so the split is exact.
   std::vector<uint32_t> fl;
   const uint32_t* hf = log->host_flags ? log->host_flags + first : nullptr;
   if (!hf && count > 0) {
@@ -532,18 +534,19 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   while (e < first + count) {
     int64_t r = e;
     while (r < first + count && !(hf[r - first] & UWVK_EV_EFFORTS)) r++;
-    if (r > e) {
-      ea.first = e;
-      ea.count = r - e;
-      HIPCHK(launch_psp_epoch(h->dof, h->stream, b, sh, ea));
-    }
+    const int64_t last = r < first + count ? r + 1 : r;
+    ea.first = e;
+    ea.count = last - e;
+    ea.efforts_only = 0;
+    HIPCHK(launch_psp_epoch(h->dof, h->stream, b, sh, ea));
     if (r < first + count) {
       ea.first = r;
       ea.count = 1;
+      ea.efforts_only = 1;
       HIPCHK(launch_pose_epoch(h->dof, h->stream, b, sh, ea));
-      r++;
+      ea.efforts_only = 0;
     }
-    e = r;
+    e = last;
   }
   return UWVK_OK;
 }

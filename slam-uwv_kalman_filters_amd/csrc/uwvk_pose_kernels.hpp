@@ -43,6 +43,9 @@ struct EpochArgs {
   double dt;
   int64_t first, count;
   uint32_t* accept_counts;  // [batch][4] nullable
+  // literal epoch kernel only: run just the BodyEfforts update of each epoch
+  // (the PSP launch before it has done the epoch's predict and other updates)
+  int efforts_only;
 };
 
 // host-callable launchers (grid = one workgroup per instance)
@@ -250,13 +253,15 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_epoch(PoseBufs b, PoseShar
   pc.off = b.off + i * 28;
   for (int64_t e = ea.first; e < ea.first + ea.count; e++) {
     const uint32_t fl = ea.flags[e];
+    bool sok = true;
+    if (!ea.efforts_only) {
     const double* g = ea.gyro + (e * B + i) * 3;
     if (all_finite(g, 3)) {  // integrateMeasurement(RotationRate): checkMeasurment, then store
       for (int k = 0; k < 3; k++) { w[k] = g[k]; pc.w[k] = g[k]; }
     } else {
       nan = true;
     }
-    bool sok = pose_predict<DOF>(sm, sh, pc, b.Q, st);
+    sok = pose_predict<DOF>(sm, sh, pc, b.Q, st);
     ok = ok && sok;
     if (fl & UWVK_EV_ACC) {
       const double* z = ea.acc + (e * B + i) * 3;
@@ -296,6 +301,7 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_epoch(PoseBufs b, PoseShar
         ok = ok && sok;
       }
     }
+    }  // !efforts_only
     if (fl & UWVK_EV_EFFORTS) {
       MeasArgs me = ma;
       me.only_vel = (fl & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0;
