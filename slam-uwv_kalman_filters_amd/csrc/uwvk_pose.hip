@@ -27,6 +27,9 @@ using namespace uwvk;
 // ===========================================================================
 // host side
 // ===========================================================================
+// ensemble statistics per instance group: 3 store + 1 doubles (store <= 54)
+constexpr int64_t kStatsMaxOut = 3 * 54 + 1;
+
 struct uwvk_pose {
   int64_t batch = 0;
   int dof = 53, store = 54, device = 0;
@@ -37,7 +40,7 @@ struct uwvk_pose {
   double* d_meas = nullptr;  // staging: batch*36 (mu) + batch*36 (cov) + batch*2 (extra)
   uint8_t* d_mask = nullptr;
   uint8_t* d_accepted = nullptr;
-  double* d_scratch = nullptr;  // ensemble stats / rotation rate outputs
+  double* d_scratch = nullptr;  // [0, 256): stats out + truth; [0, 3 batch): rotation rate; then stats partials
   PoseShared* d_shared = nullptr;  // device copy of sh for the PSP kernels
   double* d_Qp = nullptr;          // {A_ii A_jj, dt^2 Q_ij} per packed entry (PSP)
   double* d_qband = nullptr;       // [128] dt^2 Q band of rows >= 9 (PSP)
@@ -193,7 +196,7 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
             hipMalloc(&h->d_off, B * 28 * 8) == hipSuccess && hipMalloc(&h->d_model, B * 27 * 8) == hipSuccess &&
             hipMalloc(&h->d_uwv, 108 * 8) == hipSuccess && hipMalloc(&h->d_status, B * 4) == hipSuccess &&
             hipMalloc(&h->d_meas, B * 74 * 8) == hipSuccess && hipMalloc(&h->d_mask, B) == hipSuccess &&
-            hipMalloc(&h->d_accepted, B) == hipSuccess && hipMalloc(&h->d_scratch, (B * 3 + 256) * 8) == hipSuccess &&
+            hipMalloc(&h->d_accepted, B) == hipSuccess && hipMalloc(&h->d_scratch, (B * 3 + 256 + ((B + 63) / 64) * kStatsMaxOut) * 8) == hipSuccess &&
             hipMalloc(&h->d_shared, sizeof(PoseShared)) == hipSuccess &&
             hipMalloc(&h->d_Qp, n * (n + 1) * 8) == hipSuccess && hipMalloc(&h->d_qband, 128 * 8) == hipSuccess &&
             hipEventCreate(&h->ev0) == hipSuccess && hipEventCreate(&h->ev1) == hipSuccess;
@@ -564,12 +567,11 @@ uwvk_status uwvk_pose_ensemble_allreduce(uwvk_pose* h, const double* truth, doub
   std::vector<double> t(s, 0.0);
   if (truth) std::memcpy(t.data(), truth, s * 8);
   else t[3] = 1.0;
-  HIPCHK(hipMemsetAsync(d_out, 0, nout * 8, h->stream));
+  // ensemble partials after the rotation-rate area: d_scratch + 256 + 3 batch
+  double* d_part = h->d_scratch + 256 + 3 * h->batch;
   HIPCHK(hipMemcpyAsync(d_truth, t.data(), s * 8, hipMemcpyHostToDevice, h->stream));
   PoseBufs b = bufs(h);
-  const unsigned nb = (unsigned)((h->batch + 63) / 64);
-  (void)nb;
-  HIPCHK(launch_pose_stats(h->dof, h->stream, b, d_truth, d_out));
+  HIPCHK(launch_pose_stats(h->dof, h->stream, b, d_truth, d_out, d_part));
   if (comm) {  // RCCL sum across the ranks' shards, stream-ordered after the stats kernel
     const uwvk_status st = uwvk_comm_allreduce_sum_device(comm, d_out, nout, (void*)h->stream);
     if (st != UWVK_OK) return st;

@@ -20,12 +20,17 @@ hipError_t launch_pose_rotation_rate(int dof, hipStream_t st, const PoseBufs& b,
   return hipGetLastError();
 }
 
-hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const double* truth, double* out) {
-  const unsigned nb = (unsigned)((b.batch + 63) / 64);
-  if (dof == 53)
-    hipLaunchKernelGGL(k_pose_stats<53>, dim3(nb), dim3(64), 0, st, b, truth, out);
-  else
-    hipLaunchKernelGGL(k_pose_stats<26>, dim3(nb), dim3(64), 0, st, b, truth, out);
+hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const double* truth, double* out,
+                             double* part) {
+  const int64_t nb = (b.batch + 63) / 64;
+  const int nout = 3 * (dof == 53 ? Lay<53>::store : Lay<26>::store) + 1;
+  if (dof == 53) {
+    hipLaunchKernelGGL(k_pose_stats<53>, dim3((unsigned)nb), dim3(64), 0, st, b, truth, part);
+    hipLaunchKernelGGL(k_pose_stats_sum<53>, dim3(nout), dim3(256), 0, st, (const double*)part, nb, nout, out);
+  } else {
+    hipLaunchKernelGGL(k_pose_stats<26>, dim3((unsigned)nb), dim3(64), 0, st, b, truth, part);
+    hipLaunchKernelGGL(k_pose_stats_sum<26>, dim3(nout), dim3(256), 0, st, (const double*)part, nb, nout, out);
+  }
   return hipGetLastError();
 }
 

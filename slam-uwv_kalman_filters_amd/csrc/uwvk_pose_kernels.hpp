@@ -54,7 +54,9 @@ hipError_t launch_pose_update(int dof, int kind, hipStream_t st, const PoseBufs&
                               const MeasArgs& ma, int m);
 hipError_t launch_pose_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea);
 hipError_t launch_pose_rotation_rate(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double* out);
-hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const double* truth, double* out);
+// part: ceil(batch / 64) x (3 store + 1) doubles of device scratch
+hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const double* truth, double* out,
+                             double* part);
 
 #ifdef UWVK_POSE_KERNEL_BODIES
 
@@ -340,27 +342,37 @@ __global__ __launch_bounds__(64) void k_pose_rotation_rate(PoseBufs b, PoseShare
 }
 
 // ensemble statistics: one block per 64 instances, atomics into out
+// Ensemble statistics, deterministic two-stage reduction (no atomics): one wave
+// per 64 instances writes its partial sums (butterfly shuffles, the same value
+// in every lane), then k_pose_stats_sum adds the partials in a fixed order.
+// Layout of out (nout = 3 store + 1): sum mu, sum mu^2, sum err^2 (orientation
+// slots 3..5 hold the squared SO3 log error, slot 6 is 0), NEES over
+// (position, orientation, velocity).
 template <int DOF>
-__global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, const double* truth, double* out) {
+__global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, const double* truth, double* part) {
   using L = Lay<DOF>;
+  constexpr int S = L::store, NOUT = 3 * S + 1;
   const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (i >= b.batch) return;
-  const double* x = b.mu + i * L::store;
-  const double* P = b.sigma + i * (int64_t)(DOF * DOF);
-  double err[9];
-  for (int s = 0; s < L::store; s++) {
-    atomicAdd(&out[s], x[s]);
-    atomicAdd(&out[L::store + s], x[s] * x[s]);
-  }
-  for (int s = 0; s < L::store; s++) {
-    double e = x[s] - truth[s];
-    if (s >= 3 && s < 7) continue;
-    atomicAdd(&out[2 * L::store + s], e * e);
-  }
+  const bool live = i < b.batch;
+  const double* x = b.mu + (live ? i : 0) * S;
+  const double* P = b.sigma + (live ? i : 0) * (int64_t)(DOF * DOF);
+  double* o = part + (int64_t)blockIdx.x * NOUT;
+  auto put = [&](int slot, double v) {
+    v = live ? v : 0.0;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    if (threadIdx.x == 0) o[slot] = v;
+  };
   double r[3];
   qboxminus(x + 3, truth + 3, r);
-  for (int k = 0; k < 3; k++) atomicAdd(&out[2 * L::store + 3 + k], r[k] * r[k]);
+  for (int s = 0; s < S; s++) {
+    const double xs = x[s], e = xs - truth[s];
+    put(s, xs);
+    put(S + s, xs * xs);
+    put(2 * S + s, (s >= 3 && s < 6) ? r[s - 3] * r[s - 3] : (s == 6 ? 0.0 : e * e));
+  }
   // NEES over (position, orientation, velocity): e^T P_sub^-1 e via a 9x9 Cholesky solve
+  double err[9];
   for (int k = 0; k < 3; k++) { err[k] = x[k] - truth[k]; err[3 + k] = r[k]; err[6 + k] = x[7 + k] - truth[7 + k]; }
   double A[81];
   for (int a = 0; a < 9; a++)
@@ -379,7 +391,24 @@ __global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, const double* tru
     y[a] = s / A[a * 9 + a];
     nees += y[a] * y[a];
   }
-  atomicAdd(&out[3 * L::store], nees);
+  put(3 * S, nees);
+}
+
+// out[s] = sum over the nblk partial rows, block s: thread t takes rows t, t + 256, ...
+// then a fixed LDS tree; the result does not depend on timing
+template <int DOF>
+__global__ __launch_bounds__(256) void k_pose_stats_sum(const double* part, int64_t nblk, int nout, double* out) {
+  __shared__ double red[256];
+  const int s = blockIdx.x, t = threadIdx.x;
+  double acc = 0.0;
+  for (int64_t k = t; k < nblk; k += 256) acc += part[k * nout + s];
+  red[t] = acc;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  if (t == 0) out[s] = red[0];
 }
 
 

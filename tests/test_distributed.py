@@ -86,6 +86,25 @@ def test_ensemble_stats_kernel_matches_host():
     x, P = f.get_state()
     np.testing.assert_allclose(f.ensemble_stats(truth), ensemble.ensemble_stats_host(x, P, truth), rtol=1e-9,
                                atol=1e-12)
+    # fixed-order two-stage reduction: repeated calls agree bitwise
+    np.testing.assert_array_equal(f.ensemble_stats(truth), f.ensemble_stats(truth))
+
+
+@pytest.mark.gpu
+def test_ensemble_stats_many_partials():
+    """Batch 20,000: 313 wave partials (more than the 256 threads of the final
+    sum), ragged last wave; host reference and bitwise repeatability."""
+    sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+    from uwvk import engine, ensemble, synth
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(20000, 2, "C3")
+    f = engine.PoseUKFBatch(20000)
+    f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    truth = log["truth"].state(0)
+    x, P = f.get_state()
+    got = f.ensemble_stats(truth)
+    np.testing.assert_allclose(got, ensemble.ensemble_stats_host(x, P, truth), rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(got, f.ensemble_stats(truth))
 
 
 @pytest.mark.gpu
