@@ -295,9 +295,11 @@ def main():
                      "executed_tflops": exec_tf, "executed_frac": exec_tf / PEAK_FP64_TFLOPS,
                      "hbm_frac_algorithmic": (B * B_STEP * a.steps / (kernel_ms * 1e-3)) / (PEAK_HBM_GBS * 1e9),
                      "valu_issue": None if a.dense or launches != 1 else valu_issue(workload, per_launch_ms, a.steps),
-                     "note": ("achieved/frac count the reference algorithm's flops (SURVEY 8(d), 1,554,084 per step); "
-                              "the %s path executes executed_flop_per_step (executed_frac); its binding roof is "
-                              "VALU issue (valu_issue.frac, DESIGN.md section 6)" % ("literal" if a.dense else "PSP"))},
+                     "note": "achieved/frac count the reference algorithm's flops (SURVEY 8(d), 1,554,084 per step); "
+                             + ("the literal path executes executed_flop_per_step; MFMA busy 16%, the serial "
+                                "Cholesky/LDS chain binds (profiles/r01/pmc_mfma_dense_r01s.txt)" if a.dense else
+                                "the PSP path executes executed_flop_per_step (executed_frac); its binding roof is "
+                                "VALU issue (valu_issue.frac, DESIGN.md section 6)")},
         "ensemble": {"nees_mean_pos_ori_vel": float(stats[-1] / (B * world))},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
