@@ -522,7 +522,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   }
   // PSP: one launch per run of epochs up to and including the next BodyEfforts
   // epoch (its predict and other updates); that epoch's efforts update alone
-  // then goes through the literal kernel (same HBM state layout).  Efforts is
+  // then goes through the literal efforts kernel (same HBM state layout).  Efforts is
   // the last update of an epoch (the fused literal order), so the split is exact.
   std::vector<uint32_t> fl;
   const uint32_t* hf = log->host_flags ? log->host_flags + first : nullptr;
@@ -545,9 +545,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     if (r < first + count) {
       ea.first = r;
       ea.count = 1;
-      ea.efforts_only = 1;
-      HIPCHK(launch_pose_epoch(h->dof, h->stream, b, sh, ea));
-      ea.efforts_only = 0;
+      HIPCHK(launch_pose_efforts_epoch(h->dof, h->stream, b, sh, ea));
     }
     e = last;
   }

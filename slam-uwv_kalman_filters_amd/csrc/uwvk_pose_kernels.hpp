@@ -53,6 +53,8 @@ hipError_t launch_pose_predict(int dof, hipStream_t st, const PoseBufs& b, const
 hipError_t launch_pose_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                               const MeasArgs& ma, int m);
 hipError_t launch_pose_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea);
+hipError_t launch_pose_efforts_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                                     const EpochArgs& ea);
 hipError_t launch_pose_rotation_rate(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double* out);
 // part: ceil(batch / 64) x (3 store + 1) doubles of device scratch
 hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const double* truth, double* out,
@@ -227,6 +229,35 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_update(PoseBufs b, PoseSha
   if (tid() == 0) {
     if (!ok) b.status[i] |= UWVK_ST_NOTPD;
     if (ma.accepted) ma.accepted[i] = acc ? 1 : 0;
+  }
+  store_instance<DOF>(sm, b, i);
+}
+
+// The BodyEfforts update of epoch ea.first alone (run_log's PSP split: the PSP
+// launch has done that epoch's predict and other updates).  Same effect as
+// k_pose_epoch with efforts_only, but only this update is instantiated, so the
+// kernel has the single-update register footprint instead of the fused
+// kernel's (576 B/lane scratch, VGPR spills).
+template <int DOF>
+__global__ __launch_bounds__(Geo<DOF>::T) void k_pose_efforts_epoch(PoseBufs b, PoseShared sh, EpochArgs ea) {
+  __shared__ Smem<DOF> sm;
+  const int64_t B = b.batch, i = xcd_instance(B), e = ea.first;
+  const uint32_t fl = ea.flags[e];
+  if (!(fl & UWVK_EV_EFFORTS)) return;
+  load_instance<DOF>(sm, b, i);
+  MeasArgs me{};
+  me.only_vel = (fl & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0;
+  me.v3[0] = ea.p_sens[0]; me.v3[1] = ea.p_sens[1]; me.v3[2] = ea.p_sens[2];
+  double w[3] = {b.rot[i * 3], b.rot[i * 3 + 1], b.rot[i * 3 + 2]};
+  const double* z = ea.efforts + ((int64_t)ea.e_index[e] * B + i) * 6;
+  bool sok = true, nan = false;
+  uint32_t acc = 0;
+  if (all_finite(z, 6)) acc = do_update<DOF, MK_EFFORTS>(sm, sh, b, i, z, ea.e_cov, me, w, &sok) ? 1u : 0u;
+  else nan = true;
+  if (tid() == 0) {
+    if (!sok) b.status[i] |= UWVK_ST_NOTPD;
+    if (nan) b.status[i] |= UWVK_ST_NAN;
+    if (ea.accept_counts) ea.accept_counts[i * 4 + 3] += acc;
   }
   store_instance<DOF>(sm, b, i);
 }
