@@ -238,8 +238,13 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_update(PoseBufs b, PoseSha
 // k_pose_epoch with efforts_only, but only this update is instantiated, so the
 // kernel has the single-update register footprint instead of the fused
 // kernel's (576 B/lane scratch, VGPR spills).
+// 2 waves/SIMD (4 instances per CU, LDS-bound) at the price of 688 B/lane of
+// scratch spills: 6.41 -> 4.10 ms per update at batch 65,536 (C4 134.4 -> 136.6M)
+#ifndef UWVK_EFF_ATTR
+#define UWVK_EFF_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
+#endif
 template <int DOF>
-__global__ __launch_bounds__(Geo<DOF>::T) void k_pose_efforts_epoch(PoseBufs b, PoseShared sh, EpochArgs ea) {
+__global__ __launch_bounds__(Geo<DOF>::T) UWVK_EFF_ATTR void k_pose_efforts_epoch(PoseBufs b, PoseShared sh, EpochArgs ea) {
   __shared__ Smem<DOF> sm;
   const int64_t B = b.batch, i = xcd_instance(B), e = ea.first;
   const uint32_t fl = ea.flags[e];
