@@ -205,8 +205,13 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_predict(PoseBufs b, PoseSh
   store_instance<DOF>(sm, b, i);
 }
 
+// single-call literal updates at 2 waves/SIMD (scratch spills accepted), batch
+// 65,536, tools/time_single_update.py: efforts 7.0 -> 5.3 ms, dense acceleration 5.2 -> 3.2 ms
+#ifndef UWVK_UPD_ATTR
+#define UWVK_UPD_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
+#endif
 template <int DOF, int K>
-__global__ __launch_bounds__(Geo<DOF>::T) void k_pose_update(PoseBufs b, PoseShared sh, MeasArgs ma, int m) {
+__global__ __launch_bounds__(Geo<DOF>::T) UWVK_UPD_ATTR void k_pose_update(PoseBufs b, PoseShared sh, MeasArgs ma, int m) {
   __shared__ Smem<DOF> sm;
   const int64_t i = xcd_instance(b.batch);
   if (ma.mask && !ma.mask[i]) {
