@@ -322,12 +322,13 @@ uwvk_status uwvk_pose_predict(uwvk_pose* h, double dt) {
   if (!h) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   PoseBufs b = bufs(h);
-  PoseShared sh = h->sh;
   if (use_dense(h))
-    HIPCHK(launch_pose_predict(h->dof, h->stream, b, sh, dt));
+    HIPCHK(launch_pose_predict(h->dof, h->stream, b, h->sh, dt));
   else {
+    // upload_shared recomputes the Q shape (q_bw, q_simple, qlo, qoff) for this dt:
+    // the by-value PoseShared handed to the kernel must be taken after it
     HIPCHK(upload_shared(h, dt));
-    b = bufs(h);
+    const PoseShared sh = h->sh;
     HIPCHK(launch_psp_predict(h->dof, h->stream, b, sh, dt));
   }
   return UWVK_OK;
@@ -373,11 +374,11 @@ static uwvk_status launch_update(uwvk_pose* h, int m, const double* mu, const do
   ma.only_vel = only_vel;
   ma.accepted = h->d_accepted;
   PoseBufs b = bufs(h);
-  PoseShared sh = h->sh;
   if (K == MK_EFFORTS || use_dense(h))
-    HIPCHK(launch_pose_update(h->dof, K, h->stream, b, sh, ma, m));
+    HIPCHK(launch_pose_update(h->dof, K, h->stream, b, h->sh, ma, m));
   else {
     HIPCHK(upload_shared(h, h->qp_dt));
+    const PoseShared sh = h->sh;  // after upload_shared (it refreshes the Q shape)
     HIPCHK(launch_psp_update(h->dof, K, h->stream, b, sh, ma, m));
   }
   if (accepted) HIPCHK(hipMemcpyAsync(accepted, h->d_accepted, (size_t)B, hipMemcpyDeviceToHost, h->stream));
@@ -511,12 +512,11 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   ea.dt = log->dt;
   ea.accept_counts = accept_counts;
   PoseBufs b = bufs(h);
-  PoseShared sh = h->sh;
   if (use_dense(h)) {  // literal kernels: one fused launch per epoch
     for (int64_t e = first; e < first + count; e++) {
       ea.first = e;
       ea.count = 1;
-      HIPCHK(launch_pose_epoch(h->dof, h->stream, b, sh, ea));
+      HIPCHK(launch_pose_epoch(h->dof, h->stream, b, h->sh, ea));
     }
     return UWVK_OK;
   }
@@ -533,6 +533,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     hf = fl.data();
   }
   HIPCHK(upload_shared(h, log->dt));
+  const PoseShared sh = h->sh;  // after upload_shared (it refreshes the Q shape)
   int64_t e = first;
   while (e < first + count) {
     int64_t r = e;
