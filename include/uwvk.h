@@ -485,20 +485,20 @@ typedef struct uwvk_bottom uwvk_bottom;
 uwvk_status uwvk_bottom_create(int64_t batch, int device, uwvk_bottom** out);
 void uwvk_bottom_destroy(uwvk_bottom* h);
 void* uwvk_bottom_stream(const uwvk_bottom* h);
-/* BottomUKF(initial_state, state_cov) (BottomUKF.cpp:43-49): x batch*4 (normal
+/* BottomUKF(initial_state, state_cov) (BottomUKF.cpp:40-46): x batch*4 (normal
  * normalised here, as MTK::S2 does), P batch*9; process noise = identity. */
 uwvk_status uwvk_bottom_init(uwvk_bottom* h, const double* x, const double* P);
 /* setProcessNoiseCovariance [EXT base]: 3x3, shared by the batch */
 uwvk_status uwvk_bottom_set_process_noise(uwvk_bottom* h, const double Q[9]);
 /* setVelocity (BottomUKF.cpp:69-72): batch*3 */
 uwvk_status uwvk_bottom_set_velocity(uwvk_bottom* h, const double* velocity);
-/* predictionStep -> predictionStepImpl (BottomUKF.cpp:51-57) */
+/* predictionStep -> predictionStepImpl (BottomUKF.cpp:48-54) */
 uwvk_status uwvk_bottom_predict(uwvk_bottom* h, double dt);
-/* integrateMeasurement(RangeMeasurement, unit_direction, origin) (BottomUKF.cpp:59-64):
+/* integrateMeasurement(RangeMeasurement, unit_direction, origin) (BottomUKF.cpp:56-61):
  * mu batch, cov batch (NULL = shared_cov); beam direction / origin shared. */
 uwvk_status uwvk_bottom_update_range(uwvk_bottom* h, const double* mu, const double* cov, double shared_cov,
                                      const double unit_direction[3], const double origin[3], const uint8_t* mask);
-/* integrateMeasurement(NormalType, cov) (BottomUKF.cpp:66-70): mu batch*3 (normalised),
+/* integrateMeasurement(NormalType, cov) (BottomUKF.cpp:63-67): mu batch*3 (normalised),
  * cov batch*4 (NULL = shared_cov[4]) */
 uwvk_status uwvk_bottom_update_normal(uwvk_bottom* h, const double* mu, const double* cov, const double* shared_cov,
                                       const uint8_t* mask);
@@ -515,21 +515,21 @@ uwvk_status uwvk_ipose_create(int64_t batch, int device, uwvk_ipose** out);
 void uwvk_ipose_destroy(uwvk_ipose* h);
 void* uwvk_ipose_stream(const uwvk_ipose* h);
 /* IndirectPoseUKF(position_error_std, orientation_error_std, orientation_error_tau,
- * initial_position_error, initial_position_error_std) (IndirectPoseUKF.cpp:66-91):
+ * initial_position_error, initial_position_error_std) (IndirectPoseUKF.cpp:53-78):
  * stds shared; initial_position_error batch*3 (NULL = zero); initial std NULL = ones. */
 uwvk_status uwvk_ipose_init(uwvk_ipose* h, const double position_error_std[3], const double orientation_error_std[3],
                             double orientation_error_tau, const double* initial_position_error,
                             const double initial_position_error_std[3]);
 /* setProcessNoiseCovariance [EXT pose_estimation base]: 6x6, shared by the
  * batch (uwvk_ipose_init sets diag(position_error_std^2, orientation_error_std^2),
- * IndirectPoseUKF.cpp:76-80); predict shapes it as predictionStepImpl (:93-106). */
+ * IndirectPoseUKF.cpp:72-77); predict shapes it as predictionStepImpl (:80-92). */
 uwvk_status uwvk_ipose_set_process_noise(uwvk_ipose* h, const double Q[36]);
 /* updatePoseReference (IndirectPoseUKF.cpp:144-147): batch*7 body in world, t(3) q(4) */
 uwvk_status uwvk_ipose_set_pose_reference(uwvk_ipose* h, const double* pose);
-/* predictionStep -> predictionStepImpl (IndirectPoseUKF.cpp:93-106) */
+/* predictionStep -> predictionStepImpl (IndirectPoseUKF.cpp:80-92) */
 uwvk_status uwvk_ipose_predict(uwvk_ipose* h, double dt);
 /* integrateMeasurement(marker_features, feature_positions, marker_pose, cov_marker_pose,
- * camera_config, camera_in_body) (IndirectPoseUKF.cpp:108-140); arrays as for
+ * camera_config, camera_in_body) (IndirectPoseUKF.cpp:94-135); arrays as for
  * uwvk_pose_update_visual_landmark. */
 uwvk_status uwvk_ipose_update_visual(uwvk_ipose* h, int32_t n_features, const double* features,
                                      const double* feature_cov, int feature_cov_per_instance,

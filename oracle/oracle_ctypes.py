@@ -38,6 +38,20 @@ def lib():
     return _LIB
 
 
+class so3_right:
+    """Context manager: run the oracle with the body-frame (right) SO3 [+]
+    instead of the default nav-frame (left) one."""
+
+    def __enter__(self):
+        self.prev = lib().or_get_so3_right()
+        lib().or_set_so3_right(1)
+        return self
+
+    def __exit__(self, *exc):
+        lib().or_set_so3_right(self.prev)
+        return False
+
+
 def dp(a):
     if a is None:
         return None

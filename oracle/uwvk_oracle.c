@@ -108,7 +108,28 @@ void or_so3_log(const double q[4], double o[3]) {
   o[0] = k * x; o[1] = k * y; o[2] = k * z;
 }
 
-/* compound-manifold boxplus: vect x + s*d; SO3 (nav-frame/left) exp(s*d) * q */
+/* SO3 boxplus side [EXT MTK], SURVEY §8(c) item 5: the largest unpinned semantic.
+ * 0 (default): nav-frame / left, q [+] d = exp(d) * q, the convention the reference's
+ *   usage implies (omega rotated into nav, PoseUKF.cpp:31-32; Q_o rotated by R, :451);
+ * 1: body-frame / right, q [+] d = q * exp(d), classic MTK SO3::boxplus.
+ * Applies to every PoseUKF orientation [+]/[-], including processModel's
+ * new_state.orientation.boxplus (PoseUKF.cpp:32).  The HIP engine implements the
+ * default only; the switch exists so the pin can be applied once the semantics
+ * of the real MTK binary are known (tests/test_oracle_kat.py shows the two
+ * conventions give materially different C3 trajectories). */
+static int g_so3_right = 0;
+void or_set_so3_right(int on) { g_so3_right = on ? 1 : 0; }
+int or_get_so3_right(void) { return g_so3_right; }
+
+/* q [+] v for an already scaled rotation vector v */
+static void so3_plus(const double q[4], const double v[3], double o[4]) {
+  double e[4];
+  or_so3_exp(v, e);
+  if (g_so3_right) or_quat_mul(q, e, o);
+  else or_quat_mul(e, q, o);
+}
+
+/* compound-manifold boxplus: vect x + s*d; SO3 exp(s*d) * q (left) or q * exp(s*d) (right) */
 void or_boxplus(const or_layout* L, const double* x, const double* d, double s, double* o) {
   double tmp[OR_MAXS];
   for (int k = 0; k < L->dof; k++) {
@@ -116,13 +137,12 @@ void or_boxplus(const or_layout* L, const double* x, const double* d, double s, 
     int si = dof_to_store(k);
     tmp[si] = x[si] + s * d[k];
   }
-  double v[3] = {s * d[3], s * d[4], s * d[5]}, e[4];
-  or_so3_exp(v, e);
-  or_quat_mul(e, x + 3, tmp + 3);
+  double v[3] = {s * d[3], s * d[4], s * d[5]};
+  so3_plus(x + 3, v, tmp + 3);
   memcpy(o, tmp, sizeof(double) * L->store);
 }
 
-/* a boxminus b: vect a - b; SO3 log(a * b^-1) */
+/* a boxminus b: vect a - b; SO3 log(a * b^-1) (left) or log(b^-1 * a) (right) */
 void or_boxminus(const or_layout* L, const double* a, const double* b, double* o) {
   for (int k = 0; k < L->dof; k++) {
     if (k >= 3 && k < 6) continue;
@@ -130,7 +150,8 @@ void or_boxminus(const or_layout* L, const double* a, const double* b, double* o
     o[k] = a[si] - b[si];
   }
   double bc[4] = {b[3], -b[4], -b[5], -b[6]}, r[4];
-  or_quat_mul(a + 3, bc, r);
+  if (g_so3_right) or_quat_mul(bc, a + 3, r);
+  else or_quat_mul(a + 3, bc, r);
   or_so3_log(r, o + 3);
 }
 
@@ -715,9 +736,7 @@ static void pose_process(void* ctx, const double* x, double* o) {
   for (int i = 0; i < 3; i++) wb[i] = f->rotation_rate[i] - x[L->s_bg + i];
   or_quat_rotate(x + L->s_quat, wb, wn);
   for (int i = 0; i < 3; i++) wn[i] = (wn[i] - er[i]) * dt;
-  double e[4];
-  or_so3_exp(wn, e);
-  or_quat_mul(e, x + L->s_quat, s + L->s_quat);
+  so3_plus(x + L->s_quat, wn, s + L->s_quat); /* new_state.orientation.boxplus(w, dt), :32 */
   for (int i = 0; i < 3; i++) s[L->s_vel + i] = x[L->s_vel + i] + dt * x[L->s_acc + i];
   for (int i = 0; i < 3; i++) {
     double dg = (-1.0 / P->gyro_bias_tau) * (x[L->s_bg + i] - P->gyro_bias_offset[i]);

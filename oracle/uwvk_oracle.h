@@ -68,6 +68,10 @@ void or_calc_efforts(const uwvk_uwv_params* p, const double acc6[6], const doubl
                      double tau[6]);
 void or_boxplus(const or_layout* L, const double* x, const double* delta, double scale, double* out);
 void or_boxminus(const or_layout* L, const double* a, const double* b, double* out);
+/* SO3 [+] side, process-wide: 0 = nav-frame/left (default,
+ * what the HIP engine implements), 1 = body-frame/right (classic MTK). */
+void or_set_so3_right(int on);
+int or_get_so3_right(void);
 
 /* ---- PoseUKF ------------------------------------------------------------ */
 int or_pose_init_from_config(or_pose* f, int dof, const double pos[3], const double pos_cov[9], const double rot[4],

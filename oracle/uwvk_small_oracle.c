@@ -275,7 +275,7 @@ static sm_manifold bottom_manifold(void) {
   return M;
 }
 
-/* BottomUKF(initial_state, state_cov), BottomUKF.cpp:43-49: x = {d, n(3)} */
+/* BottomUKF(initial_state, state_cov), BottomUKF.cpp:40-46: x = {d, n(3)} */
 void or_bottom_init(or_bottom* f, const double x[4], const double P[9]) {
   f->mu[0] = x[0];
   or_s2_from_vector(x + 1, f->mu + 1);
@@ -300,7 +300,7 @@ static void bottom_process(void* ctx, const double* x, double* o) {
   memcpy(o, tmp, sizeof(tmp));
 }
 
-/* predictionStepImpl, BottomUKF.cpp:51-57 */
+/* predictionStepImpl, BottomUKF.cpp:48-54 */
 int or_bottom_predict(or_bottom* f, double dt) {
   sm_manifold M = bottom_manifold();
   double vxy2 = f->velocity[0] * f->velocity[0] + f->velocity[1] * f->velocity[1];
@@ -314,7 +314,7 @@ typedef struct range_ctx {
   double dir[3], origin[3];
 } range_ctx;
 
-/* measurementDistance, BottomUKF.cpp:18-31 */
+/* measurementDistance, BottomUKF.cpp:18-30 */
 static void h_range(void* c, const double* x, double* z) {
   const range_ctx* r = (const range_ctx*)c;
   double bottom[3] = {0.0, 0.0, -x[0]};
@@ -329,7 +329,7 @@ static void h_range(void* c, const double* x, double* z) {
   }
 }
 
-/* integrateMeasurement(RangeMeasurement, unit_direction, origin), BottomUKF.cpp:59-64 */
+/* integrateMeasurement(RangeMeasurement, unit_direction, origin), BottomUKF.cpp:56-61 */
 int or_bottom_update_range(or_bottom* f, double mu, double cov, const double dir[3], const double origin[3]) {
   if (!isfinite(mu) || !isfinite(cov)) return UWVK_ENAN;
   sm_manifold M = bottom_manifold();
@@ -340,10 +340,10 @@ int or_bottom_update_range(or_bottom* f, double mu, double cov, const double dir
   return sm_update(&M, f->mu, f->sigma, Z_VECT_MANIFOLD, 1, &mu, h_range, &c, &cov, &acc);
 }
 
-/* measurementNormal, BottomUKF.cpp:33-38 */
+/* measurementNormal, BottomUKF.cpp:32-37 */
 static void h_normal(void* c, const double* x, double* z) { z[0] = x[1]; z[1] = x[2]; z[2] = x[3]; }
 
-/* integrateMeasurement(NormalType, cov), BottomUKF.cpp:66-70 (no NaN check there) */
+/* integrateMeasurement(NormalType, cov), BottomUKF.cpp:63-67 (no NaN check there) */
 int or_bottom_update_normal(or_bottom* f, const double mu[3], const double cov[4]) {
   sm_manifold M = bottom_manifold();
   double z[3];
@@ -359,14 +359,14 @@ static sm_manifold ipose_manifold(int with_marker) {
   sm_manifold M = {0};
   sm_add(&M, SEG_V, 3);  /* position_error, IndirectPoseUKF.hpp:20 */
   sm_add(&M, SEG_SO3, 3); /* orientation_error, :21 */
-  if (with_marker) {      /* FilterStateWithMarker, IndirectPoseUKF.cpp:24-28 */
+  if (with_marker) {      /* FilterStateWithMarker, IndirectPoseUKF.cpp:25-29 */
     sm_add(&M, SEG_V, 3);
     sm_add(&M, SEG_SO3, 3);
   }
   return M;
 }
 
-/* IndirectPoseUKF(...), IndirectPoseUKF.cpp:66-91 */
+/* IndirectPoseUKF(...), IndirectPoseUKF.cpp:53-78 */
 void or_ipose_init(or_ipose* f, const double pos_std[3], const double ori_std[3], double tau,
                    const double init_pos_err[3], const double init_pos_std[3]) {
   memset(f, 0, sizeof(*f));
@@ -385,7 +385,7 @@ void or_ipose_init(or_ipose* f, const double pos_std[3], const double ori_std[3]
 
 void or_ipose_set_pose_reference(or_ipose* f, const double pose[7]) { memcpy(f->pose_ref, pose, sizeof(f->pose_ref)); }
 
-/* processModel, IndirectPoseUKF.cpp:8-20 */
+/* processModel, IndirectPoseUKF.cpp:7-20 */
 static void ipose_process(void* ctx, const double* x, double* o) {
   const double* c = (const double*)ctx; /* {tau, dt} */
   double l[3], d[3], e[4], tmp[7];
@@ -397,7 +397,7 @@ static void ipose_process(void* ctx, const double* x, double* o) {
   memcpy(o, tmp, sizeof(tmp));
 }
 
-/* predictionStepImpl, IndirectPoseUKF.cpp:93-106 */
+/* predictionStepImpl, IndirectPoseUKF.cpp:80-92 */
 int or_ipose_predict(or_ipose* f, double dt) {
   sm_manifold M = ipose_manifold(0);
   double R[9], Qp[36], A[9], B[9];
@@ -435,7 +435,7 @@ typedef struct vis_ctx {
 
 static void qinv_rotate(const double q[4], const double v[3], double o[3]) { or_quat_rotate_inv(q, v, o); }
 
-/* measurementVisualLandmark, IndirectPoseUKF.cpp:36-48 / PoseUKF.cpp:231-244:
+/* measurementVisualLandmark, IndirectPoseUKF.cpp:38-50 / PoseUKF.cpp:231-244:
  * feature_in_cam = ((body_in_nav [* pose_error]) * cam_in_body)^-1 * (q_m f + t_m), as S2 */
 static void h_visual(void* c, const double* x, double* z) {
   const vis_ctx* v = (const vis_ctx*)c;
@@ -456,7 +456,7 @@ static void h_visual(void* c, const double* x, double* z) {
   or_s2_from_vector(fc, z);
 }
 
-/* the augmented update loop shared by IndirectPoseUKF.cpp:108-139 and PoseUKF.cpp:613-654 */
+/* the augmented update loop shared by IndirectPoseUKF.cpp:94-135 and PoseUKF.cpp:613-654 */
 static int visual_loop(const sm_manifold* A, double* amu, double* asig, vis_ctx* c, int nf, const double* features,
                        const double* feature_cov, const double* feature_pos, const double cam_cfg[4]) {
   double fx2 = pow(cam_cfg[0], 2.0), fy2 = pow(cam_cfg[1], 2.0), fxy = cam_cfg[0] * cam_cfg[1];
@@ -480,7 +480,7 @@ static int check_features(int nf, const double* features, const double* feature_
 }
 
 /* IndirectPoseUKF::integrateMeasurement(features, positions, marker_pose, cov, camera, cam_in_body),
- * IndirectPoseUKF.cpp:108-140.  marker_pose, cam_in_body: t(3), q(4). */
+ * IndirectPoseUKF.cpp:94-135.  marker_pose, cam_in_body: t(3), q(4). */
 int or_ipose_update_visual(or_ipose* f, int nf, const double* features, const double* feature_cov,
                            const double* feature_pos, const double marker_pose[7], const double cov_marker[36],
                            const double cam_cfg[4], const double cam_in_body[7]) {

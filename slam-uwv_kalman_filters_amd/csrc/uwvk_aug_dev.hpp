@@ -419,7 +419,7 @@ struct Engine {
 
 // ---------------------------------------------------------------------------
 // visual-landmark update shared by PoseUKF (PoseUKF.cpp:613-654) and
-// IndirectPoseUKF (IndirectPoseUKF.cpp:108-140)
+// IndirectPoseUKF (IndirectPoseUKF.cpp:94-135)
 // ---------------------------------------------------------------------------
 struct VisArgs {             // device pointers
   int nf;                    // features per instance (the same for the batch)
@@ -437,7 +437,7 @@ struct VisArgs {             // device pointers
 };
 
 // measurementVisualLandmark: ((body_in_nav [* pose_error]) * cam_in_body)^-1 *
-// (q_m f + t_m) as S2 (IndirectPoseUKF.cpp:36-48, PoseUKF.cpp:231-244).
+// (q_m f + t_m) as S2 (IndirectPoseUKF.cpp:38-50, PoseUKF.cpp:231-244).
 // SM: storage offset of marker_position; INDIRECT: state is the pose error.
 template <int SM, bool INDIRECT>
 struct VisualH {

@@ -22,7 +22,7 @@ namespace {
 
 using BottomM = Manifold<Seg<SEG_V, 1>, Seg<SEG_S2>>;                        // BottomUKF.hpp:18-21
 using IPoseM = Manifold<Seg<SEG_V, 3>, Seg<SEG_SO3>>;                        // IndirectPoseUKF.hpp:19-22
-using IPoseMarkerM = Manifold<Seg<SEG_V, 3>, Seg<SEG_SO3>, Seg<SEG_V, 3>, Seg<SEG_SO3>>;  // IndirectPoseUKF.cpp:24-28
+using IPoseMarkerM = Manifold<Seg<SEG_V, 3>, Seg<SEG_SO3>, Seg<SEG_V, 3>, Seg<SEG_SO3>>;  // IndirectPoseUKF.cpp:25-29
 using BE = Engine<BottomM>;
 using IE = Engine<IPoseM>;
 using IAE = Engine<IPoseMarkerM>;
@@ -67,7 +67,7 @@ __device__ E make_engine(double* smem, const SmallBufs& b, const uint8_t* mask, 
 }
 
 // ---- BottomUKF -----------------------------------------------------------
-// predictionStepImpl (BottomUKF.cpp:51-57) + processModel (:5-16)
+// predictionStepImpl (BottomUKF.cpp:48-54) + processModel (:5-16)
 __global__ __launch_bounds__(BE::BLOCK) void k_bottom_predict(SmallBufs b, const double* vel, M9 Q, double dt) {
   __shared__ double smem[BE::IPB * BE::words];
   int64_t inst;
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(BE::BLOCK) void k_bottom_predict(SmallBufs b, const
   store(e, b, inst, ok);
 }
 
-// measurementDistance (BottomUKF.cpp:18-31)
+// measurementDistance (BottomUKF.cpp:18-30)
 struct RangeH {
   double dir[3], origin[3];
   UWVK_DEV void operator()(const double* x, double* z) const {
@@ -98,7 +98,7 @@ struct RangeH {
   }
 };
 
-// integrateMeasurement(RangeMeasurement, unit_direction, origin) (BottomUKF.cpp:59-64):
+// integrateMeasurement(RangeMeasurement, unit_direction, origin) (BottomUKF.cpp:56-61):
 // DistanceType (mtkwrap<Scalar>) measurement -> iterative vect mean
 __global__ __launch_bounds__(BE::BLOCK) void k_bottom_range(SmallBufs b, const double* z, const double* cov,
                                                             double shared_cov, RangeH h, const uint8_t* mask) {
@@ -115,12 +115,12 @@ __global__ __launch_bounds__(BE::BLOCK) void k_bottom_range(SmallBufs b, const d
   store(e, b, inst, ok);
 }
 
-// measurementNormal (BottomUKF.cpp:33-38)
+// measurementNormal (BottomUKF.cpp:32-37)
 struct NormalH {
   UWVK_DEV void operator()(const double* x, double* z) const { z[0] = x[1]; z[1] = x[2]; z[2] = x[3]; }
 };
 
-// integrateMeasurement(NormalType, cov) (BottomUKF.cpp:66-70): S2 measurement
+// integrateMeasurement(NormalType, cov) (BottomUKF.cpp:63-67): S2 measurement
 __global__ __launch_bounds__(BE::BLOCK) void k_bottom_normal(SmallBufs b, const double* z, const double* cov,
                                                              M9 shared_cov, const uint8_t* mask) {
   __shared__ double smem[BE::IPB * BE::words];
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(BE::BLOCK) void k_bottom_normal(SmallBufs b, const 
 }
 
 // ---- IndirectPoseUKF -------------------------------------------------------
-// predictionStepImpl (IndirectPoseUKF.cpp:93-106) + processModel (:8-20)
+// predictionStepImpl (IndirectPoseUKF.cpp:80-92) + processModel (:7-20)
 __global__ __launch_bounds__(IE::BLOCK) void k_ipose_predict(SmallBufs b, M36 Q, double tau, double dt) {
   __shared__ double smem[IE::IPB * IE::words];
   int64_t inst;
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(IE::BLOCK) void k_ipose_predict(SmallBufs b, M36 Q,
   store(e, b, inst, ok);
 }
 
-// integrateMeasurement(marker features, ...) (IndirectPoseUKF.cpp:108-140):
+// integrateMeasurement(marker features, ...) (IndirectPoseUKF.cpp:94-135):
 // augment with the marker pose, one S2 update per feature, keep the filter block
 __global__ __launch_bounds__(IAE::BLOCK) void k_ipose_visual(SmallBufs b, VisArgs va) {
   __shared__ double smem[IAE::IPB * IAE::words];
@@ -318,7 +318,7 @@ uwvk_status uwvk_bottom_create(int64_t batch, int device, uwvk_bottom** out) {
     delete h;
     return st;
   }
-  for (int k = 0; k < 3; k++) h->Q.v[k * 3 + k] = 1.0;  // Covariance::Identity() (BottomUKF.cpp:48)
+  for (int k = 0; k < 3; k++) h->Q.v[k * 3 + k] = 1.0;  // Covariance::Identity() (BottomUKF.cpp:45)
   *out = h;
   return UWVK_OK;
 }
@@ -380,7 +380,7 @@ uwvk_status uwvk_bottom_update_range(uwvk_bottom* h, const double* mu, const dou
   if (!h || !mu || !unit_direction || !origin) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   const int64_t B = h->batch;
-  for (int64_t i = 0; i < B; i++) {  // checkMeasurment (BottomUKF.cpp:61)
+  for (int64_t i = 0; i < B; i++) {  // checkMeasurment (BottomUKF.cpp:58)
     if (mask && !mask[i]) continue;
     if (!std::isfinite(mu[i]) || (cov && !std::isfinite(cov[i]))) return UWVK_ENAN;
   }
@@ -408,7 +408,7 @@ uwvk_status uwvk_bottom_update_normal(uwvk_bottom* h, const double* mu, const do
   if (!h || !mu || (!cov && !shared_cov)) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   const int64_t B = h->batch;
-  // the reference does not check this measurement (BottomUKF.cpp:66-70); a
+  // the reference does not check this measurement (BottomUKF.cpp:63-67); a
   // zero / non-finite normal cannot be normalised into S2
   for (int64_t i = 0; i < B; i++) {
     if (mask && !mask[i]) continue;
@@ -447,7 +447,7 @@ uwvk_status uwvk_ipose_create(int64_t batch, int device, uwvk_ipose** out) {
     delete h;
     return st;
   }
-  std::vector<double> ref((size_t)batch * 7, 0.0);  // Affine3d::Identity() (IndirectPoseUKF.cpp:72)
+  std::vector<double> ref((size_t)batch * 7, 0.0);  // Affine3d::Identity() (IndirectPoseUKF.cpp:58)
   for (int64_t i = 0; i < batch; i++) ref[i * 7 + 3] = 1.0;
   if (hipMemcpy(h->d_aux, ref.data(), ref.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
     small_destroy(h);

@@ -14,7 +14,7 @@ struct NormalMeasurement : BatchMeasurement<3> {};
 
 class BottomUKF {
  public:
-  // BottomUKF(initial_state, state_cov) (BottomUKF.cpp:43-49): state batch*4, cov batch*9
+  // BottomUKF(initial_state, state_cov) (BottomUKF.cpp:40-46): state batch*4, cov batch*9
   BottomUKF(int64_t batch, const std::vector<double>& initial_state, const std::vector<double>& state_cov,
             int device = 0)
       : batch_(batch) {
@@ -40,7 +40,7 @@ class BottomUKF {
     check(uwvk_bottom_set_velocity(h_, v.data()), "setVelocity");
   }
   void predictionStep(double delta_t) { check(uwvk_bottom_predict(h_, delta_t), "predictionStep"); }
-  // integrateMeasurement(RangeMeasurement, unit_direction, origin) (BottomUKF.cpp:59-64)
+  // integrateMeasurement(RangeMeasurement, unit_direction, origin) (BottomUKF.cpp:56-61)
   void integrateMeasurement(const RangeMeasurement& m, const std::array<double, 3>& unit_direction,
                             const std::array<double, 3>& origin) {
     if (m.mu.size() != (size_t)batch_) throw std::invalid_argument("RangeMeasurement: wrong size");
@@ -48,7 +48,7 @@ class BottomUKF {
                                    unit_direction.data(), origin.data(), m.mask.empty() ? nullptr : m.mask.data()),
           "integrateMeasurement(RangeMeasurement)");
   }
-  // integrateMeasurement(NormalType, measurement_cov) (BottomUKF.cpp:66-70)
+  // integrateMeasurement(NormalType, measurement_cov) (BottomUKF.cpp:63-67)
   void integrateMeasurement(const NormalMeasurement& m, const std::array<double, 4>& measurement_cov) {
     if (m.mu.size() != (size_t)batch_ * 3) throw std::invalid_argument("NormalType: wrong size");
     check(uwvk_bottom_update_normal(h_, m.mu.data(), m.cov.empty() ? nullptr : m.cov.data(),

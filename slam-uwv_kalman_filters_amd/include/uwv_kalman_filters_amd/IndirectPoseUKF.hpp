@@ -11,7 +11,7 @@ namespace uwv_kalman_filters_amd {
 class IndirectPoseUKF {
  public:
   // IndirectPoseUKF(position_error_std, orientation_error_std, orientation_error_tau,
-  // initial_position_error, initial_position_error_std) (IndirectPoseUKF.cpp:66-91).
+  // initial_position_error, initial_position_error_std) (IndirectPoseUKF.cpp:53-78).
   // initial_position_error: empty (zero) or batch*3.
   IndirectPoseUKF(int64_t batch, const std::array<double, 3>& position_error_std,
                   const std::array<double, 3>& orientation_error_std, double orientation_error_tau,
@@ -50,7 +50,7 @@ class IndirectPoseUKF {
   }
   void predictionStep(double delta_t) { check(uwvk_ipose_predict(h_, delta_t), "predictionStep"); }
   // integrateMeasurement(marker_features, feature_positions, marker_pose, cov_marker_pose,
-  // camera_config, camera_in_body) (IndirectPoseUKF.cpp:108-140)
+  // camera_config, camera_in_body) (IndirectPoseUKF.cpp:94-135)
   void integrateMeasurement(const std::vector<VisualFeatureMeasurement>& marker_features,
                             const std::vector<std::array<double, 3>>& feature_positions,
                             const std::vector<Pose7>& marker_pose, const std::array<double, 36>& cov_marker_pose,
