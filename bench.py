@@ -59,7 +59,6 @@ def psp_flops(n=53, k_pred=15, updates=((6, 3, 7),)):
 
 F_STEP_PSP = psp_flops()
 F_UPD3_PSP = psp_flops(updates=((6, 3, 7), (6, 3, 3))) - F_STEP_PSP  # one DVL update
-B_STEP = 45_808           # fp64 mu + Sigma read + write
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector = matrix) spec; probe measured 74 (profiles/r01_probe_fp64.txt)
 PEAK_HBM_GBS = 8000.0
 
@@ -89,7 +88,7 @@ def parse():
     ap.add_argument("--vel-groups", type=int, default=-1, help="C2: -1 auto, 0 lane per filter, 1 16-lane rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true", help="literal kernels (all 2n+1 sigma points)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core available to this process")
     return ap.parse_args()
 
 
@@ -105,71 +104,75 @@ def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance, c4_c
     return log, shift
 
 
-def pmc_entry(workload):
-    """The committed rocprofv3 PMC summary of this workload's kernel (or {})."""
+def pmc_entry(workload, steps=None):
+    """The committed rocprofv3 PMC summary of this workload's kernel for a
+    launch of `steps` epochs (profiles/pmc_traffic.json, key WORKLOAD-eSTEPS),
+    else the workload's default shape (or {})."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(workload) or {}
+            d = json.load(f)
     except (OSError, ValueError):
         return {}
+    if steps is not None and ("%s-e%d" % (workload, steps)) in d:
+        return d["%s-e%d" % (workload, steps)]
+    return d.get(workload) or {}
 
 
-def roofline_traffic(workload):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
-    e = pmc_entry(workload)
-    return float(e["bytes_per_launch"]) if "bytes_per_launch" in e else None
-
-
-# VALU issue roof: 256 CUs x 4 SIMDs, a wave64 VALU instruction occupies its
-# 16-lane SIMD for 4 cycles (fp64 FMA included), 2.4 GHz peak engine clock
-N_SIMD, CYC_PER_VALU, CLOCK_HZ = 1024, 4, 2.4e9
-
-
-def valu_issue(workload, kernel_ms_per_launch, epochs_per_launch):
-    """Fraction of the chip's VALU issue slots the kernel fills: the committed
-    SQ_INSTS_VALU count per epoch (rocprofv3 --pmc, profiles/pmc_traffic.json)
-    scaled to this launch, divided by the launch's SIMD cycles."""
-    e = pmc_entry(workload)
-    if "valu_insts_per_epoch" not in e:
+def counter_roofline(e, waves, epochs, kernel_ms):
+    """Executed-work roofline of the timed launch from the committed PMC passes
+    (profiles/pmc_traffic.json): fp64 VALU instructions per wave-epoch
+    (SQ_INSTS_VALU_{FMA,MUL,ADD}_F64) x 64 lanes x (2 for an FMA, 1 otherwise),
+    scaled to this launch's waves x epochs, over the live HIP-event kernel time.
+    The counters count issued instructions whatever the exec mask, so these are
+    lane-slot flops (an upper bound of the useful work; SQ_THREAD_CYCLES_VALU /
+    SQ_ACTIVE_INST_VALU gives the active-lane share).  None without the passes."""
+    pw = e.get("per_wave_epoch") or {}
+    if not {"valu_fma_f64", "valu_mul_f64", "valu_add_f64"} <= set(pw):
         return None
-    insts = float(e["valu_insts_per_epoch"]) * epochs_per_launch
-    slots = N_SIMD * (kernel_ms_per_launch * 1e-3) * CLOCK_HZ / CYC_PER_VALU
-    return {"valu_insts_per_launch": insts, "frac": insts / slots,
-            "valu_insts_per_wave_epoch": e.get("valu_insts_per_wave_epoch"), "source": e.get("valu_source")}
+    lane_flop = 64 * (2 * pw["valu_fma_f64"] + pw["valu_mul_f64"] + pw["valu_add_f64"])
+    out = {"fp64_lane_flop_per_wave_epoch": lane_flop,
+           "achieved_tflops": lane_flop * waves * epochs / (kernel_ms * 1e-3) / 1e12,
+           "epochs_profiled": e.get("epochs_per_launch"), "source": e.get("valu_source")}
+    for k in ("valu_busy", "active_lanes"):
+        if k in e:
+            out[k] = e[k]
+    return out
 
 
 def cpu_baseline(synth, cfg, uwv, mode, dof, threads):
-    """fp64 C oracle on a bounded sample of the same workload (host cores)."""
+    """The fp64 C oracle's timing build (oracle/liboracle_fast.so: -O3,
+    x86-64-v4, one instance per task, pthreads) on a bounded sample of the same
+    workload, on every core this process may use; plus one instance on one
+    core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as O
-    batch, epochs = 32 * threads, 2000  # ~10-20 s of CPU work
+    epochs = 2000
+    # single core first: it sizes the multi-core sample to ~15 s of wall time
+    log1 = synth.make_pose_log(1, epochs, mode=mode, dof=dof)
+    o1 = O.OraclePoseBatch(1, dof, timing=True)
+    o1.init_from_config(log1["pos0"], log1["pos_cov"], log1["rot0"], log1["rot_cov"], cfg, uwv)
+    o1.set_process_noise_from_config(cfg, log1["dt"])
+    t1 = time.perf_counter()
+    o1.run_log(log1, nthreads=1)
+    dt1 = time.perf_counter() - t1
+    rate1 = epochs / dt1
+    per_thread = max(1, int(round(15.0 * rate1 / epochs)))
+    batch = per_thread * threads
     log = synth.make_pose_log(batch, epochs, mode=mode, dof=dof)
-    o = O.OraclePoseBatch(batch, dof)
+    o = O.OraclePoseBatch(batch, dof, timing=True)
     o.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
     o.set_process_noise_from_config(cfg, log["dt"])
     t0 = time.perf_counter()
     o.run_log(log, nthreads=threads)
     dt = time.perf_counter() - t0
-    # SURVEY 8(d)(i): one instance on one core, the same log's first instance
-    o1 = O.OraclePoseBatch(1, dof)
-    log1 = {k: (v[:, :1] if k in ("gyro", "acc", "dvl", "pressure", "efforts") and hasattr(v, "ndim") and v.ndim >= 2
-                else v) for k, v in log.items()}
-    log1["adcp"] = log["adcp"][:, :, :1] if log["adcp"].size else log["adcp"]
-    for k in ("pos0", "pos_cov", "rot0", "rot_cov"):
-        log1[k] = log[k][:1]
-    log1["batch"] = 1
-    o1.init_from_config(log1["pos0"], log1["pos_cov"], log1["rot0"], log1["rot_cov"], cfg, uwv)
-    o1.set_process_noise_from_config(cfg, log["dt"])
-    t1 = time.perf_counter()
-    o1.run_log(log1, nthreads=1)
-    dt1 = time.perf_counter() - t1
     return {"value": batch * epochs / dt, "unit": "steps/s", "cores": threads, "kind": "port",
-            "sample": "%d PoseUKF instances x %d epochs (%s, incl. %d DVL updates each), %d pthreads, %.2f s wall"
-                      % (batch, epochs, mode, int(((log["flags"] & 2) != 0).sum()), threads, dt),
-            "single_core": {"value": epochs / dt1, "unit": "steps/s", "cores": 1,
+            "sample": "%d PoseUKF instances x %d epochs (%s, incl. %d DVL updates each), %d pthreads, %.2f s wall; "
+                      "oracle timing build -O3 -march=x86-64-v4" % (batch, epochs, mode,
+                                                                   int(((log["flags"] & 2) != 0).sum()), threads, dt),
+            "single_core": {"value": rate1, "unit": "steps/s", "cores": 1,
                             "sample": "1 PoseUKF instance x %d epochs, %.2f s" % (epochs, dt1)},
-            "host": {"cpu": _cpu_model(), "logical_cpus": os.cpu_count()}}
+            "host": {"cpu": _cpu_model(), "logical_cpus": os.cpu_count(), "available_to_job": threads}}
 
 
 def _cpu_model():
@@ -183,26 +186,52 @@ def _cpu_model():
     return "unknown"
 
 
+def available_cores():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup v2
+    CPU quota when one is set (the GPU box shares its host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(float(q) / float(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def launched_by_torchrun():
+    return "TORCHELASTIC_RUN_ID" in os.environ or ("LOCAL_RANK" in os.environ and "WORLD_SIZE" in os.environ)
+
+
+def init_dist(world, local, backend):
+    """One process per GPU: the process group is made whenever the job runs
+    under torch.distributed.run (world size 1 included, so the RCCL path runs
+    on a one-GPU box too) or with WORLD_SIZE > 1."""
+    if world == 1 and not launched_by_torchrun():
+        return None
+    import torch
+    import torch.distributed as dist
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo")
+    return dist
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
     # UWVK_BENCH_BACKEND=gloo: rehearsal of the N-rank path on one GPU (all ranks
     # on device 0, statistics reduced on the host); the driver's runs use RCCL
     backend = os.environ.get("UWVK_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = 0
     stat_dev = "cuda" if backend == "nccl" else None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+    dist = init_dist(world, local, backend)
     from uwvk import engine, ensemble, synth
 
     if a.mode == "C2":
@@ -226,6 +255,20 @@ def main():
     window = flags[e0:e0 + a.steps]
     n_dvl = int(((window & 2) != 0).sum())
     truth = log["truth"].state(e0 + a.steps, a.dof)
+    # the collective: with RCCL, the engine's own communicator (uwvk_comm_*,
+    # rank 0's id shipped over the process group) so the all-reduce runs on the
+    # handle's stream right after the statistics kernel; gloo rehearsals reduce
+    # on the host through torch.distributed
+    comm = None
+    if dist is not None and backend == "nccl":
+        uid = [engine.RcclComm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = engine.RcclComm(world, uid[0], rank, local)
+    # warm the statistics kernels and the collective (module load, RCCL
+    # communicator set-up) outside the timed region
+    st_w = f.ensemble_stats(truth, comm)
+    if dist is not None and comm is None:
+        ensemble.allreduce_stats(st_w, dist)
 
     def barrier():
         if dist is not None:
@@ -237,10 +280,10 @@ def main():
     f.timer_start()
     f.run_log(dlog, e0, a.steps, sync=False)
     kernel_ms = f.timer_stop()  # HIP events on the handle's stream around the epoch launches
-    stats = f.ensemble_stats(truth)  # synchronous
-    if dist is not None:
-        # RCCL over xGMI: the only collective of the workload
-        stats = ensemble.allreduce_stats(stats, dist, device=stat_dev)
+    # synchronous; RCCL over xGMI (comm) is the only collective of the workload
+    stats = f.ensemble_stats(truth, comm)
+    if dist is not None and comm is None:
+        stats = ensemble.allreduce_stats(stats, dist)
     f.synchronize()
     barrier()
     wall = time.perf_counter() - t0
@@ -262,15 +305,35 @@ def main():
     n_eff = int(((window & 0x10) != 0).sum())
     launches = a.steps if a.dense else 1 + 2 * n_eff
     per_launch_ms = kernel_ms / launches
-    # roofline.achieved: SURVEY 8(d)'s frozen algorithmic work (reference algorithm)
+    # reference-equivalent work (the literal ukfom algorithm)
     flops_ref = B * (F_STEP * a.steps + F_UPD3 * n_dvl)
-    flops_exec = B * ((F_STEP_EXEC * a.steps + F_UPD3_EXEC * n_dvl) if a.dense
-                      else (F_STEP_PSP * a.steps + F_UPD3_PSP * n_dvl))
-    achieved_tf = flops_ref / (kernel_ms * 1e-3) / 1e12
-    exec_tf = flops_exec / (kernel_ms * 1e-3) / 1e12
+    # the engine's own flop model
+    flops_model = B * ((F_STEP_EXEC * a.steps + F_UPD3_EXEC * n_dvl) if a.dense
+                       else (F_STEP_PSP * a.steps + F_UPD3_PSP * n_dvl))
+    eff_tf = flops_ref / (kernel_ms * 1e-3) / 1e12
+    model_tf = flops_model / (kernel_ms * 1e-3) / 1e12
     kname = ("k_pose_epoch<%d>" if a.dense else "k_psp_epoch<%d>") % a.dof
     workload = "%s-dof%d-b%d%s" % (a.mode, a.dof, B, "-dense" if a.dense else "")
-    traffic = roofline_traffic(workload)
+    pmc = pmc_entry(workload, a.steps)
+    cr = None if a.dense or launches != 1 else counter_roofline(pmc, B, a.steps, kernel_ms)
+    traffic = pmc.get("bytes_per_launch") if pmc.get("epochs_per_launch") == a.steps else None
+    achieved = cr["achieved_tflops"] if cr else model_tf
+    roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
+            "kernel": kname, "launches": launches, "kernel_ms_per_launch": per_launch_ms,
+            "achieved_source": ("fp64 VALU lane-flops from SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 of the committed PMC "
+                                "passes of this launch shape (%s), over this run's HIP-event kernel time"
+                                % (cr or {}).get("source") if cr else
+                                "the engine's flop model (no PMC pass of this shape committed)"),
+            "counters": cr,
+            "model_flop_per_step": (F_STEP_EXEC if a.dense else F_STEP_PSP),
+            "model_tflops": model_tf,
+            "effective_tflops": eff_tf,
+            "effective_note": "reference-equivalent rate: SURVEY 8(d)'s literal-ukfom work (1,554,084 flop per "
+                              "step + 853,707 per DVL update) over the kernel time; the PSP engine computes the "
+                              "same result with ~3.4% of those flops (DESIGN.md 4.3), so this is not a roofline",
+            "traffic_source": ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes, the timed launch of this shape "
+                               "(%s)" % pmc.get("source")) if traffic else None}
     out = {
         "metric": METRIC, "value": value, "unit": "steps/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak",
@@ -282,31 +345,23 @@ def main():
                    "dvl_epochs_in_window": n_dvl,
                    "efforts_epochs_in_window": n_eff,
                    "adcp_epochs_in_window": int(((window & 8) != 0).sum()),
-                   "c4_cycle_s": list(cyc) if a.mode == "C4" else None, "parallelism": "instance-sharded x%d (no data-path collective)"
-                                                                  % world,
+                   "c4_cycle_s": list(cyc) if a.mode == "C4" else None,
+                   "parallelism": "instance-sharded x%d (no data-path collective)" % world,
+                   "collective": ("RCCL all_reduce of the ensemble statistics on the handle's stream "
+                                  "(uwvk_pose_ensemble_allreduce)" if comm else
+                                  "gloo all_reduce of the ensemble statistics") if dist else None,
                    "path": "dense (all 2n+1 sigma points)" if a.dense else "PSP (partitioned sigma points)",
                    "kernel": kname},
-        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": traffic,
-                     "kernel": kname, "launches": launches, "kernel_ms_per_launch": per_launch_ms,
-                     "algorithmic_flop_per_launch": flops_ref / launches,
-                     "algorithmic_flop_per_step": F_STEP,
-                     "executed_flop_per_step": (F_STEP_EXEC if a.dense else F_STEP_PSP),
-                     "executed_tflops": exec_tf, "executed_frac": exec_tf / PEAK_FP64_TFLOPS,
-                     "hbm_frac_algorithmic": (B * B_STEP * a.steps / (kernel_ms * 1e-3)) / (PEAK_HBM_GBS * 1e9),
-                     "valu_issue": None if a.dense or launches != 1 else valu_issue(workload, per_launch_ms, a.steps),
-                     "note": "achieved/frac count the reference algorithm's flops (SURVEY 8(d), 1,554,084 per step); "
-                             + ("the literal path executes executed_flop_per_step; MFMA busy 16%, the serial "
-                                "Cholesky/LDS chain binds (profiles/r01/pmc_mfma_dense_r01s.txt)" if a.dense else
-                                "the PSP path executes executed_flop_per_step (executed_frac); its binding roof is "
-                                "VALU issue (valu_issue.frac, DESIGN.md section 6)")},
+        "roofline": roof,
+        "timing": {"wall_ms": wall * 1e3, "kernel_ms": kernel_ms, "outside_kernel_ms": wall * 1e3 - kernel_ms},
         "ensemble": {"nees_mean_pos_ori_vel": float(stats[-1] / (B * world))},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(synth, cfg, uwv, a.mode, a.dof, threads)
+        out["cpu_baseline"] = cpu_baseline(synth, cfg, uwv, a.mode, a.dof, a.cpu_threads or available_cores())
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -358,13 +413,13 @@ def bench_vel(a, engine, synth, world, rank, local, dist):
                      "kernel_ms_per_launch": kernel_ms / launches, "algorithmic_flop_per_step": F_VEL_STEP},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = a.cpu_threads or available_cores()
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_ctypes as O
         # bounded sample (~10 s on 16 cores): the 2000-epoch log replayed `passes` times
         nb, ne, passes = 64 * threads, 2000, 30
         clog = synth.make_vel_log(nb, ne)
-        o = O.OracleVelBatch(nb)
+        o = O.OracleVelBatch(nb, timing=True)
         o.init(clog["x0"], clog["P0"])
         o.set_gyro(clog["gyro"][0])
         o.setup_motion_model(synth.default_uwv())

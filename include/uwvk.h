@@ -189,7 +189,11 @@ int uwvk_pose_dof(const uwvk_pose* h);
 void* uwvk_pose_stream(const uwvk_pose* h);
 uwvk_status uwvk_pose_synchronize(uwvk_pose* h);
 
-/* PoseUKF::PoseUKF(pos, pos_cov, rot, rot_cov, cfg, uwv, imu_in_body)
+/* Both init calls are the reference's constructors: every instance becomes a
+ * NEW filter, so the process noise is zero until set again and the stored
+ * rotation rate is zero (PoseUKF.cpp:380).
+ *
+ * PoseUKF::PoseUKF(pos, pos_cov, rot, rot_cov, cfg, uwv, imu_in_body)
  * (PoseUKF.hpp:100-103, PoseUKF.cpp:288-372).  Per instance: pos[3],
  * pos_cov[9], rot[4] (w,x,y,z), rot_cov[9].  imu_in_body = {tx,ty,tz,qw,qx,qy,qz}
  * (NULL = identity), shared by the batch. */

@@ -17,6 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
 from uwvk import abi  # noqa: E402
 
 _LIB = None
+_LIB_FAST = None
 DP = C.POINTER(C.c_double)
 
 
@@ -24,18 +25,32 @@ def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
 
+def _load(name):
+    path = os.path.join(HERE, name)
+    if not os.path.exists(path):
+        build()
+    L = C.CDLL(path)
+    L.or_pose_sizeof.restype = C.c_size_t
+    L.or_vel_sizeof.restype = C.c_size_t
+    L.or_wgs84_gravity.restype = C.c_double
+    return L
+
+
 def lib():
+    """The parity build (-O2 -ffp-contract=off)."""
     global _LIB
     if _LIB is None:
-        path = os.path.join(HERE, "liboracle.so")
-        if not os.path.exists(path):
-            build()
-        L = C.CDLL(path)
-        L.or_pose_sizeof.restype = C.c_size_t
-        L.or_vel_sizeof.restype = C.c_size_t
-        L.or_wgs84_gravity.restype = C.c_double
-        _LIB = L
+        _LIB = _load("liboracle.so")
     return _LIB
+
+
+def lib_timing():
+    """The timing build (-O3 -march=x86-64-v4, contraction on): bench.py's
+    cpu_baseline only, never a parity checker."""
+    global _LIB_FAST
+    if _LIB_FAST is None:
+        _LIB_FAST = _load("liboracle_fast.so")
+    return _LIB_FAST
 
 
 class so3_right:
@@ -83,8 +98,8 @@ class VelRunArgs(C.Structure):
 class OraclePoseBatch:
     """`batch` independent oracle PoseUKF instances in one contiguous buffer."""
 
-    def __init__(self, batch, dof=53):
-        self.L = lib()
+    def __init__(self, batch, dof=53, timing=False):
+        self.L = lib_timing() if timing else lib()
         self.batch, self.dof = batch, dof
         self.lay = abi.layout(dof)
         self.sz = self.L.or_pose_sizeof()
@@ -214,8 +229,8 @@ class OraclePoseBatch:
 
 
 class OracleVelBatch:
-    def __init__(self, batch):
-        self.L = lib()
+    def __init__(self, batch, timing=False):
+        self.L = lib_timing() if timing else lib()
         self.batch = batch
         self.sz = self.L.or_vel_sizeof()
         self.buf = (C.c_char * (self.sz * batch))()

@@ -237,8 +237,19 @@ uwvk_status uwvk_pose_synchronize(uwvk_pose* h) {
   return hipStreamSynchronize(h->stream) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
 }
 
+// Both init calls replace the reference's constructors (PoseUKF.cpp:288-391):
+// the filter object is new, so the process noise is zero until it is set again
+// and the stored rotation rate is zero (:380); the handle keeps its stream,
+// buffers and options.
 static uwvk_status upload_state(uwvk_pose* h, const std::vector<double>& x, const std::vector<double>& P,
                                 const std::vector<double>& off, const std::vector<double>& model) {
+  const size_t n = (size_t)h->dof;
+  h->Qh.assign(n * n, 0.0);
+  h->qp_dt = -1.0;
+  for (double& v : h->sh.q_ori) v = 0.0;
+  for (double& v : h->sh.q_wv) v = 0.0;
+  HIPCHK(hipMemsetAsync(h->d_Q, 0, n * n * 8, h->stream));
+  HIPCHK(hipMemsetAsync(h->d_rot, 0, (size_t)h->batch * 3 * 8, h->stream));
   HIPCHK(hipMemcpyAsync(h->d_mu, x.data(), x.size() * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d_sigma, P.data(), P.size() * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, h->stream));

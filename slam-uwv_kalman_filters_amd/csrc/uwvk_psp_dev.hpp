@@ -62,18 +62,22 @@ struct PG {
   static constexpr int NSLOT = (NP + 63) / 64;       // flat slots per lane
   static constexpr int N = 2 * DOF + 1;              // ukfom sigma points
   static constexpr int KP = 15;                      // predict: nonlinear prefix (pos.x .. gyro bias)
-  static constexpr int STG = 160;                    // L_a rows for the point lanes / Cholesky column / C~
-
+  // staging area (L_a rows for the point lanes, the Cholesky column, C~ halves,
+  // LDS transposes): 115 doubles puts PspSmem<53> at 12,800 B, the most that
+  // fits 12 one-wave workgroups on a gfx950 CU (tools/probe_lds_occupancy.hip:
+  // 12,800 B -> 12 per CU, 13,056 B -> 11); the r01 layout (160) ran at 11
+  static constexpr int STG = 115;
 };
 
 template <int DOF>
 struct alignas(16) PspSmem {
-  double S[PG<DOF>::NP];  // Sigma, packed lower triangle
-  double mu[56];          // mean (store layout)
-  double stg[PG<DOF>::STG];  // rows of L_a read by the sigma-point lanes
+  double S[PG<DOF>::NP];          // Sigma, packed lower triangle
+  double mu[Lay<DOF>::store];     // mean (store layout)
+  double stg[PG<DOF>::STG];       // staging (see PG::STG)
   // everything else (Delta, Dz, H, P, delta, offsets, the Q band) lives in
-  // lane registers or uniform SGPRs: 12.9 KB per instance -> 12 waves per CU
+  // lane registers or uniform SGPRs
 };
+static_assert(sizeof(PspSmem<53>) <= 12800, "12 instances per CU");
 
 UWVK_DEV constexpr int pidx(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
 
@@ -213,7 +217,7 @@ UWVK_DEV void wsync() {  // LDS ordering point between the lanes of one wave
 // i by a pairwise tree; out[i] is read back as a uniform value.
 template <int R, int NL, int STRIDE>
 UWVK_DEV void lds_sums(const double (&v)[R], double* buf, int l, double (&out)[R]) {
-  static_assert(NL % 2 == 0 && R * NL <= 160, "transpose buffer");
+  static_assert(NL % 2 == 0 && R * NL <= 115, "transpose buffer (PG::STG)");
   const int c = l / STRIDE;
   if (l % STRIDE == 0 && c < NL) {
 #pragma unroll
@@ -269,7 +273,10 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
     if constexpr (J + 1 < K) pnext = readlane_d(a[J + 1] - a[J] * a[J], J + 1);
     if (q >= 0) rows[q * K + J] = a[J];
     if constexpr (J + 1 < K) {
-      if (r < K) col[r] = a[J];
+      // col aliases the LAST staged row's not-yet-written slots J+1 .. K-1:
+      // only L[c][J] for c > J is read, and that row's own L[.][c] lands in
+      // slot c at step c, after this step's reads (one wave: LDS in order)
+      if (r > J && r < K) col[r] = a[J];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -282,11 +289,12 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
   }
 }
 
-// staged rows of L_a start here inside sm.stg (the column buffer is stg[0..32))
-constexpr int STG_ROWS = 32;
+// staged rows of L_a start here inside sm.stg; the Cholesky column buffer is
+// folded into the last staged row (pchol_step_lds)
+constexpr int STG_ROWS = 0;
 
 // panel Sigma[r][0..K) = d_r d_c Sigma~[r][c] (dl: this lane's d); stg: the
-// staging area (column buffer + the rows of RL::rows, see STG_ROWS)
+// staging area (the rows of RL::rows, the column buffer inside the last one)
 template <int DOF, int K, class RL>
 UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* stg) {
   const int rr = r < DOF ? r : DOF - 1;
@@ -305,8 +313,8 @@ UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* s
   int q = -1;
 #pragma unroll
   for (int k = 0; k < RL::NR; k++) q = (r == RL::rows[k]) ? k : q;
-  static_assert(K <= STG_ROWS && STG_ROWS + RL::NR * K <= 160, "staging area");
-  pchol_step_lds<K, 0>(a, r, ok, stg, stg + STG_ROWS, q, readlane_d(a[0], 0));
+  static_assert(RL::NR >= 1 && STG_ROWS + RL::NR * K <= 115, "staging area (PG::STG)");
+  pchol_step_lds<K, 0>(a, r, ok, stg + STG_ROWS + (RL::NR - 1) * K, stg + STG_ROWS, q, readlane_d(a[0], 0));
   psync();  // the staged rows are read by the point lanes next
   return ok;
 }
@@ -859,14 +867,14 @@ struct PZ {  // measurementZPosition, PoseUKF.cpp:100-105: linear (k = 0)
 // C~_i is an LDS broadcast (stg[M i ..]).  Rows are loaded before any store.
 // Lanes l > i load a neighbouring entry of the same PspSmem (never stored).
 template <int R, int M>
-UWVK_DEV void rankm_rows(double* S, const double* stg, int i0, int l, const double (&Kt)[M]) {
+UWVK_DEV void rankm_rows(double* S, const double* stg, int i0, int c0, int l, const double (&Kt)[M]) {
   const int tri = i0 * (i0 + 1) / 2;
   double sv[R], cv[R][M];
 #pragma unroll
   for (int r = 0; r < R; r++) {
     sv[r] = S[tri + r * i0 + r * (r + 1) / 2 + l];
 #pragma unroll
-    for (int a = 0; a < M; a++) cv[r][a] = stg[M * (i0 + r) + a];
+    for (int a = 0; a < M; a++) cv[r][a] = stg[M * (i0 - c0 + r) + a];
   }
 #pragma unroll
   for (int r = 0; r < R; r++) {
@@ -1109,17 +1117,31 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     Kt[i] = Kg[i] * ids;
   }
   {
-    if (l < DOF) {  // C~ rows for the broadcast reads (stg is free here)
+    // C~ rows for the broadcast reads (stg is free here), in two halves of
+    // rows [0, H) and [H, DOF) so that M * max(H, DOF - H) fits PG::STG
+    constexpr int RB = PSP_RB, NB = DOF / RB, REM = DOF - NB * RB;
+    constexpr int NB1 = (NB + 1) / 2, H = NB1 * RB;
+    static_assert(M * H <= PG<DOF>::STG && M * (DOF - H) <= PG<DOF>::STG, "C~ halves (PG::STG)");
+    static_assert(63 < Lay<DOF>::store + PG<DOF>::STG, "row over-read (lanes l > i, last rows) stays inside PspSmem");
+    if (l < H) {
 #pragma unroll
       for (int a2 = 0; a2 < M; a2++) sm.stg[M * l + a2] = Ct[a2];
     }
     psync();
-    constexpr int RB = PSP_RB, NB = DOF / RB, REM = DOF - NB * RB;
-    static_assert(63 < 56 + PG<DOF>::STG, "row over-read (lanes l > i, last rows) stays inside PspSmem");
     if (!(PSP_ABL & 2)) {
 #pragma unroll 1
-      for (int b = 0; b < NB; b++) rankm_rows<RB, M>(sm.S, sm.stg, b * RB, l, Kt);
-      if constexpr (REM > 0) rankm_rows<REM, M>(sm.S, sm.stg, NB * RB, l, Kt);
+      for (int b = 0; b < NB1; b++) rankm_rows<RB, M>(sm.S, sm.stg, b * RB, 0, l, Kt);
+    }
+    psync();
+    if (l >= H && l < DOF) {
+#pragma unroll
+      for (int a2 = 0; a2 < M; a2++) sm.stg[M * (l - H) + a2] = Ct[a2];
+    }
+    psync();
+    if (!(PSP_ABL & 2)) {
+#pragma unroll 1
+      for (int b = NB1; b < NB; b++) rankm_rows<RB, M>(sm.S, sm.stg, b * RB, H, l, Kt);
+      if constexpr (REM > 0) rankm_rows<REM, M>(sm.S, sm.stg, NB * RB, H, l, Kt);
     }
   }
   psync();

@@ -15,6 +15,16 @@
 namespace uwvk {
 namespace psp {
 
+#ifdef UWVK_TIMELINE
+// diagnostic build only (tools/timeline.py): per-wave wall-clock marks of the
+// epoch kernel (entry, Sigma loaded, epochs done, stored) and the CU it ran on
+__device__ unsigned long long uwvk_timeline[8 * 131072];
+UWVK_DEV void tl_mark(int64_t w, int k) {
+  const unsigned long long t = wall_clock64();
+  if (lane_id() == 0 && w < 131072) uwvk_timeline[w * 8 + k] = t;
+}
+#endif
+
 template <int DOF>
 UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
   using G = PG<DOF>;
@@ -26,7 +36,12 @@ UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
     const int e = l + 64 * t;
     int i = 0, j = 0;
     if (e < G::NP) unpack(e, i, j);
+#ifdef UWVK_ABL_NOLOAD  // timing ablation only (results invalid): Sigma = I, no HBM read
+    v[t] = (e < G::NP && i == j) ? 1.0 : 0.0;
+    (void)gs;
+#else
     v[t] = e < G::NP ? gs[i * DOF + j] : 0.0;
+#endif
   }
   const double m = l < Lay<DOF>::store ? b.mu[inst * Lay<DOF>::store + l] : 0.0;
 #pragma unroll
@@ -69,6 +84,9 @@ UWVK_DEV void store_psp(const PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst)
   // column-strided 8-B stores)
   const int l = lane_id();
   double* gs = b.sigma + inst * (int64_t)(DOF * DOF);
+#ifdef UWVK_ABL_NOSTORE  // timing ablation only (results invalid): Sigma not written back
+  if (sm.S[0] == 12345.678)
+#endif
 #pragma unroll 4
   for (int e = l; e < DOF * DOF; e += 64) {
     const int i = e / DOF, j = e - i * DOF;
@@ -200,7 +218,19 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
 #else
   Stamper* st = nullptr;
 #endif
+#ifdef UWVK_TIMELINE
+  tl_mark(blockIdx.x, 0);
+  if (lane_id() == 0 && blockIdx.x < 131072) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uwvk_timeline[blockIdx.x * 8 + 4] = ((unsigned long long)xcc << 32) | (unsigned)__smid();
+    uwvk_timeline[blockIdx.x * 8 + 5] = (unsigned long long)inst;
+  }
+#endif
   load_psp<DOF>(sm, b, inst);
+#ifdef UWVK_TIMELINE
+  tl_mark(blockIdx.x, 1);
+#endif
   UWVK_STAMP(40);
   double ds = 1.0, ids = 1.0;  // time scale of the Markov DOFs (Sigma = D Sigma~ D)
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
@@ -290,8 +320,15 @@ __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, Ep
     if (ea.accept_counts)
       for (int k = 0; k < 4; k++) ea.accept_counts[inst * 4 + k] += cnt[k];
   }
+#ifdef UWVK_TIMELINE
+  tl_mark(blockIdx.x, 2);
+#endif
   psp_fold<DOF>(sm, ds, ids);
   store_psp<DOF>(sm, b, inst);
+#ifdef UWVK_TIMELINE
+  __builtin_amdgcn_s_waitcnt(0);
+  tl_mark(blockIdx.x, 3);
+#endif
 }
 
 }  // namespace psp
@@ -336,6 +373,12 @@ hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const Po
 }
 
 }  // namespace uwvk
+
+#ifdef UWVK_TIMELINE
+extern "C" int uwvk_debug_read_timeline(unsigned long long* out, long long n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(uwvk::psp::uwvk_timeline), (size_t)n * 8) != hipSuccess;
+}
+#endif
 
 #ifdef UWVK_STAMPS
 // diagnostic build only: per-phase cycle sums of the PSP epoch kernel

@@ -46,9 +46,10 @@ def ensemble_stats_host(x, P, truth):
 
 
 def allreduce_stats(stats, dist, device=None):
-    """Sum the per-rank statistics vectors (torch.distributed, any backend)."""
+    """Sum the per-rank statistics vectors (torch.distributed, any backend).
+    Returns a new array; `stats` is left as it was."""
     import torch
-    t = torch.from_numpy(np.ascontiguousarray(stats, dtype=np.float64))
+    t = torch.from_numpy(np.array(stats, dtype=np.float64, copy=True))
     if device is not None:
         t = t.to(device)
     dist.all_reduce(t)

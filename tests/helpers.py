@@ -46,3 +46,10 @@ def init_both(oracle, engine, cfg, uwv, log, dt=1e-3):
     for f in (oracle, engine):
         f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
         f.set_process_noise_from_config(cfg, dt)
+
+
+def qrot_inv(q, v):
+    """conj(q) v q for arrays of unit quaternions [..., 4] (w, x, y, z) and vectors [..., 3]."""
+    w, u = q[..., :1], -q[..., 1:]
+    t = 2.0 * np.cross(u, v)
+    return v + w * t + np.cross(u, t)

@@ -124,3 +124,108 @@ def test_rccl_allreduce_through_c_abi():
     comm = engine.RcclComm(1, engine.RcclComm.unique_id(), 0, 0)
     np.testing.assert_array_equal(f.ensemble_stats(truth, comm), f.ensemble_stats(truth))
     comm.close()
+
+
+# ---- the sharded path on the HIP engine -----------------------
+
+SHARD = int(os.environ.get("UWVK_TEST_SHARD", "131072"))  # C5: 1,048,576 instances / 8 GPUs
+GPU_EPOCHS = 220  # includes the 5 Hz DVL update at epoch 199
+
+
+def _digest(P):
+    """Per-instance 64-bit digest of the covariance bytes (weighted wrap-around
+    sum of the fp64 bit patterns): equal digests <=> bitwise-equal rows, up to
+    a 2^-64 collision chance."""
+    w = np.random.default_rng(123).integers(1, 2 ** 63, size=P.shape[1:], dtype=np.uint64) | np.uint64(1)
+    v = np.ascontiguousarray(P).view(np.uint64)
+    with np.errstate(over="ignore"):
+        return (v * w).sum(axis=(1, 2), dtype=np.uint64)
+
+
+def _gpu_shard_run(lo, hi, device=0):
+    from uwvk import engine, synth
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(hi - lo, GPU_EPOCHS, "C3", first_instance=lo)
+    f = engine.PoseUKFBatch(hi - lo, device=device)
+    f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    f.set_process_noise_from_config(cfg, log["dt"])
+    f.run_log(f.upload_log(log))
+    assert not f.get_status().any()
+    return f, log["truth"].state(GPU_EPOCHS)
+
+
+def _gpu_worker(rank, world, port, outdir, q):
+    try:
+        import torch.distributed as dist  # torch (and its bundled HIP runtime / RCCL) first, as in bench.py
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+        from uwvk import ensemble
+        lo, hi = ensemble.shard_range(rank, world, SHARD * world)
+        f, truth = _gpu_shard_run(lo, hi)
+        local = f.ensemble_stats(truth)
+        summed = ensemble.allreduce_stats(local, dist)
+        x, P = f.get_state()
+        np.save(os.path.join(outdir, "x%d.npy" % rank), x)
+        q.put((rank, lo, hi, _digest(P), local, summed, None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of leaving the parent waiting
+        q.put((rank, None, None, None, None, None, repr(e)))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_gpu_two_rank_shards_bitwise(tmp_path):
+    """Two ranks (processes, gloo) each drive libuwvk on device 0 with C5's
+    shard size (131,072 instances per rank): per-instance mu bit-identical and
+    Sigma digests equal to ONE process running all 262,144 instances, the
+    all-reduced statistics equal to the sum of the per-rank ones and to the
+    host reduction over the full batch."""
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+    from uwvk import ensemble
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + (os.getpid() % 1000)
+    world = 2
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+    errs = [r[-1] for r in res if r[-1]]
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs)
+    f, truth = _gpu_shard_run(0, SHARD * world)
+    x1, P1 = f.get_state()
+    d1 = _digest(P1)
+    for rank, lo, hi, dig, local, summed, _ in res:
+        x = np.load(str(tmp_path / ("x%d.npy" % rank)))
+        np.testing.assert_array_equal(x, x1[lo:hi])
+        np.testing.assert_array_equal(dig, d1[lo:hi])
+        np.testing.assert_array_equal(summed, res[0][5])
+    np.testing.assert_array_equal(res[0][5], res[0][4] + res[1][4])  # a two-term sum is exact in any order
+    host = ensemble.ensemble_stats_host(x1, P1, truth)
+    np.testing.assert_allclose(res[0][5], host, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(res[0][5], f.ensemble_stats(truth), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_rccl_c_abi_two_devices():
+    """uwvk_pose_ensemble_allreduce across two GPUs (rank r on device r) through
+    the C ABI's own RCCL communicator; skipped on a one-GPU box."""
+    sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+    from uwvk import engine
+    import ctypes as C
+    n = C.c_int(0)
+    hip = C.CDLL("libamdhip64.so.7")
+    hip.hipGetDeviceCount(C.byref(n))
+    if n.value < 2:
+        pytest.skip("needs 2 GPUs (%d visible)" % n.value)
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_two_rank.py"), "--ranks", "2"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+    assert engine.device_available(1)

@@ -278,3 +278,45 @@ def test_nan_measurement_rejected():
     o, _ = _filter()
     with pytest.raises(RuntimeError):
         o.update("velocity", np.array([[np.nan, 0, 0]]), np.eye(3))
+
+
+def test_efforts_side_effect_reaches_velocity_only_update():
+    """measurementEfforts leaves the filter's shared DynamicModel holding the
+    LAST sigma point's model parameters (PoseUKF.cpp:158-173); the next
+    velocity-only update (constrainVelocity, :592) evaluates that model.  A
+    filter re-created from the same state (PoseUKF.cpp:374-391: model = the
+    configured UWV parameters) must therefore give a different velocity-only
+    update: the GPU tests of the full -> velocity-only sequence
+    (tests/test_gpu_surface.py) exercise a real dependency.  The last sigma
+    point is mu (-) L_{n-1}, which differs from mu only in the water density
+    (L lower triangular), so the model left behind is the PRIOR mean's
+    parameters: two full updates are needed before they differ from the
+    configured ones."""
+    B = 2
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(B, 10, "C4")
+    a = O.OraclePoseBatch(B, 53)
+    a.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    a.set_process_noise_from_config(cfg, 1e-3)
+    R = np.diag([25.0, 25, 25, 1, 1, 1])
+    for e, t in enumerate((30.0, 35.0)):
+        a.set_rotation_rate(log["gyro"][e])
+        a.predict(1e-3)
+        a.update("efforts", np.full((B, 6), t), R, only_vel=0)
+    x, P = a.get_state()
+    b = O.OraclePoseBatch(B, 53)
+    param = abi.PoseParameter()
+    param.gyro_bias_tau = param.acc_bias_tau = 600.0
+    param.inertia_tau = param.lin_damping_tau = param.quad_damping_tau = 3600.0
+    param.water_velocity_tau, param.adcp_bias_tau, param.water_density_tau = 900.0, 900.0, 3600.0
+    param.water_velocity_limits, param.water_velocity_scale = 0.1, 1e-3
+    param.atmospheric_pressure = 101325.0
+    b.init_from_state(x, P, abi.Location(synth.LAT0, synth.LON0, 0.0), uwv, param)
+    b.set_rotation_rate(log["gyro"][1])
+    np.testing.assert_array_equal(a.get_rotation_rate(), b.get_rotation_rate())
+    tau = np.full((B, 6), -10.0)
+    for f in (a, b):
+        f.update("efforts", tau, R, only_vel=1)
+    va, vb = a.get_state()[0][:, 7:10], b.get_state()[0][:, 7:10]
+    assert np.all(np.isfinite(va)) and np.all(np.isfinite(vb))
+    assert np.max(np.abs(va - vb)) > 1e-9
