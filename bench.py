@@ -354,7 +354,8 @@ def main():
                    "kernel": kname},
         "roofline": roof,
         "timing": {"wall_ms": wall * 1e3, "kernel_ms": kernel_ms, "outside_kernel_ms": wall * 1e3 - kernel_ms},
-        "ensemble": {"nees_mean_pos_ori_vel": float(stats[-1] / (B * world))},
+        "ensemble": {"nees_mean_pos_ori_vel": float(stats[-2] / max(1.0, B * world - stats[-1])),
+                     "nees_excluded_instances": int(stats[-1])},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(synth, cfg, uwv, a.mode, a.dof, a.cpu_threads or available_cores())

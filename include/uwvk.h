@@ -169,11 +169,17 @@ int uwvk_abi_version(void);
 int uwvk_device_available(int device);
 const char* uwvk_status_string(uwvk_status s);
 
-/* device memory helpers for device-resident logs (bench / run_log) */
+/* device memory helpers for device-resident logs (bench / run_log).
+ * uwvk_memcpy_h2d / _d2h are synchronous with ALL device work (they wait for
+ * every stream, the handles' non-blocking ones included, then copy).
+ * uwvk_memcpy_*_on are ordered on one stream (a handle's uwvk_*_stream) and
+ * return once the copy has completed. */
 uwvk_status uwvk_device_malloc(int device, size_t bytes, void** out);
 uwvk_status uwvk_device_free(void* p);
 uwvk_status uwvk_memcpy_h2d(void* dst, const void* src, size_t bytes);
 uwvk_status uwvk_memcpy_d2h(void* dst, const void* src, size_t bytes);
+uwvk_status uwvk_memcpy_h2d_on(void* dst, const void* src, size_t bytes, void* stream);
+uwvk_status uwvk_memcpy_d2h_on(void* dst, const void* src, size_t bytes, void* stream);
 
 /* ======================================================================== */
 /* PoseUKF                                                                   */
@@ -337,8 +343,10 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
  * out[0..store)        = sum_i x_i (orientation quaternion summed componentwise)
  * out[store..2*store)  = sum_i x_i^2
  * out[2*store..3*store)= sum_i (x_i - truth)^2 (orientation: rotation-vector error, 3 entries used)
- * out[3*store]         = sum_i NEES_i over (position, orientation, velocity) (9 DOF)
- * truth: host store-vector (nullable -> zeros).  out: host doubles, 3*store+1. */
+ * out[3*store]         = sum_i NEES_i over (position, orientation, velocity) (9 DOF),
+ *                        over the instances whose 9x9 covariance block is positive definite
+ * out[3*store+1]       = number of instances left out of that NEES sum (not positive definite / NaN)
+ * truth: host store-vector (nullable -> zeros).  out: host doubles, 3*store+2. */
 uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* out);
 
 /* Multi-GPU ensembles: one process (or thread) per GPU owns a

@@ -28,7 +28,7 @@ using namespace uwvk;
 // host side
 // ===========================================================================
 // ensemble statistics per instance group: 3 store + 1 doubles (store <= 54)
-constexpr int64_t kStatsMaxOut = 3 * 54 + 1;
+constexpr int64_t kStatsMaxOut = 3 * 54 + 2;
 
 struct uwvk_pose {
   int64_t batch = 0;
@@ -571,7 +571,7 @@ uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* 
 uwvk_status uwvk_pose_ensemble_allreduce(uwvk_pose* h, const double* truth, double* out, void* comm) {
   if (!h || !out) return UWVK_EINVAL;
   const int s = h->store;
-  const int nout = 3 * s + 1;
+  const int nout = 3 * s + 2;
   double* d_out = h->d_scratch;
   double* d_truth = h->d_scratch + 192;
   std::vector<double> t(s, 0.0);

@@ -23,7 +23,7 @@ hipError_t launch_pose_rotation_rate(int dof, hipStream_t st, const PoseBufs& b,
 hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const double* truth, double* out,
                              double* part) {
   const int64_t nb = (b.batch + 63) / 64;
-  const int nout = 3 * (dof == 53 ? Lay<53>::store : Lay<26>::store) + 1;
+  const int nout = 3 * (dof == 53 ? Lay<53>::store : Lay<26>::store) + 2;
   if (dof == 53) {
     hipLaunchKernelGGL(k_pose_stats<53>, dim3((unsigned)nb), dim3(64), 0, st, b, truth, part);
     hipLaunchKernelGGL(k_pose_stats_sum<53>, dim3(nout), dim3(256), 0, st, (const double*)part, nb, nout, out);

@@ -386,13 +386,14 @@ __global__ __launch_bounds__(64) void k_pose_rotation_rate(PoseBufs b, PoseShare
 // Ensemble statistics, deterministic two-stage reduction (no atomics): one wave
 // per 64 instances writes its partial sums (butterfly shuffles, the same value
 // in every lane), then k_pose_stats_sum adds the partials in a fixed order.
-// Layout of out (nout = 3 store + 1): sum mu, sum mu^2, sum err^2 (orientation
+// Layout of out (nout = 3 store + 2): sum mu, sum mu^2, sum err^2 (orientation
 // slots 3..5 hold the squared SO3 log error, slot 6 is 0), NEES over
-// (position, orientation, velocity).
+// (position, orientation, velocity) summed over the instances whose 9x9 block
+// is positive definite, and the number of instances left out of that sum.
 template <int DOF>
 __global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, const double* truth, double* part) {
   using L = Lay<DOF>;
-  constexpr int S = L::store, NOUT = 3 * S + 1;
+  constexpr int S = L::store, NOUT = 3 * S + 2;
   const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const bool live = i < b.batch;
   const double* x = b.mu + (live ? i : 0) * S;
@@ -418,11 +419,13 @@ __global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, const double* tru
   double A[81];
   for (int a = 0; a < 9; a++)
     for (int c = 0; c < 9; c++) A[a * 9 + c] = P[a * DOF + c];
+  bool pd = true;  // a non-positive pivot (or a NaN) leaves the instance out of the NEES sum
   for (int a = 0; a < 9; a++) {
     for (int c = 0; c <= a; c++) {
       double s = A[a * 9 + c];
       for (int k = 0; k < c; k++) s -= A[a * 9 + k] * A[c * 9 + k];
-      A[a * 9 + c] = (a == c) ? sqrt(s) : s / A[c * 9 + c];
+      if (a == c) pd = pd && (s > 0.0);
+      A[a * 9 + c] = (a == c) ? sqrt(s > 0.0 ? s : 1.0) : s / A[c * 9 + c];
     }
   }
   double y[9], nees = 0;
@@ -432,7 +435,9 @@ __global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, const double* tru
     y[a] = s / A[a * 9 + a];
     nees += y[a] * y[a];
   }
-  put(3 * S, nees);
+  pd = pd && isfinite(nees);
+  put(3 * S, pd ? nees : 0.0);
+  put(3 * S + 1, pd ? 0.0 : 1.0);
 }
 
 // out[s] = sum over the nblk partial rows, block s: thread t takes rows t, t + 256, ...

@@ -5,8 +5,9 @@
 // requested range with Sigma packed in LDS, and writes it back once:
 //   RotationRate -> predictionStep(dt) -> Acceleration update
 //   [-> Velocity (DVL) -> Pressure -> ADCP cells]
-// BodyEfforts epochs are routed by the host to the literal kernels
-// (k_pose_epoch), whose HBM layout is shared.
+// The host splits a launch after each BodyEfforts epoch (this kernel runs that
+// epoch's predict and other updates) and runs the efforts update alone on the
+// literal k_pose_efforts_epoch, whose HBM layout is shared.
 #define UWVK_POSE_KERNEL_BODIES
 #include "uwvk_pose_kernels.hpp"
 #include "uwvk_psp_dev.hpp"

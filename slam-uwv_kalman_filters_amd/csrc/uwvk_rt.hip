@@ -52,11 +52,28 @@ uwvk_status uwvk_device_malloc(int device, size_t bytes, void** out) {
   return hipMalloc(out, bytes ? bytes : 16) == hipSuccess ? UWVK_OK : UWVK_ENOMEM;
 }
 uwvk_status uwvk_device_free(void* p) { return hipFree(p) == hipSuccess ? UWVK_OK : UWVK_EDEVICE; }
+// Synchronous with ALL device work: every handle launches on its own
+// non-blocking stream, which the null-stream hipMemcpy does not wait for, so
+// a read after run_log(sync = 0) would otherwise race the epoch kernels.
 uwvk_status uwvk_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  if (hipDeviceSynchronize() != hipSuccess) return UWVK_EDEVICE;
   return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
 }
 uwvk_status uwvk_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  if (hipDeviceSynchronize() != hipSuccess) return UWVK_EDEVICE;
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
+}
+// Stream-ordered: queued on `stream` (a handle's uwvk_*_stream), behind
+// everything already queued there; returns once the copy has completed.
+uwvk_status uwvk_memcpy_h2d_on(void* dst, const void* src, size_t bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st) != hipSuccess) return UWVK_EDEVICE;
+  return hipStreamSynchronize(st) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
+}
+uwvk_status uwvk_memcpy_d2h_on(void* dst, const void* src, size_t bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) return UWVK_EDEVICE;
+  return hipStreamSynchronize(st) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
 }
 
 }  // extern "C"

@@ -243,7 +243,7 @@ class PoseUKF {
   // Ensemble statistics (layout: uwvk_pose_ensemble_stats); with an RCCL
   // communicator (uwvk_comm_init, void* ncclComm_t) summed over all ranks.
   std::vector<double> ensembleStats(const double* truth = nullptr, void* comm = nullptr) {
-    std::vector<double> out(3 * store() + 1);
+    std::vector<double> out(3 * store() + 2);
     check(uwvk_pose_ensemble_allreduce(h_, truth, out.data(), comm), "ensembleStats");
     return out;
   }
@@ -254,7 +254,9 @@ class PoseUKF {
     check(uwvk_pose_get_status(h_, s.data(), clear ? 1 : 0), "status");
     return s;
   }
-  // Persistent multi-epoch path: one fused kernel launch per epoch.
+  // Multi-epoch path (uwvk_pose_run_log): one PSP k_psp_epoch launch per run of
+  // epochs, split after each BodyEfforts epoch, whose efforts update then runs
+  // alone on k_pose_efforts_epoch; UWVK_OPT_DENSE_SIGMA: one literal launch per epoch.
   void runLog(const uwvk_pose_log& log, int64_t first, int64_t count, uint32_t* accept_counts = nullptr) {
     check(uwvk_pose_run_log(h_, &log, first, count, accept_counts), "runLog");
   }

@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("UWVK_LIB") or os.path.join(PKG, "libuwvk.so")
 # every symbol include/uwvk.h declares (checked by tests/test_abi.py)
 SYMBOLS = [
     "uwvk_abi_version", "uwvk_device_available", "uwvk_status_string", "uwvk_device_malloc", "uwvk_device_free",
-    "uwvk_memcpy_h2d", "uwvk_memcpy_d2h",
+    "uwvk_memcpy_h2d", "uwvk_memcpy_d2h", "uwvk_memcpy_h2d_on", "uwvk_memcpy_d2h_on",
     "uwvk_pose_create", "uwvk_pose_destroy", "uwvk_pose_batch", "uwvk_pose_dof", "uwvk_pose_stream",
     "uwvk_pose_synchronize", "uwvk_pose_init_from_config", "uwvk_pose_init_from_state",
     "uwvk_pose_set_process_noise_from_config", "uwvk_pose_set_process_noise", "uwvk_pose_set_rotation_rate",
@@ -73,6 +73,8 @@ def lib(path=None):
         L.uwvk_device_free.argtypes = [VP]
         L.uwvk_memcpy_h2d.argtypes = [VP, VP, C.c_size_t]
         L.uwvk_memcpy_d2h.argtypes = [VP, VP, C.c_size_t]
+        L.uwvk_memcpy_h2d_on.argtypes = [VP, VP, C.c_size_t, VP]
+        L.uwvk_memcpy_d2h_on.argtypes = [VP, VP, C.c_size_t, VP]
         L.uwvk_device_malloc.argtypes = [C.c_int, C.c_size_t, C.POINTER(VP)]
         _LIB = L
     return _LIB
@@ -102,9 +104,14 @@ class DeviceBuffer:
         if arr.nbytes:
             _chk(lib().uwvk_memcpy_h2d(self.ptr, arr.ctypes.data_as(VP), arr.nbytes), "memcpy_h2d")
 
-    def read(self, dtype, shape):
+    def read(self, dtype, shape, stream=None):
+        """Copy to the host after all queued device work (stream=None), or
+        ordered on one handle's stream (e.g. PoseUKFBatch.stream)."""
         out = np.empty(shape, dtype)
-        _chk(lib().uwvk_memcpy_d2h(out.ctypes.data_as(VP), self.ptr, out.nbytes), "memcpy_d2h")
+        if stream is None:
+            _chk(lib().uwvk_memcpy_d2h(out.ctypes.data_as(VP), self.ptr, out.nbytes), "memcpy_d2h")
+        else:
+            _chk(lib().uwvk_memcpy_d2h_on(out.ctypes.data_as(VP), self.ptr, out.nbytes, stream), "memcpy_d2h_on")
         return out
 
     def free(self):
@@ -250,7 +257,7 @@ class PoseUKFBatch:
     def ensemble_stats(self, truth=None, comm=None):
         """Ensemble statistics of this handle's instances; with an RcclComm,
         summed over every rank's shard by RCCL (uwvk_pose_ensemble_allreduce)."""
-        out = np.zeros(3 * self.lay["store"] + 1)
+        out = np.zeros(3 * self.lay["store"] + 2)
         t = _f64(truth)
         if comm is None:
             _chk(self.L.uwvk_pose_ensemble_stats(self.h, _p(t), _p(out)), "ensemble_stats")

@@ -30,7 +30,7 @@ def _qlog_delta(q, t):
 def ensemble_stats_host(x, P, truth):
     """Host reference of uwvk_pose_ensemble_stats (same layout of `out`)."""
     store = x.shape[1]
-    out = np.zeros(3 * store + 1)
+    out = np.zeros(3 * store + 2)
     out[:store] = x.sum(0)
     out[store:2 * store] = (x * x).sum(0)
     e = x - truth
@@ -40,9 +40,26 @@ def ensemble_stats_host(x, P, truth):
     sq[3:6] += (r * r).sum(0)
     out[2 * store:3 * store] = sq
     err = np.concatenate([x[:, 0:3] - truth[0:3], r, x[:, 7:10] - truth[7:10]], 1)
-    sub = P[:, :9, :9]
-    out[3 * store] = float(np.einsum("bi,bi->", err, np.linalg.solve(sub, err[..., None])[..., 0]))
+    # instances whose 9x9 block is not positive definite are counted, not summed
+    sub = np.ascontiguousarray(P[:, :9, :9])
+    try:
+        ok = np.ones(x.shape[0], bool)
+        Lc = np.linalg.cholesky(sub)
+    except np.linalg.LinAlgError:
+        ok = np.array([np.all(np.linalg.eigvalsh(m) > 0) and _chol_ok(m) for m in sub])
+        Lc = np.linalg.cholesky(np.where(ok[:, None, None], sub, np.eye(9)))
+    y = np.linalg.solve(Lc, err[..., None])[..., 0]
+    out[3 * store] = float(np.sum(np.where(ok, np.sum(y * y, 1), 0.0)))
+    out[3 * store + 1] = float((~ok).sum())
     return out
+
+
+def _chol_ok(m):
+    try:
+        np.linalg.cholesky(m)
+        return True
+    except np.linalg.LinAlgError:
+        return False
 
 
 def allreduce_stats(stats, dist, device=None):

@@ -229,3 +229,27 @@ def test_rccl_c_abi_two_devices():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
     assert engine.device_available(1)
+
+
+@pytest.mark.gpu
+def test_ensemble_stats_excludes_non_pd_instances():
+    """An instance whose (position, orientation, velocity) block is not positive
+    definite is counted in out[3 store + 1] and left out of the NEES sum
+    instead of turning the whole batch's NEES into NaN (advisor r01)."""
+    sys.path.insert(0, os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "python"))
+    from uwvk import abi, engine, ensemble, synth
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    B = 130
+    log = synth.make_pose_log(B, 2, "C3")
+    f = engine.PoseUKFBatch(B)
+    f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    x, P = f.get_state()
+    P[7, 0, 0] = -1.0  # indefinite
+    P[64, 4, 4] = 0.0  # singular
+    f.init_from_state(x, P, abi.Location(synth.LAT0, synth.LON0, 0.0), uwv, abi.PoseParameter())
+    truth = log["truth"].state(0)
+    got = f.ensemble_stats(truth)
+    host = ensemble.ensemble_stats_host(x, P, truth)
+    assert np.all(np.isfinite(got))
+    assert got[-1] == 2 and host[-1] == 2
+    np.testing.assert_allclose(got, host, rtol=1e-9, atol=1e-12)

@@ -107,3 +107,26 @@ def test_count_zero_and_argument_errors():
     with pytest.raises(engine.UWVKError) as e:  # unsupported state layout
         engine.PoseUKFBatch(4, 30)
     assert e.value.code == 1
+
+
+def test_device_buffer_read_after_async_run_log():
+    """run_log(sync=False) leaves the epoch kernels in flight on the handle's
+    non-blocking stream; DeviceBuffer.read (uwvk_memcpy_d2h: waits for all
+    device work) and DeviceBuffer.read(stream=...) (ordered on that stream)
+    must both return the finished accept counts, equal to a synchronous run."""
+    B, E = 65536, 400  # ~40 ms of kernel work queued before the reads
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(B, E, "C4", dropout_on=0.3, dropout_off=0.1)
+    counts = []
+    for mode in ("sync", "async_device", "async_stream"):
+        f = engine.PoseUKFBatch(B)
+        f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+        f.set_process_noise_from_config(cfg, 1e-3)
+        d = f.upload_log(log)
+        acc = engine.DeviceBuffer(np.zeros((B, 4), np.uint32))
+        f.run_log(d, accept_counts=acc, sync=(mode == "sync"))
+        counts.append(acc.read(np.uint32, (B, 4), stream=f.stream if mode == "async_stream" else None))
+        f.synchronize()
+    assert counts[0].sum() > 0
+    np.testing.assert_array_equal(counts[1], counts[0])
+    np.testing.assert_array_equal(counts[2], counts[0])
