@@ -129,6 +129,21 @@ UWVK_DEV int64_t xcd_instance(int64_t batch) {
   return w < (n << 3) ? (w & 7) * n + (w >> 3) : w;
 }
 
+// Packed lower triangle (row i at i (i + 1) / 2): Sigma's layout in HBM
+// ([batch][dof (dof + 1) / 2], every kernel) and in the PSP kernels' LDS.
+UWVK_DEV constexpr int pidx(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+template <int DOF>
+constexpr int tri_n() { return DOF * (DOF + 1) / 2; }
+
+// flat packed index e -> (i, j), i >= j
+UWVK_DEV void unpack(int e, int& i, int& j) {
+  int r = (int)((__builtin_sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+  if ((r + 1) * (r + 2) / 2 <= e) r++;
+  if (r * (r + 1) / 2 > e) r--;
+  i = r;
+  j = e - r * (r + 1) / 2;
+}
+
 UWVK_DEV double shfl_d(double v, int src) {
   int lo = __double2loint(v), hi = __double2hiint(v);
   lo = __shfl(lo, src, 64);

@@ -191,7 +191,9 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
     return UWVK_EDEVICE;
   }
   const size_t B = (size_t)batch, n = (size_t)dof;
-  bool ok = hipMalloc(&h->d_mu, B * h->store * 8) == hipSuccess && hipMalloc(&h->d_sigma, B * n * n * 8) == hipSuccess &&
+  // Sigma: packed lower triangle per instance (B n (n + 1) / 2 doubles)
+  bool ok = hipMalloc(&h->d_mu, B * h->store * 8) == hipSuccess &&
+            hipMalloc(&h->d_sigma, B * (n * (n + 1) / 2) * 8) == hipSuccess &&
             hipMalloc(&h->d_Q, n * n * 8) == hipSuccess && hipMalloc(&h->d_rot, B * 3 * 8) == hipSuccess &&
             hipMalloc(&h->d_off, B * 28 * 8) == hipSuccess && hipMalloc(&h->d_model, B * 27 * 8) == hipSuccess &&
             hipMalloc(&h->d_uwv, 108 * 8) == hipSuccess && hipMalloc(&h->d_status, B * 4) == hipSuccess &&
@@ -251,7 +253,14 @@ static uwvk_status upload_state(uwvk_pose* h, const std::vector<double>& x, cons
   HIPCHK(hipMemsetAsync(h->d_Q, 0, n * n * 8, h->stream));
   HIPCHK(hipMemsetAsync(h->d_rot, 0, (size_t)h->batch * 3 * 8, h->stream));
   HIPCHK(hipMemcpyAsync(h->d_mu, x.data(), x.size() * 8, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->d_sigma, P.data(), P.size() * 8, hipMemcpyHostToDevice, h->stream));
+  // HBM keeps the packed lower triangle (the caller's P is the full matrix;
+  // its lower triangle is taken, like the Cholesky-based ukfom reads it)
+  const int tn = h->dof * (h->dof + 1) / 2;
+  std::vector<double> Pp((size_t)h->batch * tn);
+  for (int64_t b = 0; b < h->batch; b++)
+    for (int i = 0, k = 0; i < h->dof; i++)
+      for (int j = 0; j <= i; j++, k++) Pp[b * tn + k] = P[(b * h->dof + i) * h->dof + j];
+  HIPCHK(hipMemcpyAsync(h->d_sigma, Pp.data(), Pp.size() * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d_model, model.data(), model.size() * 8, hipMemcpyHostToDevice, h->stream));
   double uw[108];
@@ -479,9 +488,21 @@ uwvk_status uwvk_pose_reset_with_external_pose(uwvk_pose* h, const double* pose)
 uwvk_status uwvk_pose_get_state(uwvk_pose* h, double* x, double* P) {
   if (!h || !x) return UWVK_EINVAL;
   HIPCHK(hipMemcpyAsync(x, h->d_mu, (size_t)h->batch * h->store * 8, hipMemcpyDeviceToHost, h->stream));
-  if (P)
-    HIPCHK(hipMemcpyAsync(P, h->d_sigma, (size_t)h->batch * h->dof * h->dof * 8, hipMemcpyDeviceToHost, h->stream));
+  if (!P) {
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return UWVK_OK;
+  }
+  // packed lower triangle -> the full symmetric matrix
+  const int n = h->dof, tn = n * (n + 1) / 2;
+  std::vector<double> Pp((size_t)h->batch * tn);
+  HIPCHK(hipMemcpyAsync(Pp.data(), h->d_sigma, Pp.size() * 8, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  for (int64_t b = 0; b < h->batch; b++) {
+    const double* s = &Pp[b * tn];
+    double* d = P + (size_t)b * n * n;
+    for (int i = 0, k = 0; i < n; i++)
+      for (int j = 0; j <= i; j++, k++) d[i * n + j] = d[j * n + i] = s[k];
+  }
   return UWVK_OK;
 }
 

@@ -70,12 +70,13 @@ template <int DOF>
 UWVK_DEV void load_instance(Smem<DOF>& sm, const PoseBufs& b, int64_t i) {
   const int l = tid();
   constexpr int T = Geo<DOF>::T, NL = (DOF * DOF + T - 1) / T;
-  const double* gs = b.sigma + i * (int64_t)(DOF * DOF);
+  const double* gs = b.sigma + i * (int64_t)tri_n<DOF>();  // packed lower triangle in HBM
   double v[NL];
 #pragma unroll
   for (int u = 0; u < NL; u++) {  // all loads in flight before the first LDS store
     const int k = l + u * T;
-    v[u] = (k < DOF * DOF) ? gs[k] : 0.0;
+    const int r = k / DOF, c = k - (k / DOF) * DOF;
+    v[u] = (k < DOF * DOF) ? gs[pidx(r, c)] : 0.0;
   }
   const double m = (l < Lay<DOF>::store) ? b.mu[i * Lay<DOF>::store + l] : 0.0;
 #pragma unroll
@@ -90,8 +91,12 @@ UWVK_DEV void load_instance(Smem<DOF>& sm, const PoseBufs& b, int64_t i) {
 template <int DOF>
 UWVK_DEV void store_instance(const Smem<DOF>& sm, const PoseBufs& b, int64_t i) {
   const int l = tid();
-  double* gs = b.sigma + i * (int64_t)(DOF * DOF);
-  for (int k = l; k < DOF * DOF; k += Geo<DOF>::T) gs[k] = sm.S[k];
+  double* gs = b.sigma + i * (int64_t)tri_n<DOF>();
+  for (int e = l; e < tri_n<DOF>(); e += Geo<DOF>::T) {
+    int r, c;
+    unpack(e, r, c);
+    gs[e] = sm.S[r * DOF + c];
+  }
   if (l < Lay<DOF>::store) b.mu[i * Lay<DOF>::store + l] = sm.mu[l];
 }
 
@@ -397,7 +402,7 @@ __global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, const double* tru
   const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const bool live = i < b.batch;
   const double* x = b.mu + (live ? i : 0) * S;
-  const double* P = b.sigma + (live ? i : 0) * (int64_t)(DOF * DOF);
+  const double* P = b.sigma + (live ? i : 0) * (int64_t)tri_n<DOF>();
   double* o = part + (int64_t)blockIdx.x * NOUT;
   auto put = [&](int slot, double v) {
     v = live ? v : 0.0;
@@ -418,7 +423,7 @@ __global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, const double* tru
   for (int k = 0; k < 3; k++) { err[k] = x[k] - truth[k]; err[3 + k] = r[k]; err[6 + k] = x[7 + k] - truth[7 + k]; }
   double A[81];
   for (int a = 0; a < 9; a++)
-    for (int c = 0; c < 9; c++) A[a * 9 + c] = P[a * DOF + c];
+    for (int c = 0; c <= a; c++) A[a * 9 + c] = P[pidx(a, c)];  // the lower triangle is all the solve reads
   bool pd = true;  // a non-positive pivot (or a NaN) leaves the instance out of the NEES sum
   for (int a = 0; a < 9; a++) {
     for (int c = 0; c <= a; c++) {

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(aug::Engine<PoseMarkerM<DOF>>::BLOCK) void k_pose_v
     for (int i = e.g; i < na * na; i += E::G) {
       const int r = i / na, c = i % na;
       double v = 0.0;
-      if (r < n && c < n) v = b.sigma[inst * n * n + r * n + c];
+      if (r < n && c < n) v = b.sigma[inst * tri_n<n>() + pidx(r, c)];
       else if (r >= n && c >= n) v = va.cov_marker[(r - n) * 6 + (c - n)];
       e.sm[E::o_sig + i] = v;
     }
@@ -46,7 +46,11 @@ __global__ __launch_bounds__(aug::Engine<PoseMarkerM<DOF>>::BLOCK) void k_pose_v
   const bool ok = aug::visual_loop<E, S, false>(e, va, inst);
   // ukf.reset(new MTK_UKF(mu.filter_state, sigma.block(0, 0, n, n))) (PoseUKF.cpp:652)
   if (e.live && ok) {
-    for (int i = e.g; i < n * n; i += E::G) b.sigma[inst * n * n + i] = e.sm[E::o_sig + (i / n) * na + (i % n)];
+    for (int i = e.g; i < tri_n<n>(); i += E::G) {
+      int r, c;
+      unpack(i, r, c);
+      b.sigma[inst * tri_n<n>() + i] = e.sm[E::o_sig + r * na + c];
+    }
     for (int k = e.g; k < S; k += E::G) b.mu[inst * S + k] = e.sm[E::o_mu + k];
   }
   if (e.live && !ok && e.g == 0) b.status[inst] |= UWVK_ST_NOTPD;

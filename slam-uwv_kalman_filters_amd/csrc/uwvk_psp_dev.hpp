@@ -79,16 +79,7 @@ struct alignas(16) PspSmem {
 };
 static_assert(sizeof(PspSmem<53>) <= 12800, "12 instances per CU");
 
-UWVK_DEV constexpr int pidx(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
-
-// flat packed index e -> (i, j), i >= j
-UWVK_DEV void unpack(int e, int& i, int& j) {
-  int r = (int)((__builtin_sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
-  if ((r + 1) * (r + 2) / 2 <= e) r++;
-  if (r * (r + 1) / 2 > e) r--;
-  i = r;
-  j = e - r * (r + 1) / 2;
-}
+// pidx / unpack: uwvk_dev.hpp (the HBM layout is the same packed triangle)
 
 // lane id that the optimiser cannot treat as loop-invariant: phases inside the
 // multi-epoch loop recompute their lane-derived addresses instead of having
@@ -736,21 +727,20 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   return ok;
 }
 
-// Sigma~ -> Sigma (d folded in, d = 1 afterwards).  Uses stg as the d table.
+// Sigma~ -> Sigma (d folded in, d = 1 afterwards): row sweep, lane l owns
+// column l of every row i >= l (uniform row offset, d_i a uniform read-back);
+// d = 1 on the unscaled DOFs, so their entries are multiplied by 1 (bitwise kept)
 template <int DOF>
 UWVK_DEV void psp_fold(PspSmem<DOF>& sm, double& ds, double& ids) {
-  using G = PG<DOF>;
   const int l = olane();
   psync();
-  if (l < DOF) sm.stg[l] = ds;
-  psync();
-#pragma unroll 1
-  for (int t = 0; t < G::NSLOT; t++) {
-    const int e = l + 64 * t;
-    if (e < G::NP) {
-      int i, j;
-      unpack(e, i, j);
-      if (scaled_dof(i) || scaled_dof(j)) sm.S[e] = sm.S[e] * (sm.stg[i] * sm.stg[j]);
+  const double dl = l < DOF ? ds : 1.0;
+#pragma unroll 4
+  for (int i = 12; i < DOF; i++) {  // rows < 12 and columns < 12 of them are unscaled
+    const double di = readlane_d(ds, i);
+    if (l <= i) {
+      const int e = i * (i + 1) / 2 + l;
+      sm.S[e] = sm.S[e] * (di * dl);
     }
   }
   psync();

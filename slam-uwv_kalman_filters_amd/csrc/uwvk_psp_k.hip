@@ -30,19 +30,12 @@ template <int DOF>
 UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
   using G = PG<DOF>;
   const int l = lane_id();
-  const double* gs = b.sigma + inst * (int64_t)(DOF * DOF);
+  const double* gs = b.sigma + inst * (int64_t)G::NP;  // packed in HBM as in LDS: one coalesced copy
   double v[G::NSLOT];
 #pragma unroll
   for (int t = 0; t < G::NSLOT; t++) {  // all loads in flight before the LDS stores
     const int e = l + 64 * t;
-    int i = 0, j = 0;
-    if (e < G::NP) unpack(e, i, j);
-#ifdef UWVK_ABL_NOLOAD  // timing ablation only (results invalid): Sigma = I, no HBM read
-    v[t] = (e < G::NP && i == j) ? 1.0 : 0.0;
-    (void)gs;
-#else
-    v[t] = e < G::NP ? gs[i * DOF + j] : 0.0;
-#endif
+    v[t] = e < G::NP ? gs[e] : 0.0;
   }
   const double m = l < Lay<DOF>::store ? b.mu[inst * Lay<DOF>::store + l] : 0.0;
 #pragma unroll
@@ -80,18 +73,13 @@ UWVK_DEV void lane_proc(const PoseBufs& b, const PoseShared& sh, int64_t inst, i
 
 template <int DOF>
 UWVK_DEV void store_psp(const PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
-  // the full symmetric matrix in row-major order, 64 consecutive entries per
-  // store instruction (a mirrored write of the packed triangle would scatter
-  // column-strided 8-B stores)
+  using G = PG<DOF>;
   const int l = lane_id();
-  double* gs = b.sigma + inst * (int64_t)(DOF * DOF);
-#ifdef UWVK_ABL_NOSTORE  // timing ablation only (results invalid): Sigma not written back
-  if (sm.S[0] == 12345.678)
-#endif
+  double* gs = b.sigma + inst * (int64_t)G::NP;
 #pragma unroll 4
-  for (int e = l; e < DOF * DOF; e += 64) {
-    const int i = e / DOF, j = e - i * DOF;
-    gs[e] = sm.S[pidx(i, j)];
+  for (int t = 0; t < G::NSLOT; t++) {
+    const int e = l + 64 * t;
+    if (e < G::NP) gs[e] = sm.S[e];
   }
   if (l < Lay<DOF>::store) b.mu[inst * Lay<DOF>::store + l] = sm.mu[l];
 }
@@ -209,6 +197,11 @@ UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
   return *p;
 }
 
+// Needs <= 168 VGPRs (3 waves per SIMD: with 12 instances per CU from the LDS
+// budget every wave slot is used; 156 now, tools/timeline.py shows 3,072
+// resident waves).  amdgpu_waves_per_eu(3) also gives 156 but schedules the
+// epoch loop worse: 145.0M against 148.5M steps/s (r02 A/B), so it is not set;
+// a fully unrolled Sigma store once took the kernel to 188 (2 waves per SIMD).
 template <int DOF>
 __global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
