@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Fold one tools/pmc_r02.sh run into profiles/pmc_traffic.json (key
+WORKLOAD-eSTEPS) and copy the summaries bench.py's roofline is computed from
+into profiles/r02/.  The timed launch is the LAST k_psp_epoch<53> dispatch of
+the bench (the alignment shift and the warm-up launches come first).
+
+usage: tools/pmc_fold.py TAG STEPS [WORKLOAD]"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+tag, steps = sys.argv[1], int(sys.argv[2])
+workload = sys.argv[3] if len(sys.argv) > 3 else "C3-dof53-b65536"
+base = os.path.join(ROOT, "gpurun_out", tag, "s%d" % steps)
+KERNEL = "k_psp_epoch<53>"
+N_SIMD = 1024
+
+
+def last(pass_name):
+    rows = [r for r in csv.DictReader(open(os.path.join(base, pass_name, "run_counter_collection.csv")))
+            if KERNEL in r["Kernel_Name"]]
+    did = max(int(r["Dispatch_Id"]) for r in rows)
+    sel = [r for r in rows if int(r["Dispatch_Id"]) == did]
+    c = {}
+    for r in sel:  # rocprofv3 may list a counter once per agent/dimension: sum
+        c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return c, did, sel
+
+
+mix, d1, rows_mix = last("sq_mix")
+busy, d2, rows_busy = last("sq_busy")
+fetch, d3, rows_f = last("fetch")
+write, d4, rows_w = last("write")
+waves = mix["SQ_WAVES"]
+we = waves * steps
+e = {
+    "kernel": KERNEL, "epochs_per_launch": steps, "waves": waves,
+    "fetch_size_kib_raw": fetch["FETCH_SIZE"], "write_size_kib_raw": write["WRITE_SIZE"],
+    "fetch_bytes": fetch["FETCH_SIZE"] * 1024 * 2, "write_bytes": write["WRITE_SIZE"] * 1024,
+}
+e["bytes_per_launch"] = e["fetch_bytes"] + e["write_bytes"]
+e["per_wave_epoch"] = {k.replace("SQ_INSTS_", "").lower(): v / we for k, v in mix.items() if k.startswith("SQ_INSTS_")}
+# VALU busy from the measured issue counter: SQ_ACTIVE_INST_VALU counts quad-cycles
+# (SQ_WAVE_CYCLES x 4 = a wave's lifetime in clocks, cross-checked against the
+# wall-clock timeline); GRBM_GUI_ACTIVE is summed over the 8 XCDs
+xcd_cycles = busy["GRBM_GUI_ACTIVE"] / 8.0
+e["valu_busy"] = {
+    "frac": busy["SQ_ACTIVE_INST_VALU"] * 4.0 / (N_SIMD * xcd_cycles),
+    "definition": "SQ_ACTIVE_INST_VALU x 4 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); the counter's "
+                  "quad-cycle granularity rounds a 2-cycle wave64 32-bit VALU op up to 4, so this is an upper bound",
+    "model_frac": (4.0 * (mix["SQ_INSTS_VALU_FMA_F64"] + mix["SQ_INSTS_VALU_MUL_F64"] + mix["SQ_INSTS_VALU_ADD_F64"]
+                          + mix["SQ_INSTS_VALU_TRANS_F64"])
+                   + 2.0 * (mix["SQ_INSTS_VALU"] - mix["SQ_INSTS_VALU_FMA_F64"] - mix["SQ_INSTS_VALU_MUL_F64"]
+                            - mix["SQ_INSTS_VALU_ADD_F64"] - mix["SQ_INSTS_VALU_TRANS_F64"])) / (N_SIMD * xcd_cycles),
+    "model_definition": "issue-cycle model: 4 cycles per wave64 fp64 instruction (78.6 TFLOP/s = 1024 x 2.4 GHz x 32), "
+                        "2 per other wave64 VALU instruction (MI355X_MICROARCH.md), over the same SIMD-cycles (lower bound)",
+    "counters": busy,
+}
+e["active_lanes"] = {
+    "thread_cycles_per_valu_quad_cycle": busy["SQ_THREAD_CYCLES_VALU"] / busy["SQ_ACTIVE_INST_VALU"],
+    "note": "SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU; 64 would be every lane of every VALU cycle",
+}
+e["source"] = ("profiles/r02/pmc_%s_s%d.csv (rocprofv3 --pmc, one pass per counter group; dispatch %d = the %d-epoch "
+               "timed launch; FETCH_SIZE doubled per MI355X_MICROARCH.md)" % (tag, steps, d3, steps))
+e["valu_source"] = "profiles/r02/pmc_%s_s%d.csv (dispatch %d)" % (tag, steps, d1)
+path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+d = json.load(open(path)) if os.path.exists(path) else {}
+d["%s-e%d" % (workload, steps)] = e
+json.dump(d, open(path, "w"), indent=1)
+os.makedirs(os.path.join(ROOT, "profiles", "r02"), exist_ok=True)
+keep = ("Dispatch_Id", "Kernel_Name", "Grid_Size", "VGPR_Count", "SGPR_Count", "LDS_Block_Size", "Counter_Name",
+        "Counter_Value", "Start_Timestamp", "End_Timestamp")
+with open(os.path.join(ROOT, "profiles", "r02", "pmc_%s_s%d.csv" % (tag, steps)), "w") as f:
+    w = csv.DictWriter(f, fieldnames=list(keep))
+    w.writeheader()
+    for rows in (rows_mix, rows_busy, rows_f, rows_w):
+        for r in rows:
+            w.writerow({k: r[k] for k in keep})
+shutil.copy(os.path.join(base, "trace", "run_kernel_stats.csv"),
+            os.path.join(ROOT, "profiles", "r02", "kernel_stats_%s_s%d.csv" % (tag, steps)))
+shutil.copy(os.path.join(base, "trace.json"), os.path.join(ROOT, "profiles", "r02", "bench_%s_s%d_traced.json" % (tag, steps)))
+print(json.dumps({k: v for k, v in e.items() if k != "valu_busy"}, indent=1))
+print("valu_busy", e["valu_busy"]["frac"], "model", e["valu_busy"]["model_frac"])
