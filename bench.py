@@ -206,8 +206,13 @@ def launched_by_torchrun():
 
 def init_dist(world, local, backend):
     """One process per GPU: the process group is made whenever the job runs
-    under torch.distributed.run (world size 1 included, so the RCCL path runs
-    on a one-GPU box too) or with WORLD_SIZE > 1."""
+    under torch.distributed.run (world size 1 included) or with WORLD_SIZE > 1.
+    It is a host-side control plane (gloo by default): barriers, the id of the
+    RCCL check communicator and the 163-double statistics sum.  An RCCL
+    communicator in the process (torch's nccl group or the engine's own) slows
+    the concurrently running epoch kernel by 6-7% on the GPU (r02: 9.20 ->
+    9.88 ms per 20-epoch launch, rocprofv3 kernel trace),
+    so none exists during the timed region."""
     if world == 1 and not launched_by_torchrun():
         return None
     import torch
@@ -225,10 +230,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # UWVK_BENCH_BACKEND=gloo: rehearsal of the N-rank path on one GPU (all ranks
-    # on device 0, statistics reduced on the host); the driver's runs use RCCL
-    backend = os.environ.get("UWVK_BENCH_BACKEND", "nccl")
-    if backend == "gloo":
+    backend = os.environ.get("UWVK_BENCH_BACKEND", "gloo")
+    # UWVK_BENCH_SAME_DEVICE=1: rehearsal of the N-rank path on one GPU (all ranks on device 0)
+    if os.environ.get("UWVK_BENCH_SAME_DEVICE") == "1":
         local = 0
     stat_dev = "cuda" if backend == "nccl" else None
     dist = init_dist(world, local, backend)
@@ -255,20 +259,25 @@ def main():
     window = flags[e0:e0 + a.steps]
     n_dvl = int(((window & 2) != 0).sum())
     truth = log["truth"].state(e0 + a.steps, a.dof)
-    # the collective: with RCCL, the engine's own communicator (uwvk_comm_*,
-    # rank 0's id shipped over the process group) so the all-reduce runs on the
-    # handle's stream right after the statistics kernel; gloo rehearsals reduce
-    # on the host through torch.distributed
+    # the collective of the timed region: the per-rank statistics summed over the
+    # process group (host side, 163 doubles).  UWVK_BENCH_COLL=rccl sums them with
+    # the engine's RCCL communicator on the handle's stream instead (slower, see
+    # init_dist); by default RCCL runs after the timed region as a cross-check.
     comm = None
-    if dist is not None and backend == "nccl":
+    coll = os.environ.get("UWVK_BENCH_COLL", "host")
+
+    def make_comm():
         uid = [engine.RcclComm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        comm = engine.RcclComm(world, uid[0], rank, local)
-    # warm the statistics kernels and the collective (module load, RCCL
-    # communicator set-up) outside the timed region
+        return engine.RcclComm(world, uid[0], rank, local)
+
+    if dist is not None and coll == "rccl":
+        comm = make_comm()
+    # warm the statistics kernels and the collective (module load, communicator
+    # set-up) outside the timed region
     st_w = f.ensemble_stats(truth, comm)
     if dist is not None and comm is None:
-        ensemble.allreduce_stats(st_w, dist)
+        ensemble.allreduce_stats(st_w, dist, device=stat_dev)
 
     def barrier():
         if dist is not None:
@@ -283,7 +292,7 @@ def main():
     # synchronous; RCCL over xGMI (comm) is the only collective of the workload
     stats = f.ensemble_stats(truth, comm)
     if dist is not None and comm is None:
-        stats = ensemble.allreduce_stats(stats, dist)
+        stats = ensemble.allreduce_stats(stats, dist, device=stat_dev)
     f.synchronize()
     barrier()
     wall = time.perf_counter() - t0
@@ -294,6 +303,13 @@ def main():
             w = w.cuda()
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
+    # untimed: the same sum through the engine's RCCL path (uwvk_pose_ensemble_allreduce)
+    rccl_check = None
+    same_dev = os.environ.get("UWVK_BENCH_SAME_DEVICE") == "1"  # RCCL refuses two ranks on one GPU
+    if dist is not None and comm is None and not same_dev and os.environ.get("UWVK_BENCH_RCCL_CHECK", "1") == "1":
+        comm = make_comm()
+        rs = f.ensemble_stats(truth, comm)
+        rccl_check = bool(np.allclose(rs, stats, rtol=1e-12, atol=1e-12))
     status = f.get_status()
     if status.any():
         print("warning: %d instances flagged (status bits)" % int((status != 0).sum()), file=sys.stderr)
@@ -347,9 +363,10 @@ def main():
                    "adcp_epochs_in_window": int(((window & 8) != 0).sum()),
                    "c4_cycle_s": list(cyc) if a.mode == "C4" else None,
                    "parallelism": "instance-sharded x%d (no data-path collective)" % world,
-                   "collective": ("RCCL all_reduce of the ensemble statistics on the handle's stream "
-                                  "(uwvk_pose_ensemble_allreduce)" if comm else
-                                  "gloo all_reduce of the ensemble statistics") if dist else None,
+                   "collective": (("RCCL all_reduce of the ensemble statistics on the handle's stream "
+                                   "(uwvk_pose_ensemble_allreduce)") if coll == "rccl" else
+                                  ("%s all_reduce of the ensemble statistics (host); untimed RCCL cross-check: %s"
+                                   % (backend, rccl_check))) if dist else None,
                    "path": "dense (all 2n+1 sigma points)" if a.dense else "PSP (partitioned sigma points)",
                    "kernel": kname},
         "roofline": roof,
