@@ -202,8 +202,13 @@ UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
 // resident waves).  amdgpu_waves_per_eu(3) also gives 156 but schedules the
 // epoch loop worse: 145.0M against 148.5M steps/s (r02 A/B), so it is not set;
 // a fully unrolled Sigma store once took the kernel to 188 (2 waves per SIMD).
+#ifdef PSP_WPE  // A/B builds only: amdgpu_waves_per_eu(PSP_WPE)
+#define PSP_EPOCH_ATTR __attribute__((amdgpu_waves_per_eu(PSP_WPE)))
+#else
+#define PSP_EPOCH_ATTR
+#endif
 template <int DOF>
-__global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
+__global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const int64_t B = b.batch, inst = xcd_instance(B);
 #ifdef UWVK_STAMPS
