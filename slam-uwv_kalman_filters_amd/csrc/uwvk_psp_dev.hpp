@@ -43,14 +43,16 @@
 // Cholesky column incl. its diagonal, 32 v_rcp_f64 + Newton for 1/d, 64 the
 // Cholesky panel read with immediate offsets from the row start, 256 the
 // update's z-bar and S sums as one LDS-transposed round (lds_sums), 512 the
-// same for the predict's ori x ori sums.
+// same for the predict's ori x ori sums, 2048 (r02) the rank-M pass over the
+// short rows 0..31 two rows per instruction (rankm_pairs: 88.4 -> 86.0 ms,
+// 148.0 -> 152.1M steps/s).
 // Measured on the C3 bench (kernel ms per 200-epoch launch): none 103.2,
 // 1-8 97.5, +16 95.4, +32 within noise, +64 94.3, +256/512 92.0.  Rejected:
 // Delta_j as LDS broadcasts instead of v_readlane (105.9), the same for Dz / P
 // (no change), lds_sums in the manifold-mean loop (+0.7%), s_setprio around
 // the Cholesky column chain (within noise).
 #ifndef PSP_FAST
-#define PSP_FAST 895
+#define PSP_FAST 2943
 #endif
 
 namespace uwvk {
@@ -882,6 +884,35 @@ UWVK_DEV void rankm_rows(double* S, const double* stg, int i0, int c0, int l, co
   }
 }
 
+// The short rows 0 .. P-1 (P = min(32, DOF), at most 32 entries each) two to an
+// instruction: lanes 0-31 take row p, lanes 32-63 row P-1-p (column l & 31),
+// so rows [0, P) cost P/2 row steps instead of P.  The uniform row offsets and
+// C~ addresses are selected per half (two broadcast addresses, one per half);
+// Kx = K~ of column l & 31.
+template <int R, int M, int P>
+UWVK_DEV void rankm_pairs(double* S, const double* stg, int p0, int l, const double (&Kx)[M]) {
+  const bool hi = l >= 32;
+  const int col = l & 31;
+  double sv[R], cv[R][M];
+  int ad[R], row[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int pa = p0 + r, pb = P - 1 - pa;
+    row[r] = hi ? pb : pa;
+    ad[r] = (hi ? pb * (pb + 1) / 2 : pa * (pa + 1) / 2) + col;
+    sv[r] = S[ad[r]];
+#pragma unroll
+    for (int a = 0; a < M; a++) cv[r][a] = stg[M * row[r] + a];
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    double s2 = sv[r];
+#pragma unroll
+    for (int a = 0; a < M; a++) s2 = fma(-cv[r][a], Kx[a], s2);
+    if (col <= row[r]) S[ad[r]] = s2;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // ukf::update [EXT], PSP form.  gate: 0 accept any, 1 d2p95.  Returns the gate
 // decision; *ok = false on a non-positive pivot of the partial Cholesky.
@@ -1106,6 +1137,43 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     Ct[i] = C[i] * ids;
     Kt[i] = Kg[i] * ids;
   }
+#if PSP_FAST & 2048
+  {
+    // rows [0, P) paired (rankm_pairs), then rows [P, DOF) one per step; the
+    // C~ rows of each part are staged in stg in turn
+    constexpr int P = DOF < 32 ? DOF : 32, NPAIR = P / 2, RB = PSP_RB;
+    static_assert(P % 2 == 0 && M * P <= PG<DOF>::STG && M * (DOF - P) <= PG<DOF>::STG, "C~ parts (PG::STG)");
+    static_assert(63 < Lay<DOF>::store + PG<DOF>::STG, "row over-read (lanes l > i, last rows) stays inside PspSmem");
+    double Kx[M];
+#pragma unroll
+    for (int a2 = 0; a2 < M; a2++) Kx[a2] = shfl_d(Kt[a2], l & 31);
+    if (l < P) {
+#pragma unroll
+      for (int a2 = 0; a2 < M; a2++) sm.stg[M * l + a2] = Ct[a2];
+    }
+    psync();
+    if (!(PSP_ABL & 2)) {
+      constexpr int NBP = NPAIR / RB, REMP = NPAIR - NBP * RB;
+#pragma unroll 1
+      for (int b = 0; b < NBP; b++) rankm_pairs<RB, M, P>(sm.S, sm.stg, b * RB, l, Kx);
+      if constexpr (REMP > 0) rankm_pairs<REMP, M, P>(sm.S, sm.stg, NBP * RB, l, Kx);
+    }
+    if constexpr (DOF > P) {
+      psync();
+      if (l >= P && l < DOF) {
+#pragma unroll
+        for (int a2 = 0; a2 < M; a2++) sm.stg[M * (l - P) + a2] = Ct[a2];
+      }
+      psync();
+      if (!(PSP_ABL & 2)) {
+        constexpr int NR2 = DOF - P, NB2 = NR2 / RB, REM2 = NR2 - NB2 * RB;
+#pragma unroll 1
+        for (int b = 0; b < NB2; b++) rankm_rows<RB, M>(sm.S, sm.stg, P + b * RB, P, l, Kt);
+        if constexpr (REM2 > 0) rankm_rows<REM2, M>(sm.S, sm.stg, P + NB2 * RB, P, l, Kt);
+      }
+    }
+  }
+#else
   {
     // C~ rows for the broadcast reads (stg is free here), in two halves of
     // rows [0, H) and [H, DOF) so that M * max(H, DOF - H) fits PG::STG
@@ -1134,6 +1202,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       if constexpr (REM > 0) rankm_rows<REM, M>(sm.S, sm.stg, NB * RB, H, l, Kt);
     }
   }
+#endif
   psync();
   UWVK_STAMP(34);
   // apply_delta, exact nav-frame form: mu <- mu [+] delta, Sigma <- T Sigma T^T
