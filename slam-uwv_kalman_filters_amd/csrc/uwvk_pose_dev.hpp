@@ -192,8 +192,70 @@ UWVK_DEV void chol_step(double (&a)[DOF], Smem<DOF>& sm, int r, bool& ok, double
   }
 }
 
+// Two-wave form (NW = 2, the 53-DOF state): wave W keeps columns [C0, C1) of
+// every row (27 + 26 doubles per lane instead of 53: no scratch spills), the
+// owner of column J scales it and publishes it through the LDS column buffer,
+// and both waves update their own later columns in parallel; one workgroup
+// barrier per column.  The same operations per entry as chol_step, so the
+// factor is bitwise the one-wave factor.
+template <int DOF, int W, int C0, int C1, int J>
+UWVK_DEV void chol2_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, double piv) {
+  if constexpr (J < DOF) {
+    constexpr int H = (DOF + 1) / 2;
+    constexpr bool own = (J < H) == (W == 0);
+    double pnext = 0.0;
+    if constexpr (own) {
+      constexpr int jj = J - C0;
+      ok = ok && (piv > 0.0);
+      const double inv = rsqrt_f64(piv);
+      const double d = piv * inv;
+      a[jj] = (r == J) ? d : a[jj] * inv;
+      if constexpr (J + 1 < C1) pnext = readlane_d(a[jj + 1] - a[jj] * a[jj], J + 1);
+      sm.col[J & 1][r] = a[jj];
+    }
+    __syncthreads();
+    const double lr = own ? a[J - C0 < 0 ? 0 : (J - C0 >= C1 - C0 ? 0 : J - C0)] : sm.col[J & 1][r];
+#pragma unroll
+    for (int c = (J + 1 > C0 ? J + 1 : C0); c < C1; c++) a[c - C0] -= lr * sm.col[J & 1][c];
+#pragma unroll
+    for (int c = (J + 1 > C0 ? J + 1 : C0); c < C1; c++) asm volatile("" : "+v"(a[c - C0]));
+    // the first column of wave 1 takes its pivot from its own updated registers
+    if constexpr (W == 1 && J + 1 == C0) pnext = readlane_d(a[0], C0);
+    chol2_step<DOF, W, C0, C1, J + 1>(a, sm, r, ok, pnext);
+  }
+}
+
+template <int DOF, int W, int C0, int C1>
+UWVK_DEV void chol2_wave(Smem<DOF>& sm) {
+  const int r = lane_id();
+  const int rr = r < DOF ? r : DOF - 1;  // lanes >= DOF shadow the last row (discarded)
+  double a[C1 - C0];
+#pragma unroll
+  for (int c = C0; c < C1; c++) a[c - C0] = sm.S[rr * DOF + c];
+  bool ok = true;
+  chol2_step<DOF, W, C0, C1, 0>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
+  if (r < DOF) {
+    const int base = r * (r + 1) / 2;
+#pragma unroll
+    for (int c = C0; c < C1; c++)
+      if (c <= r) sm.Lp[base + c] = a[c - C0];
+  }
+  if (r == 0) sm.vec[62 + W] = ok ? 1.0 : 0.0;
+}
+
 template <int DOF>
 UWVK_DEV bool chol_lds(Smem<DOF>& sm) {
+  if constexpr (Geo<DOF>::NW == 2) {
+    constexpr int H = (DOF + 1) / 2;
+    if (wid() == 0)
+      chol2_wave<DOF, 0, 0, H>(sm);
+    else
+      chol2_wave<DOF, 1, H, DOF>(sm);
+    __syncthreads();
+    const bool ok = sm.vec[62] != 0.0 && sm.vec[63] != 0.0;
+    __syncthreads();
+    return ok;
+  }
   if (wid() == 0) {
     const int r = lane_id();
     const int rr = r < DOF ? r : DOF - 1;  // lanes >= DOF shadow the last row (discarded)
