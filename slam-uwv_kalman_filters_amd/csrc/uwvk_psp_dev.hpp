@@ -31,6 +31,9 @@
 #ifndef PSP_RB
 #define PSP_RB 8          // rows per block of the row-block sweeps
 #endif
+#ifndef PSP_RBP
+#define PSP_RBP 8         // row pairs per block of the paired rank-M sweep (rankm_pairs)
+#endif
 // ablation knobs for timing analysis only (results are invalid when set):
 // PSP_ABL = bitmask: 1 mean 1 iteration, 2 no rank-m pass, 4 no L Delta / X,
 // 8 no predict Cholesky, 16 no predict points, 32 no update Cholesky, 64 no HG/C/S
@@ -1153,10 +1156,10 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     }
     psync();
     if (!(PSP_ABL & 2)) {
-      constexpr int NBP = NPAIR / RB, REMP = NPAIR - NBP * RB;
+      constexpr int RBP = PSP_RBP < NPAIR ? PSP_RBP : NPAIR, NBP = NPAIR / RBP, REMP = NPAIR - NBP * RBP;
 #pragma unroll 1
-      for (int b = 0; b < NBP; b++) rankm_pairs<RB, M, P>(sm.S, sm.stg, b * RB, l, Kx);
-      if constexpr (REMP > 0) rankm_pairs<REMP, M, P>(sm.S, sm.stg, NBP * RB, l, Kx);
+      for (int b = 0; b < NBP; b++) rankm_pairs<RBP, M, P>(sm.S, sm.stg, b * RBP, l, Kx);
+      if constexpr (REMP > 0) rankm_pairs<REMP, M, P>(sm.S, sm.stg, NBP * RBP, l, Kx);
     }
     if constexpr (DOF > P) {
       psync();
