@@ -48,14 +48,15 @@
 // update's z-bar and S sums as one LDS-transposed round (lds_sums), 512 the
 // same for the predict's ori x ori sums, 2048 (r02) the rank-M pass over the
 // short rows 0..31 two rows per instruction (rankm_pairs: 88.4 -> 86.0 ms,
-// 148.0 -> 152.1M steps/s).
+// 148.0 -> 152.1M steps/s), 4096 (r02) a fresh laundered lane id per phase
+// (PSP_PHASE: 85.8 -> 85.4 ms).
 // Measured on the C3 bench (kernel ms per 200-epoch launch): none 103.2,
 // 1-8 97.5, +16 95.4, +32 within noise, +64 94.3, +256/512 92.0.  Rejected:
 // Delta_j as LDS broadcasts instead of v_readlane (105.9), the same for Dz / P
 // (no change), lds_sums in the manifold-mean loop (+0.7%), s_setprio around
 // the Cholesky column chain (within noise).
 #ifndef PSP_FAST
-#define PSP_FAST 2943
+#define PSP_FAST 7039
 #endif
 
 namespace uwvk {
@@ -231,6 +232,20 @@ UWVK_DEV void lds_sums(const double (&v)[R], double* buf, int l, double (&out)[R
 #pragma unroll
   for (int i = 0; i < R; i++) out[i] = readlane_d(p[0], i);
 }
+
+// phase boundary: the stamp of the diagnostic build, and (PSP_FAST & 4096) a
+// fresh laundered lane id, so that lane masks are recomputed per phase (one
+// v_cmp each) instead of being kept as SGPR pairs across the epoch, where they
+// were spilled to VGPR lanes and reloaded (two v_readlane each) in every phase
+#if PSP_FAST & 4096
+#define PSP_PHASE(ph) \
+  do {                \
+    UWVK_STAMP(ph);   \
+    l = olane();      \
+  } while (0)
+#else
+#define PSP_PHASE(ph) UWVK_STAMP(ph)
+#endif
 
 UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -505,7 +520,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   using L = Lay<DOF>;
   using G = PG<DOF>;
   constexpr int K = G::KP;
-  const int l = olane();
+  int l = olane();  // re-laundered per phase (PSP_PHASE)
   const double dt = pc.dt, dt2 = dt * dt;
   // process-noise shaping from the pre-predict mean (PoseUKF.cpp:448-460)
   double qo_lane = 0.0;  // lane a*3+b (< 9) keeps (R Q_ori R^T)[a][b]
@@ -539,7 +554,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #else
   const bool ok = pchol<DOF, K, PredRows>(sm.S, l, a, ds, sm.stg);
 #endif
-  UWVK_STAMP(20);
+  PSP_PHASE(20);
   // sigma points: lanes < 2K plus the centre lane 2K; orientation output only
   const bool pt = l < 2 * K, ctr = l == 2 * K;
   double o[4];
@@ -552,7 +567,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     proc_orientation<DOF>(x, sh, pc, o);
 #endif
   }
-  UWVK_STAMP(21);
+  PSP_PHASE(21);
   // manifold mean of the orientations (ukfom: ref = X_0, Gauss-Newton, |d| <= 1e-6)
   constexpr double wc = 1.0 + 2.0 * (DOF - K);
   double mq[4];
@@ -587,7 +602,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     } while (!(PSP_ABL & 1) && nrm > 1e-6 && ++it < 10000);
 #endif
   }
-  UWVK_STAMP(22);
+  PSP_PHASE(22);
   // deviations; ori x ori block; Delta_j = d_{j+} - d_{j-}
   double d[3];
   qboxminus_psp(o, mq, d);
@@ -640,7 +655,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       X[i] = 0.5 * (cp >= 0 ? (ar * Y[i] + dt * yc) : ar * Y[i]);
     }
   }
-  UWVK_STAMP(23);
+  PSP_PHASE(23);
   // rows/cols coupled by A (pos, vel): new values into registers first.
   // Sigma[p][jl] = d_jl Sigma~[p][jl] (p, jc < 12 carry d = 1)
   constexpr int pv[6] = {0, 1, 2, 6, 7, 8};
@@ -667,7 +682,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #endif
   }
   psync();
-  UWVK_STAMP(24);
+  PSP_PHASE(24);
   // rewrite rows/cols < 9 (stored as Sigma / d'_l): A-coupled rows (pos, vel),
   // orientation rows (cross terms), ori x ori
   const bool qs = sh.q_simple != 0;
@@ -720,7 +735,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       }
     }
   }
-  UWVK_STAMP(25);
+  PSP_PHASE(25);
   // new mean: vect parts f(mu), orientation the manifold mean
   double mv = 0.0;
   if (l < L::store && !(l >= 3 && l < 7)) mv = proc_vect_lane(l, sm.mu, pc);
@@ -728,7 +743,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   if (l < L::store && !(l >= 3 && l < 7)) sm.mu[l] = mv;
   if (l < 4) sm.mu[3 + l] = mq[l];
   psync();
-  UWVK_STAMP(26);
+  PSP_PHASE(26);
   return ok;
 }
 
@@ -926,7 +941,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   using L = Lay<DOF>;
   using G = PG<DOF>;
   constexpr int M = HM::M, K = HM::K, NC = HM::NC, KA = K > 0 ? K : 1;
-  const int l = olane();
+  int l = olane();  // re-laundered per phase (PSP_PHASE)
   double a[KA];
   bool cok = true;
   if constexpr (K > 0) {
@@ -936,7 +951,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     cok = pchol<DOF, K, HM>(sm.S, l, a, ds, sm.stg);
 #endif
   }
-  UWVK_STAMP(30);
+  PSP_PHASE(30);
   const bool pt = l < 2 * K;
   double zp[M];
   {
@@ -1060,7 +1075,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     }
   }
 #endif
-  UWVK_STAMP(31);
+  PSP_PHASE(31);
   const int rl = l < DOF ? l : DOF - 1;
   double Gr[M];
 #pragma unroll
@@ -1074,7 +1089,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   }
 #pragma unroll
   for (int i = 0; i < M; i++) Gr[i] = Gr[i] * ds;  // Sigma[r][c] = d_r d_c Sigma~[r][c]
-  UWVK_STAMP(32);
+  PSP_PHASE(32);
   // Glin_r = G_r - sum_j L[r][j] P[:, j]: row r of (Sigma - L_a L_a^T) H^T;
   // C_r = Glin_r + 1/2 sum_j L[r][j] Dz_j; S += H Glin + R  (H Glin = H Sigma H^T - P P^T)
   double Gl[M], C[M];
@@ -1126,7 +1141,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   *ok = cok;
   const bool accept = gate == 0 ? true : !(d2 > kD2P95);
   if (!accept) return false;
-  UWVK_STAMP(33);
+  PSP_PHASE(33);
   // Sigma -= C K^T: row sweep (rankm_rows), lane = column j holds K_j, C_i is
   // an LDS broadcast; each block's loads precede its stores.  delta = K nu (lane r).
   psync();
@@ -1207,7 +1222,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   }
 #endif
   psync();
-  UWVK_STAMP(34);
+  PSP_PHASE(34);
   // apply_delta, exact nav-frame form: mu <- mu [+] delta, Sigma <- T Sigma T^T
   {
     const double dv[3] = {readlane_d(dl, 3), readlane_d(dl, 4), readlane_d(dl, 5)};
@@ -1253,7 +1268,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     if (l < 4) sm.mu[3 + l] = qn[l];
     psync();
   }
-  UWVK_STAMP(35);
+  PSP_PHASE(35);
   return true;
 }
 
