@@ -190,11 +190,26 @@ __global__ __launch_bounds__(64) void k_psp_update(PoseBufs b, PoseShared sh, Me
 }
 
 // batch-shared parameters read through a pointer laundered once per epoch:
-// nothing derived from them is hoisted out of the epoch loop (VGPR pressure)
+// nothing derived from them is hoisted out of the epoch loop (VGPR pressure).
+// The pointer is laundered in the constant address space: laundered as a
+// generic pointer, every field read became a flat_load followed by
+// s_waitcnt vmcnt(0) lgkmcnt(0) (a memory round trip on the epoch's critical
+// path, which also drained the input prefetch); as a constant-space pointer
+// the reads are scalar loads through the scalar cache.
+#ifndef PSP_SHARED_CONST
+#define PSP_SHARED_CONST 1
+#endif
 UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
+#if PSP_SHARED_CONST
+  using CP = const __attribute__((address_space(4))) PoseShared*;
+  CP p = (CP)b.shared;
+  asm volatile("" : "+s"(p));
+  return *(const PoseShared*)p;
+#else
   const PoseShared* p = b.shared;
   asm volatile("" : "+s"(p));
   return *p;
+#endif
 }
 
 // Needs <= 168 VGPRs (3 waves per SIMD: with 12 instances per CU from the LDS
