@@ -686,22 +686,35 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   // rewrite rows/cols < 9 (stored as Sigma / d'_l): A-coupled rows (pos, vel),
   // orientation rows (cross terms), ori x ori
   const bool qs = sh.q_simple != 0;
-  if (l < DOF && !(l >= 3 && l < 6)) {
-    const bool jpv = jc >= 0;
-    const double2* f2 = reinterpret_cast<const double2*>(fq);
+  // the lane-resident Q (qs, a uniform branch) needs no global load: the
+  // dt^2 Q table is read only for a general Q (a load under a per-lane select
+  // was issued anyway and waited for on the critical path)
+  auto rows_lt9 = [&](auto QS) {
+    constexpr bool kQS = decltype(QS)::value;
+    if (l < DOF && !(l >= 3 && l < 6)) {
+      const bool jpv = jc >= 0;
+      const double2* f2 = reinterpret_cast<const double2*>(fq);
 #pragma unroll
-    for (int q = 0; q < 6; q++)
-      if (!jpv || l <= pv[q]) {
-        const int e = pidx(pv[q], l);
-        const double qq = qs ? (l == pv[q] ? lq.q0 : 0.0) : f2[e].y;
-        sm.S[e] = (nv[q] + qq) * ids;
+      for (int q = 0; q < 6; q++)
+        if (!jpv || l <= pv[q]) {
+          const int e = pidx(pv[q], l);
+          double qq;
+          if constexpr (kQS) qq = (l == pv[q]) ? lq.q0 : 0.0;
+          else qq = f2[e].y;
+          sm.S[e] = (nv[q] + qq) * ids;
+        }
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        const int e = pidx(3 + i, l);
+        if constexpr (kQS) sm.S[e] = X[i] * ids;
+        else sm.S[e] = (X[i] + f2[e].y) * ids;
       }
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-      const int e = pidx(3 + i, l);
-      sm.S[e] = (X[i] + (qs ? 0.0 : f2[e].y)) * ids;
     }
-  }
+  };
+  if (qs)
+    rows_lt9(std::true_type{});
+  else
+    rows_lt9(std::false_type{});
   if (l < 9 && (l / 3) >= (l % 3)) {
     const int a2 = l / 3, b2 = l % 3;
     sm.S[pidx(3 + a2, 3 + b2)] = sel6(oo[0], oo[1], oo[2], oo[3], oo[4], oo[5], a2 * (a2 + 1) / 2 + b2) + dt2 * qo_lane;
@@ -720,7 +733,11 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       const int j = l - k;
       if (l >= R0 && l < DOF && j >= R0 && k <= bw) {
         const int e = pidx(l, j);
-        double q = qs ? (k == 0 ? lq.q0 : (k == 1 ? lq.q1 : lq.q2)) : f2[e].y;
+        double q;
+        if (qs)
+          q = k == 0 ? lq.q0 : (k == 1 ? lq.q1 : lq.q2);
+        else
+          q = f2[e].y;
         if (k == 0 && l >= L::d_wv && l < L::d_wv + 4) q = dt2 * (sh.q_wv[l - L::d_wv] + wv_add);
         if (q != 0.0) sm.S[e] += q * (ids * idk);
       }
