@@ -88,6 +88,8 @@ def parse():
     ap.add_argument("--vel-groups", type=int, default=-1, help="C2: -1 auto, 0 lane per filter, 1 16-lane rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true", help="literal kernels (all 2n+1 sigma points)")
+    ap.add_argument("--tail-slots", type=int, default=0,
+                    help="UWVK_OPT_TAIL_SLOTS: 0 runtime occupancy, > 0 blocks per XCD, < 0 no tail spreading")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core available to this process")
     return ap.parse_args()
 
@@ -245,6 +247,7 @@ def main():
     cyc = tuple(float(v) for v in a.c4_cycle.split(","))
     log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, a.mode, a.dof, first_instance=rank * B, c4_cycle=cyc)
     f = engine.PoseUKFBatch(B, a.dof, device=local)
+    f.set_tail_slots(a.tail_slots)
     if a.dense:
         f.set_dense_sigma(True)
     f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)

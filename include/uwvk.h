@@ -52,6 +52,7 @@ typedef enum uwvk_status {
 #define UWVK_ST_NOTPD 0x1u    /* Cholesky of Sigma failed (non-positive pivot) */
 #define UWVK_ST_NAN 0x2u      /* non-finite measurement skipped for this instance */
 #define UWVK_ST_NONFINITE 0x4u/* non-finite state after a step */
+#define UWVK_ST_SCHEDULE 0x8u /* engine fault: a tail-chunk hand-off timed out (see UWVK_OPT_TAIL_SLOTS) */
 
 /* ---- PoseState layout (src/PoseState.hpp:29-45) ------------------------ */
 /* Full layout: 53 DOF, 54 stored scalars (SO3 as a quaternion).           */
@@ -377,7 +378,24 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   1 propagates all 2n+1 sigma points (MFMA covariance GEMM).  Setting
  *   UWVK_OPT_LITERAL_APPLY_DELTA also selects the literal kernels. */
 #define UWVK_OPT_DENSE_SIGMA 2
+/* UWVK_OPT_TAIL_SLOTS: last-generation spreading of the PSP run_log launch.
+ *   When batch / 8 instances per XCD leave a partial last generation of the
+ *   XCD's resident blocks, those tail instances run as a few epoch chunks
+ *   handed from block to block (Sigma~ and its time scale unfolded, so the
+ *   result is bitwise the one-block run), spread over the slots that would
+ *   idle.  0 (default): plan for the occupancy the runtime reports; > 0: plan
+ *   for that many resident blocks per XCD (tests); < 0: off.  Needs
+ *   batch % 8 == 0. */
+#define UWVK_OPT_TAIL_SLOTS 3
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
+/* Host-only query (no device work): the chunks per tail instance the
+ * UWVK_OPT_TAIL_SLOTS planner picks for one XCD's instances over its resident
+ * blocks in an epochs-long launch; 1 = no spreading. */
+int uwvk_pose_tail_chunks(int64_t instances_per_xcd, int64_t slots_per_xcd, int64_t epochs);
+/* Resident PSP epoch-kernel blocks per XCD the runtime reports for this dof on
+ * device (occupancy x CUs / 8; what UWVK_OPT_TAIL_SLOTS = 0 plans for), 0 if
+ * unknown. */
+int64_t uwvk_pose_resident_slots(int dof, int device);
 
 /* Kernel-timing helper: HIP events recorded on the handle's stream. */
 uwvk_status uwvk_pose_timer_start(uwvk_pose* h);

@@ -7,6 +7,8 @@
 //   RotationRate -> predictionStep(dt) -> Acceleration update
 //   [-> Velocity (DVL) -> Pressure -> ADCP cells -> BodyEfforts]
 // with Sigma resident in LDS across all steps of the epoch.
+#include <array>
+#include <map>
 #include "uwvk_pose_kernels.hpp"
 #include "uwvk_psp.hpp"
 #include "uwvk_host.hpp"
@@ -51,6 +53,13 @@ struct uwvk_pose {
   uwvk_uwv_params uwv{};
   bool has_state = false, has_Q = false;
   int dense = 0;  // UWVK_OPT_DENSE_SIGMA
+  // last-generation spreading of the PSP epoch launch (UWVK_OPT_TAIL_SLOTS)
+  int64_t tail_slots = 0;  // resident blocks per XCD to plan for: 0 auto, < 0 off
+  std::map<std::array<int64_t, 3>, int> tail_chunks;  // (instances per XCD, slots, epochs) -> chunks
+  uint32_t* d_tail_flag = nullptr;  // per tail instance (batch / 8 - 1 per XCD at most)
+  double* d_tail_carry = nullptr;   // per tail instance: 64 x (ds, ids)
+  int64_t tail_inst_cap = 0;
+  uint32_t tail_tag = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   aug::VisStage vis;  // visual-landmark update staging
 };
@@ -222,7 +231,8 @@ void uwvk_pose_destroy(uwvk_pose* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_Q, (void*)h->d_rot, (void*)h->d_off,
                   (void*)h->d_model, (void*)h->d_uwv, (void*)h->d_status, (void*)h->d_meas, (void*)h->d_mask,
-                  (void*)h->d_accepted, (void*)h->d_scratch, (void*)h->d_shared, (void*)h->d_Qp, (void*)h->d_qband})
+                  (void*)h->d_accepted, (void*)h->d_scratch, (void*)h->d_shared, (void*)h->d_Qp, (void*)h->d_qband,
+                  (void*)h->d_tail_flag, (void*)h->d_tail_carry})
     if (p) (void)hipFree(p);
   h->vis.release();
   if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -525,6 +535,56 @@ uwvk_status uwvk_pose_get_status(uwvk_pose* h, uint32_t* status, int clear) {
   return UWVK_OK;
 }
 
+// the tail layout of one PSP epoch launch (uwvk_psp_k.hip, plan_tail), cached
+// per (instances per XCD, slots, epochs); fills ea's tail fields and the grid
+static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
+  ea.chunks = 1;
+  grid = 0;
+  if (h->tail_slots < 0 || h->batch % 8 != 0) return hipSuccess;
+  const int64_t n = h->batch / 8;
+  const int64_t s = h->tail_slots > 0 ? h->tail_slots : psp_epoch_slots_per_xcd(h->dof, h->device);
+  const std::array<int64_t, 3> key{n, s, ea.count};
+  auto it = h->tail_chunks.find(key);
+  if (it == h->tail_chunks.end()) {
+    if (h->tail_chunks.size() >= 64) h->tail_chunks.clear();
+    it = h->tail_chunks.emplace(key, plan_tail(n, s, ea.count)).first;
+  }
+  const int c = it->second;
+  if (c <= 1) return hipSuccess;
+  const int64_t r = c * s;
+  if (8 * r > h->tail_inst_cap) {  // sized once for the largest plan (8 chunks) of these slots
+    // the previous buffers may still be read by a queued launch
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return e;
+    if (h->d_tail_flag) (void)hipFree(h->d_tail_flag);
+    if (h->d_tail_carry) (void)hipFree(h->d_tail_carry);
+    h->d_tail_flag = nullptr;
+    h->d_tail_carry = nullptr;
+    h->tail_inst_cap = 0;
+    const int64_t cap = 8 * std::max<int64_t>(r, 8 * s);
+    e = hipMalloc(&h->d_tail_flag, (size_t)cap * 4);
+    if (e == hipSuccess) e = hipMalloc(&h->d_tail_carry, (size_t)cap * 128 * 8);
+    if (e == hipSuccess) e = hipMemsetAsync(h->d_tail_flag, 0, (size_t)cap * 4, h->stream);
+    if (e != hipSuccess) return e;
+    h->tail_inst_cap = cap;
+    h->tail_tag = 0;
+  }
+  if (++h->tail_tag >= (1u << 27)) {  // flags hold tag * 16 + chunks done: restart on zeroed flags
+    hipError_t e = hipMemsetAsync(h->d_tail_flag, 0, (size_t)h->tail_inst_cap * 4, h->stream);
+    if (e != hipSuccess) return e;
+    h->tail_tag = 1;
+  }
+  ea.tail_flag = h->d_tail_flag;
+  ea.tail_carry = h->d_tail_carry;
+  ea.n_x = n;
+  ea.tail0 = n - r;
+  ea.r_x = r;
+  ea.chunks = c;
+  ea.tag = h->tail_tag;
+  grid = 8 * (n + (c - 1) * r);
+  return hipSuccess;
+}
+
 uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t first, int64_t count,
                               uint32_t* accept_counts) {
   if (!h || !log || first < 0 || count < 0 || first + count > log->epochs || log->adcp_cells > 8) return UWVK_EINVAL;
@@ -574,7 +634,9 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     ea.first = e;
     ea.count = last - e;
     ea.efforts_only = 0;
-    HIPCHK(launch_psp_epoch(h->dof, h->stream, b, sh, ea));
+    int64_t grid = 0;
+    HIPCHK(prepare_tail(h, ea, grid));
+    HIPCHK(launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid));
     if (r < first + count) {
       ea.first = r;
       ea.count = 1;
@@ -622,7 +684,20 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
     h->dense = value ? 1 : 0;
     return UWVK_OK;
   }
+  if (option == UWVK_OPT_TAIL_SLOTS) {
+    h->tail_slots = value;
+    return UWVK_OK;
+  }
   return UWVK_EINVAL;
+}
+
+int64_t uwvk_pose_resident_slots(int dof, int device) {
+  if (dof != 53 && dof != 26) return 0;
+  return psp_epoch_slots_per_xcd(dof, device);
+}
+
+int uwvk_pose_tail_chunks(int64_t instances_per_xcd, int64_t slots_per_xcd, int64_t epochs) {
+  return plan_tail(instances_per_xcd, slots_per_xcd, epochs);
 }
 
 uwvk_status uwvk_pose_timer_start(uwvk_pose* h) {

@@ -46,6 +46,19 @@ struct EpochArgs {
   // literal epoch kernel only: run just the BodyEfforts update of each epoch
   // (the PSP launch before it has done the epoch's predict and other updates)
   int efforts_only;
+  // PSP epoch kernel, last-generation spreading (uwvk_psp_k.hip, plan_tail):
+  // chunks <= 1 = one block per instance over [first, first + count).
+  // Otherwise block b runs on XCD x = b & 7 at position i = b >> 3: whole
+  // instance x n_x + i for i < tail0, else chunk k = (i - tail0) / r_x of tail
+  // instance x n_x + tail0 + (i - tail0) % r_x, handed on through tail_flag /
+  // tail_carry
+  uint32_t* tail_flag;  // per tail instance: tag * 16 + chunks done
+  double* tail_carry;   // per tail instance: the time scale (ds, ids) per lane
+  int64_t n_x;          // instances per XCD
+  int64_t tail0;        // first tail instance (XCD-local) = n_x - r_x
+  int64_t r_x;          // tail instances per XCD (chunks x resident blocks)
+  int chunks;
+  uint32_t tag;         // per launch
 };
 
 // host-callable launchers (grid = one workgroup per instance)

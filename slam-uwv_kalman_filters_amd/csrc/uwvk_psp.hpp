@@ -6,5 +6,13 @@ namespace uwvk {
 hipError_t launch_psp_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt);
 hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                              const MeasArgs& ma, int m);
-hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea);
+#include <vector>
+// grid 0: one block per instance; otherwise 8 (n_x + (chunks - 1) r_x)
+hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
+                            int64_t grid = 0);
+// resident k_psp_epoch blocks per XCD (occupancy x CUs / 8), 0 if unknown
+int64_t psp_epoch_slots_per_xcd(int dof, int device);
+// chunks per tail instance for one XCD's n instances over s resident blocks in
+// a count-epoch launch (1: no tail spreading)
+int plan_tail(int64_t n, int64_t s, int64_t count);
 }  // namespace uwvk

@@ -8,6 +8,9 @@
 // The host splits a launch after each BodyEfforts epoch (this kernel runs that
 // epoch's predict and other updates) and runs the efforts update alone on the
 // literal k_pose_efforts_epoch, whose HBM layout is shared.
+#include <algorithm>
+#include <vector>
+
 #define UWVK_POSE_KERNEL_BODIES
 #include "uwvk_pose_kernels.hpp"
 #include "uwvk_psp_dev.hpp"
@@ -25,6 +28,57 @@ UWVK_DEV void tl_mark(int64_t w, int k) {
   if (lane_id() == 0 && w < 131072) uwvk_timeline[w * 8 + k] = t;
 }
 #endif
+
+// tail-chunk hand-off (EpochArgs::chunks > 1).  Chunk k of a tail instance is
+// placed later in its XCD's block order than chunk k - 1 (plan_tail), and
+// blocks are dispatched in order, so the block waited for is resident or done:
+// the wait cannot deadlock.  The bound (about 4 s) only keeps a broken
+// ordering from hanging the device; it flags the instance and goes on.
+struct TailUnit {
+  int64_t inst, e0, e1, tslot;
+  int chunk;  // >= 0: a chunk of a tail instance
+};
+UWVK_DEV TailUnit tail_unit(const EpochArgs& ea, int64_t B) {
+  TailUnit u{xcd_instance(B), ea.first, ea.first + ea.count, 0, -1};
+  if (ea.chunks > 1) {
+    const int64_t x = blockIdx.x & 7, i = blockIdx.x >> 3;
+    if (i < ea.tail0) {
+      u.inst = x * ea.n_x + i;
+    } else {
+      const uint32_t q = (uint32_t)(i - ea.tail0), m = (uint32_t)ea.r_x;
+      const uint32_t k = q / m, t = q - k * m;
+      u.inst = x * ea.n_x + ea.tail0 + t;
+      u.chunk = (int)k;
+      u.tslot = x * ea.r_x + t;
+      u.e0 = ea.first + ea.count * k / ea.chunks;
+      u.e1 = ea.first + ea.count * (k + 1) / ea.chunks;
+    }
+  }
+  return u;
+}
+
+__device__ __attribute__((noinline)) void tail_wait(const EpochArgs& ea, int64_t t, int chunk, uint32_t* status) {
+  if (lane_id() == 0) {
+    const uint32_t want = ea.tag * 16u + (uint32_t)chunk;
+    uint32_t* f = ea.tail_flag + t;
+    int n = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want && ++n < (1 << 20))
+      __builtin_amdgcn_s_sleep(64);
+    if (n >= (1 << 20)) *status |= UWVK_ST_SCHEDULE;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous chunk's stores, from any CU
+}
+__device__ __attribute__((noinline)) double2 tail_carry_in(const EpochArgs& ea, int64_t t) {
+  return reinterpret_cast<const double2*>(ea.tail_carry)[t * 64 + lane_id()];
+}
+UWVK_DEV void tail_signal(const EpochArgs& ea, int64_t t, int chunk) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every lane's Sigma~ / mu / carry / rot stores first
+  __builtin_amdgcn_wave_barrier();
+  if (lane_id() == 0)
+    __hip_atomic_store(ea.tail_flag + t, ea.tag * 16u + (uint32_t)(chunk + 1), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
 
 template <int DOF>
 UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
@@ -225,7 +279,10 @@ UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
 template <int DOF>
 __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
-  const int64_t B = b.batch, inst = xcd_instance(B);
+  const int64_t B = b.batch;
+  TailUnit tu = tail_unit(ea, B);
+  const int64_t inst = tu.inst, e_begin = tu.e0, e_end = tu.e1;
+  if (tu.chunk > 0) tail_wait(ea, tu.tslot, tu.chunk, b.status + inst);
 #ifdef UWVK_STAMPS
   Stamper stamper;
   Stamper* st = &stamper;
@@ -247,6 +304,11 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
 #endif
   UWVK_STAMP(40);
   double ds = 1.0, ids = 1.0;  // time scale of the Markov DOFs (Sigma = D Sigma~ D)
+  if (tu.chunk > 0) {  // the previous chunk's, unfolded: bitwise the one-block run
+    const double2 c = tail_carry_in(ea, tu.tslot);
+    ds = c.x;
+    ids = c.y;
+  }
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
   bool ok = true, nan = false;
   uint32_t cnt[4] = {0, 0, 0, 0};
@@ -262,7 +324,6 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
   // latency overlaps this epoch's arithmetic)
   uint32_t fl_n = 0;
   double g_n[3] = {0, 0, 0}, a_n[3] = {0, 0, 0};
-  const int64_t e_end = ea.first + ea.count;
   auto fetch = [&](int64_t e) {
     fl_n = ea.flags[e];
 #pragma unroll
@@ -271,9 +332,9 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
       a_n[k] = ea.acc[(e * B + inst) * 3 + k];
     }
   };
-  if (ea.count > 0) fetch(ea.first);
+  if (e_end > e_begin) fetch(e_begin);
 #pragma unroll 1
-  for (int64_t e = ea.first; e < e_end; e++) {
+  for (int64_t e = e_begin; e < e_end; e++) {
     const uint32_t fl = fl_n;
     const double g[3] = {g_n[0], g_n[1], g_n[2]}, za[3] = {a_n[0], a_n[1], a_n[2]};
     if (e + 1 < e_end) fetch(e + 1);
@@ -328,7 +389,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
   if (lane_id() == 0) {
     if (!ok) b.status[inst] |= UWVK_ST_NOTPD;
     if (nan) b.status[inst] |= UWVK_ST_NAN;
-    if (ea.count > 0) {
+    if (e_end > e_begin) {
       b.rot[inst * 3] = w[0]; b.rot[inst * 3 + 1] = w[1]; b.rot[inst * 3 + 2] = w[2];
     }
     if (ea.accept_counts)
@@ -337,8 +398,18 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
 #ifdef UWVK_TIMELINE
   tl_mark(blockIdx.x, 2);
 #endif
-  psp_fold<DOF>(sm, ds, ids);
+  tu = tail_unit(ea, B);  // re-read, not kept live through the epochs
+  const bool hand = tu.chunk >= 0 && tu.chunk + 1 < ea.chunks;
+  if (hand) {  // hand on: Sigma~ and d unfolded
+    double* c = ea.tail_carry + (tu.tslot * 64 + lane_id()) * 2;
+    c[0] = ds;
+    c[1] = ids;
+    psync();
+  } else {
+    psp_fold<DOF>(sm, ds, ids);
+  }
   store_psp<DOF>(sm, b, inst);
+  if (hand) tail_signal(ea, tu.tslot, tu.chunk);
 #ifdef UWVK_TIMELINE
   __builtin_amdgcn_s_waitcnt(0);
   tl_mark(blockIdx.x, 3);
@@ -378,12 +449,57 @@ hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& 
   return dof == 53 ? psp_update_dof<53>(kind, st, b, sh, ma, m) : psp_update_dof<26>(kind, st, b, sh, ma, m);
 }
 
-hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea) {
+hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
+                            int64_t grid) {
+  const dim3 g((unsigned)(grid > 0 ? grid : b.batch));
   if (dof == 53)
-    hipLaunchKernelGGL(psp::k_psp_epoch<53>, dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, ea);
+    hipLaunchKernelGGL(psp::k_psp_epoch<53>, g, dim3(64), 0, st, b, sh, ea);
   else
-    hipLaunchKernelGGL(psp::k_psp_epoch<26>, dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, ea);
+    hipLaunchKernelGGL(psp::k_psp_epoch<26>, g, dim3(64), 0, st, b, sh, ea);
   return hipGetLastError();
+}
+
+int64_t psp_epoch_slots_per_xcd(int dof, int device) {
+  int per_cu = 0, cus = 0;
+  const void* k = dof == 53 ? (const void*)psp::k_psp_epoch<53> : (const void*)psp::k_psp_epoch<26>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return 0;
+  return (int64_t)per_cu * cus / 8;
+}
+
+// Last-generation spreading.  Blocks of one XCD are dispatched in order to
+// its s resident slots; wave speeds differ (the first generation's waves end
+// anywhere between 0.8 and 1.25 of the mean), so after a few generations the
+// slots free up at scattered times and a launch of whole-instance blocks of
+// duration D ends with a ramp: the slots idle for D / 2 on average while the
+// last blocks finish.  Spreading ends the launch on short blocks instead: the
+// last m = C s instances of each XCD run as C epoch chunks, grouped by chunk
+// (all chunk-0 blocks after the whole instances, then all chunk-1 blocks,
+// ...), so each group keeps the XCD busy for about D and a chunk's
+// predecessor, m blocks earlier, has long finished; the ramp shrinks to
+// D / (2 C), for (C - 1) m extra block prologues and epilogues (Sigma~ and
+// its time scale reloaded and stored, the IMU prefetch restarted: about 0.75
+// epoch each, r02 timeline).  C minimises
+// count / (2 C) + 0.3 C (C - 1) epochs; none below a 10 % gain or when the
+// XCD has under (C + 1) s instances.
+#ifndef PSP_TAIL_OVH
+#define PSP_TAIL_OVH 0.75
+#endif
+int plan_tail(int64_t n, int64_t s, int64_t count) {
+  if (s <= 0 || count < 4) return 1;
+  const double base = 0.5 * (double)count;
+  double best = 0.9 * base;
+  int chunks = 1;
+  for (int c = 2; c <= 8 && 2 * c <= count; c++) {
+    if (n < (c + 1) * s) break;
+    const double cost = (double)count / (2.0 * c) + PSP_TAIL_OVH * c * (c - 1);
+    if (cost < best) {
+      best = cost;
+      chunks = c;
+    }
+  }
+  return chunks;
 }
 
 }  // namespace uwvk

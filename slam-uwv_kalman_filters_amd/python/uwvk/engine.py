@@ -43,6 +43,7 @@ SYMBOLS = [
     "uwvk_ipose_create", "uwvk_ipose_destroy", "uwvk_ipose_stream", "uwvk_ipose_init",
     "uwvk_ipose_set_pose_reference", "uwvk_ipose_predict", "uwvk_ipose_update_visual",
     "uwvk_ipose_get_corrected_pose", "uwvk_ipose_get_state", "uwvk_ipose_get_status",
+    "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots",
 ]
 
 _LIB = None
@@ -71,6 +72,9 @@ def lib(path=None):
         L.uwvk_vel_destroy.argtypes = [VP]
         L.uwvk_comm_destroy.argtypes = [VP]
         L.uwvk_device_free.argtypes = [VP]
+        L.uwvk_pose_tail_chunks.argtypes = [C.c_int64, C.c_int64, C.c_int64]
+        L.uwvk_pose_resident_slots.argtypes = [C.c_int, C.c_int]
+        L.uwvk_pose_resident_slots.restype = C.c_int64
         L.uwvk_memcpy_h2d.argtypes = [VP, VP, C.c_size_t]
         L.uwvk_memcpy_d2h.argtypes = [VP, VP, C.c_size_t]
         L.uwvk_memcpy_h2d_on.argtypes = [VP, VP, C.c_size_t, VP]
@@ -154,6 +158,11 @@ class PoseUKFBatch:
     def set_dense_sigma(self, on=True):
         """Propagate all 2n+1 sigma points (literal kernels) instead of the PSP form."""
         _chk(self.L.uwvk_pose_set_option(self.h, 2, int(bool(on))), "set_option")
+
+    def set_tail_slots(self, slots):
+        """Last-generation spreading of run_log (UWVK_OPT_TAIL_SLOTS): 0 plans for
+        the runtime's occupancy, > 0 for that many resident blocks per XCD, < 0 off."""
+        _chk(self.L.uwvk_pose_set_option(self.h, 3, int(slots)), "set_option")
 
     def set_literal_apply_delta(self, on=True):
         """ukfom's literal apply_delta re-spread instead of the exact T Sigma T^T form."""

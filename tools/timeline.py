@@ -21,11 +21,17 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--out", default="")
+    ap.add_argument("--tail-slots", type=int, default=0)
     a = ap.parse_args()
     B, E = a.batch, a.steps
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     log = synth.make_pose_log(B, E + 5, "C3")
     f = engine.PoseUKFBatch(B)
+    f.set_tail_slots(a.tail_slots)
+    L0 = engine.lib()
+    s_x = L0.uwvk_pose_resident_slots(53, 0)
+    ch = L0.uwvk_pose_tail_chunks(B // 8, a.tail_slots or s_x, E) if a.tail_slots >= 0 else 1
+    print("resident slots per XCD (runtime): %d; tail_slots %d; chunks %d" % (s_x, a.tail_slots, ch))
     f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
     f.set_process_noise_from_config(cfg, log["dt"])
     d = f.upload_log(log)
@@ -34,10 +40,12 @@ def main():
     f.run_log(d, 5, E, sync=False)
     ms = f.timer_stop()
     L = engine.lib()
-    n = min(B, 131072)
+    n = min(B + 8 * (ch - 1) * ch * (a.tail_slots or s_x), 131072)  # spread launches: 8 (c - 1) r_x more blocks
     buf = np.zeros(n * 8, np.uint64)
     assert L.uwvk_debug_read_timeline(buf.ctypes.data_as(C.c_void_p), C.c_longlong(n * 8)) == 0
     t = buf.reshape(n, 8)
+    t = t[t[:, 3] != 0]  # blocks that ran
+    n = len(t)
     ts = t[:, :4].astype(np.int64)
     t0 = ts[:, 0].min()
     rel = (ts - t0) * 10e-3  # 100 MHz realtime counter -> us
@@ -66,6 +74,12 @@ def main():
     if gaps:
         print("  per-CU refill gap (end of wave -> start of the 12th-next): median %.2f us" % np.median(gaps))
     print("  start spread of the first 3072 waves: %.2f us" % np.sort(rel[:, 0])[3071])
+    for x in range(8):
+        m = xcc == x
+        if m.any():
+            e = np.sort(rel[m, 3])
+            print("  XCC %d: %5d blocks, last end %8.1f us, 95%% of ends by %8.1f us, mean duration %6.1f us" %
+                  (x, m.sum(), e[-1], e[int(0.95 * (len(e) - 1))], (rel[m, 3] - rel[m, 0]).mean()))
     if a.out:
         np.savez_compressed(a.out, rel=rel.astype(np.float32), cu=cu, xcc=xcc, inst=t[:, 5].astype(np.int64), ms=ms)
 
