@@ -35,9 +35,13 @@ busy, d2, rows_busy = last("sq_busy")
 fetch, d3, rows_f = last("fetch")
 write, d4, rows_w = last("write")
 waves = mix["SQ_WAVES"]
-we = waves * steps
+# normalised per instance-epoch: one wave per instance, except that the tail
+# instances of a spread launch (UWVK_OPT_TAIL_SLOTS) run as several chunk
+# waves, so SQ_WAVES exceeds the batch; "per_wave_epoch" keeps its r02 name
+instances = int(workload.rsplit("-b", 1)[1])
+we = instances * steps
 e = {
-    "kernel": KERNEL, "epochs_per_launch": steps, "waves": waves,
+    "kernel": KERNEL, "epochs_per_launch": steps, "waves": waves, "instances": instances,
     "fetch_size_kib_raw": fetch["FETCH_SIZE"], "write_size_kib_raw": write["WRITE_SIZE"],
     "fetch_bytes": fetch["FETCH_SIZE"] * 1024 * 2, "write_bytes": write["WRITE_SIZE"] * 1024,
 }
