@@ -118,6 +118,9 @@ struct alignas(16) Smem {
   double vec[64];          // broadcast vectors (sums, delta)
   double red[2][24];       // cross-wave partial sums
   double qori[9];          // R Q_ori R^T for the predict
+  // ref .. red as one scratch run (the update's Dz staging, when none of them is live)
+  static constexpr int kScratch = 56 + 2 * 64 + 64 + 2 * 24;
+  UWVK_DEV double* scratch() { return ref; }
 };
 
 UWVK_DEV int tid() { return threadIdx.x; }
@@ -225,6 +228,73 @@ UWVK_DEV void chol2_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, d
   }
 }
 
+// The same two-wave factor with up to UWVK_CHOL_GROUP columns per barrier
+// (columns J .. J+g-1 of one owner): the owner takes each pivot in turn from
+// its own lanes (readlane), scales the column and applies it to the group's
+// later columns (L[m][k] by readlane), then publishes the g columns; after the
+// barrier every wave applies them in order to its later columns.  Each entry
+// sees the same fused multiply-adds in the same order as in chol2_step, so the
+// factor is bitwise the one-column-per-barrier factor (tools/diag_lib_bitwise.py)
+// with 18 barriers instead of 53 at g = 3.  S counts barriers (the buffer set);
+// the 2 x g 64-double column buffers live in the factor region sm.Lp, which
+// takes the factor only after the last barrier (no buffer is read after it).
+#ifndef UWVK_CHOL_GROUP
+#define UWVK_CHOL_GROUP 3
+#endif
+template <int DOF, int J, int GS>
+constexpr int chol_group() {  // columns J .. J+g-1 with one owner (the halves of the two waves)
+  constexpr int H = (DOF + 1) / 2;
+  int g = 1;
+  while (g < GS && J + g < DOF && ((J < H) == (J + g < H))) g++;
+  return g;
+}
+template <int DOF, int W, int C0, int C1, int J, int S>
+UWVK_DEV void chol2g_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, double piv) {
+  if constexpr (J < DOF) {
+    constexpr int H = (DOF + 1) / 2;
+    constexpr bool own = (J < H) == (W == 0);
+    constexpr int g = chol_group<DOF, J, UWVK_CHOL_GROUP>();
+    constexpr int b0 = (S & 1) * UWVK_CHOL_GROUP;
+    constexpr int JN = J + g;  // first column after this step
+    static_assert(Geo<DOF>::LPSZ >= 2 * UWVK_CHOL_GROUP * 64, "column buffers in the factor region");
+    double* buf = sm.Lp + b0 * 64;
+    if constexpr (own) {
+      constexpr int jj = J - C0;
+#pragma unroll
+      for (int k = 0; k < g; k++) {
+        const double p = k == 0 ? piv : readlane_d(a[jj + k], J + k);
+        ok = ok && (p > 0.0);
+        const double inv = rsqrt_f64(p);
+        const double d = p * inv;
+        a[jj + k] = (r == J + k) ? d : a[jj + k] * inv;
+        buf[k * 64 + r] = a[jj + k];
+#pragma unroll
+        for (int m = k + 1; m < g; m++) {
+          const double lmk = readlane_d(a[jj + k], J + m);  // L[J+m][J+k]
+          a[jj + m] -= a[jj + k] * lmk;
+          asm volatile("" : "+v"(a[jj + m]));
+        }
+      }
+    }
+    __syncthreads();
+    constexpr int cs = JN > C0 ? JN : C0;
+    if constexpr (cs < C1) {
+#pragma unroll
+      for (int k = 0; k < g; k++) {
+        const double lk = own ? a[(J + k - C0) >= 0 && (J + k - C0) < (C1 - C0) ? J + k - C0 : 0] : buf[k * 64 + r];
+#pragma unroll
+        for (int c = cs; c < C1; c++) a[c - C0] -= lk * buf[k * 64 + c];
+      }
+#pragma unroll
+      for (int c = cs; c < C1; c++) asm volatile("" : "+v"(a[c - C0]));
+    }
+    // the next pivot: lane JN's fully updated entry (owner of column JN only)
+    double pnext = 0.0;
+    if constexpr (JN < DOF && JN >= C0 && JN < C1) pnext = readlane_d(a[JN - C0], JN);
+    chol2g_step<DOF, W, C0, C1, JN, S + 1>(a, sm, r, ok, pnext);
+  }
+}
+
 template <int DOF, int W, int C0, int C1>
 UWVK_DEV void chol2_wave(Smem<DOF>& sm) {
   const int r = lane_id();
@@ -233,7 +303,11 @@ UWVK_DEV void chol2_wave(Smem<DOF>& sm) {
 #pragma unroll
   for (int c = C0; c < C1; c++) a[c - C0] = sm.S[rr * DOF + c];
   bool ok = true;
+#if UWVK_CHOL_GROUP > 1
+  chol2g_step<DOF, W, C0, C1, 0, 0>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
+#else
   chol2_step<DOF, W, C0, C1, 0>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
+#endif
   if (r < DOF) {
     const int base = r * (r + 1) / 2;
 #pragma unroll
@@ -797,6 +871,12 @@ UWVK_DEV bool apply_delta(Smem<DOF>& sm, bool literal, Stamper* st = nullptr) {
 //   gate 0: accept_any_mahalanobis_distance; 1: d2p95 (PoseUKF.cpp:275-286)
 // Returns the gate decision; *ok = false on a Cholesky failure.
 // ---------------------------------------------------------------------------
+// one past the highest tangent DOF measurement model H reads (Dz_j = 0 beyond)
+template <class H, int DOF>
+struct HJmax {
+  static constexpr int value = DOF;
+};
+
 template <int DOF, int M, class H>
 UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)[M * M], int zmode, int gate, H h,
                           bool* ok, Stamper* st = nullptr, bool literal = false) {
@@ -847,7 +927,7 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
   double dz[M];
 #pragma unroll
   for (int a = 0; a < M; a++) dz[a] = mine ? (zp[a] - zm[a]) : 0.0;
-  double S[M * M], Si[M * M];
+  double S[M * M];
   {
     constexpr int NS = M * (M + 1) / 2;
     double sp[NS];
@@ -868,49 +948,8 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
       }
   }
   UWVK_STAMP(5);
-  // cross covariance C = 1/2 sum dx dz^T; thread r (< DOF) accumulates row r.
-  // dx is staged through the (dead) Cholesky-factor region in 16-point chunks;
-  // Sigma in sm.S stays intact for the covariance update below.
-  double C[M];
-#pragma unroll
-  for (int a = 0; a < M; a++) C[a] = 0.0;
-  {
-    constexpr int CS = DOF | 1;
-    double dx[DOF];
-    boxminus_lds<DOF>(x, sm.mu, dx);
-#pragma unroll
-    for (int c = 0; c < (G::N + 15) / 16; c++) {
-      if ((t >> 4) == c) {
-        const int row = t & 15;
-#pragma unroll
-        for (int k = 0; k < DOF; k++) sm.Lp[row * CS + k] = mine ? dx[k] : 0.0;
-#pragma unroll
-        for (int a = 0; a < M; a++) sm.Lp[16 * CS + row * 8 + a] = dz[a];
-      }
-      __syncthreads();
-      const int npts = (G::N - 16 * c) < 16 ? (G::N - 16 * c) : 16;
-      if (t < DOF) {
-        for (int q = 0; q < npts; q++) {
-          const double v = sm.Lp[q * CS + t];
-#pragma unroll
-          for (int a = 0; a < M; a++) C[a] += v * sm.Lp[16 * CS + q * 8 + a];
-        }
-      }
-      __syncthreads();
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < M; a++) C[a] = 0.5 * C[a];
-  UWVK_STAMP(6);
+  double Si[M * M];
   small_inv<M>(S, Si);
-  double K[M];
-#pragma unroll
-  for (int a = 0; a < M; a++) {
-    double s = 0.0;
-#pragma unroll
-    for (int b = 0; b < M; b++) s += C[b] * Si[b * M + a];
-    K[a] = s;
-  }
   double nu[M];
 #pragma unroll
   for (int a = 0; a < M; a++) nu[a] = z[a] - zm[a];
@@ -927,23 +966,90 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
     *ok = cok;
     return false;
   }
-  // Sigma -= C K^T ; delta = K nu
-  if (t < DOF) {
+  // cross covariance C = 1/2 sum_p dx_p dz_p^T.  The points are mu [+] +-L_j,
+  // so dx_{2j+1} = L_j = -dx_{2j+2} (to rounding: [+] then [-] returns the
+  // step) and each pair sums to L_j (z_{2j+1} - z_{2j+2}), the mean
+  // cancelling: C = 1/2 L Dz^T with Dz_j = z_{2j+1} - z_{2j+2}, lower-
+  // triangular L (row r sums j <= r).  Dz_j is exactly 0 for j >= JM when h
+  // reads no tangent DOF >= JM (the two points' inputs are then bitwise mu's).
+  // Dz is staged in sm.scratch(); the waves split the M components; C and the
+  // gain K then go through the (dead) factor region for the Sigma update.
+  constexpr int JM = HJmax<H, DOF>::value;
+  static_assert(JM * M <= Smem<DOF>::kScratch, "Dz staging (Smem::scratch)");
+  double* dzs = sm.scratch();
+  {
+    const int j = (t - 1) >> 1;
+    if (t >= 1 && (t & 1) && j < JM) {
 #pragma unroll
-    for (int a = 0; a < M; a++) sm.Lp[t * M + a] = K[a];  // K rows (the factor is dead)
+      for (int a = 0; a < M; a++) dzs[j * M + a] = zp[a];
+    }
+    __syncthreads();
+    if (t >= 2 && !(t & 1) && j < JM) {
+#pragma unroll
+      for (int a = 0; a < M; a++) dzs[j * M + a] = dzs[j * M + a] - zp[a];
+    }
+    __syncthreads();
+  }
+  // components per wave: two waves split them (wave 0 the first NA), one wave takes all
+  constexpr int NA = G::NW > 1 ? (M + 1) / 2 : M;
+  const int w = G::NW > 1 ? (t >> 6) : 0, r = G::NW > 1 ? (t & 63) : t;
+  const int a0 = w * NA, na = (M - a0) < NA ? (M - a0) : NA;
+  double* cst = sm.Lp;  // C rows [DOF][M], then K rows [DOF][M] (the factor is dead by then)
+  double* kst = sm.Lp + DOF * M;
+  {
+    double Cw[NA];
+#pragma unroll
+    for (int a = 0; a < NA; a++) Cw[a] = 0.0;
+    if (r < DOF && na > 0) {
+      const int jn = r + 1 < JM ? r + 1 : JM;
+      const double* lr = sm.Lp + r * (r + 1) / 2;
+      for (int j = 0; j < jn; j++) {
+        const double l = lr[j];
+#pragma unroll
+        for (int a = 0; a < NA; a++)
+          if (a < na) Cw[a] += l * dzs[j * M + a0 + a];
+      }
+    }
+    __syncthreads();  // every L row read: the factor region takes C
+    if (r < DOF && na > 0) {
+#pragma unroll
+      for (int a = 0; a < NA; a++)
+        if (a < na) cst[r * M + a0 + a] = 0.5 * Cw[a];
+    }
   }
   __syncthreads();
+  // K = C S^-1 and delta = K nu (rows r < DOF of wave 0)
   if (t < DOF) {
-    for (int c = 0; c < DOF; c++) {
-      double s = 0.0;
+    double Cr[M];
 #pragma unroll
-      for (int a = 0; a < M; a++) s += C[a] * sm.Lp[c * M + a];
-      sm.S[t * DOF + c] -= s;
-    }
+    for (int a = 0; a < M; a++) Cr[a] = cst[t * M + a];
     double dl = 0.0;
 #pragma unroll
-    for (int a = 0; a < M; a++) dl += K[a] * nu[a];
+    for (int a = 0; a < M; a++) {
+      double s = 0.0;
+#pragma unroll
+      for (int b = 0; b < M; b++) s += Cr[b] * Si[b * M + a];
+      kst[t * M + a] = s;
+      dl += s * nu[a];
+    }
     sm.vec[t] = dl;
+  }
+  __syncthreads();
+  // Sigma -= C K^T: the waves split the columns
+  {
+    constexpr int CW = (DOF + G::NW - 1) / G::NW;
+    const int c0 = w * CW, c1 = c0 + CW < DOF ? c0 + CW : DOF;
+    if (r < DOF) {
+      double Cr[M];
+#pragma unroll
+      for (int a = 0; a < M; a++) Cr[a] = cst[r * M + a];
+      for (int c = c0; c < c1; c++) {
+        double s = 0.0;
+#pragma unroll
+        for (int a = 0; a < M; a++) s += Cr[a] * kst[c * M + a];
+        sm.S[r * DOF + c] -= s;
+      }
+    }
   }
   __syncthreads();
   UWVK_STAMP(7);
@@ -1116,6 +1222,17 @@ struct HConstrain {  // constrainVelocity, PoseUKF.cpp:199-219
     for (int i = 0; i < 3; i++) { vel6[i] = vb[i] - rw[i]; vel6[3 + i] = wb[i]; acc6[i] = ab[i]; acc6[3 + i] = 0.0; }
     ef.eval(acc6, vel6, q, blk, z);
   }
+};
+
+// measurementEfforts reads orientation, velocity, acceleration, the model blocks
+// and the water velocity; constrainVelocity only the velocity
+template <int DOF>
+struct HJmax<HEfforts<DOF>, DOF> {
+  static constexpr int value = Lay<DOF>::d_wv + 2;
+};
+template <int DOF>
+struct HJmax<HConstrain<DOF>, DOF> {
+  static constexpr int value = Lay<DOF>::d_vel + 3;
 };
 
 // getRotationRate (PoseUKF.cpp:693-699) at the current mean

@@ -16,3 +16,17 @@ hipError_t launch_pose_efforts_epoch(int dof, hipStream_t st, const PoseBufs& b,
 }
 
 }  // namespace uwvk
+
+#ifdef UWVK_STAMPS
+// diagnostic build only: per-phase cycle sums of k_pose_efforts_epoch
+extern "C" int uwvk_debug_read_stamps_eff(unsigned long long* sum, unsigned long long* cnt, int reset) {
+  if (hipMemcpyFromSymbol(sum, HIP_SYMBOL(uwvk::uwvk_stamp_sum), 64 * 8) != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(uwvk::uwvk_stamp_cnt), 64 * 8) != hipSuccess) return 1;
+  if (reset) {
+    unsigned long long z[64] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(uwvk::uwvk_stamp_sum), z, 64 * 8) != hipSuccess) return 1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(uwvk::uwvk_stamp_cnt), z, 64 * 8) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif

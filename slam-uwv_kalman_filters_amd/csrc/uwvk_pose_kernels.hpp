@@ -272,7 +272,14 @@ __global__ __launch_bounds__(Geo<DOF>::T) UWVK_EFF_ATTR void k_pose_efforts_epoc
   const int64_t B = b.batch, i = xcd_instance(B), e = ea.first;
   const uint32_t fl = ea.flags[e];
   if (!(fl & UWVK_EV_EFFORTS)) return;
+#ifdef UWVK_STAMPS
+  Stamper stamper;
+  Stamper* st = &stamper;
+#else
+  Stamper* st = nullptr;
+#endif
   load_instance<DOF>(sm, b, i);
+  UWVK_STAMP(11);
   MeasArgs me{};
   me.only_vel = (fl & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0;
   me.v3[0] = ea.p_sens[0]; me.v3[1] = ea.p_sens[1]; me.v3[2] = ea.p_sens[2];
@@ -280,14 +287,16 @@ __global__ __launch_bounds__(Geo<DOF>::T) UWVK_EFF_ATTR void k_pose_efforts_epoc
   const double* z = ea.efforts + ((int64_t)ea.e_index[e] * B + i) * 6;
   bool sok = true, nan = false;
   uint32_t acc = 0;
-  if (all_finite(z, 6)) acc = do_update<DOF, MK_EFFORTS>(sm, sh, b, i, z, ea.e_cov, me, w, &sok) ? 1u : 0u;
+  if (all_finite(z, 6)) acc = do_update<DOF, MK_EFFORTS>(sm, sh, b, i, z, ea.e_cov, me, w, &sok, st) ? 1u : 0u;
   else nan = true;
+  UWVK_STAMP(12);
   if (tid() == 0) {
     if (!sok) b.status[i] |= UWVK_ST_NOTPD;
     if (nan) b.status[i] |= UWVK_ST_NAN;
     if (ea.accept_counts) ea.accept_counts[i * 4 + 3] += acc;
   }
   store_instance<DOF>(sm, b, i);
+  UWVK_STAMP(13);
 }
 
 template <int DOF>
