@@ -55,6 +55,9 @@
 // Delta_j as LDS broadcasts instead of v_readlane (105.9), the same for Dz / P
 // (no change), lds_sums in the manifold-mean loop (+0.7%), s_setprio around
 // the Cholesky column chain (within noise).
+#ifndef PSP_DIAG_SEL  // per-lane decay factors and water-velocity noise by uniform selects (r02)
+#define PSP_DIAG_SEL 1
+#endif
 #ifndef PSP_FAST
 #define PSP_FAST 7039
 #endif
@@ -481,6 +484,26 @@ UWVK_DEV double proc_diag(int d, const PoseShared& sh, double dt) {
   if (d == L::d_rho) return 1.0 + dt * sh.ntau[7];
   return 1.0;
 }
+// the same per lane from the eight uniform decay rates by selects: a runtime
+// index into sh.ntau was a per-lane global load whose s_waitcnt vmcnt(0) also
+// drained the next epoch's IMU prefetch on the predict's critical path
+template <int DOF>
+UWVK_DEV double proc_diag_sel(int d, const PoseShared& sh, double dt) {
+  using L = Lay<DOF>;
+  double nt = 0.0;
+  nt = (d >= L::d_bg && d < L::d_bg + 3) ? sh.ntau[0] : nt;
+  nt = (d >= L::d_ba && d < L::d_ba + 3) ? sh.ntau[1] : nt;
+  if constexpr (L::has_params) {
+    nt = (d >= L::d_inertia && d < L::d_inertia + 9) ? sh.ntau[2] : nt;
+    nt = (d >= L::d_lin && d < L::d_lin + 9) ? sh.ntau[3] : nt;
+    nt = (d >= L::d_quad && d < L::d_quad + 9) ? sh.ntau[4] : nt;
+  }
+  nt = (d >= L::d_wv && d < L::d_wv + 4) ? sh.ntau[5] : nt;
+  nt = (d >= L::d_badcp && d < L::d_badcp + 2) ? sh.ntau[6] : nt;
+  nt = (d == L::d_rho) ? sh.ntau[7] : nt;
+  const bool markov = scaled_dof(d) && d < DOF;
+  return markov ? 1.0 + dt * nt : 1.0;
+}
 // coupled column of row d (pos -> vel, vel -> acc) or -1
 UWVK_DEV constexpr int proc_couple(int d) { return d < 3 ? d + 6 : (d >= 6 && d < 9 ? d + 3 : -1); }
 
@@ -648,7 +671,11 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       for (int i = 0; i < 3; i++) Y[i] += a[j] * readlane_d(dd[i], 2 * j);
     const int cp = proc_couple(l);
     const int src = cp >= 0 ? cp : l;
+#if PSP_DIAG_SEL
+    const double ar = proc_diag_sel<DOF>(l, sh, dt);
+#else
     const double ar = proc_diag<DOF>(l, sh, dt);
+#endif
 #pragma unroll
     for (int i = 0; i < 3; i++) {
       const double yc = shfl_d(Y[i], src);
@@ -662,7 +689,11 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   double nv[6];
   const int jl = l < DOF ? l : DOF - 1;
   const int jc = proc_couple(jl);
+#if PSP_DIAG_SEL
+  const double aj = proc_diag_sel<DOF>(jl, sh, dt);
+#else
   const double aj = proc_diag<DOF>(jl, sh, dt);
+#endif
 #pragma unroll
   for (int q = 0; q < 6; q++) {
     const int r = pv[q], rc = proc_couple(r);
@@ -726,6 +757,41 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     constexpr int R0 = 9;
     const double2* f2 = reinterpret_cast<const double2*>(fq);
     const int bw = sh.q_bw;
+#if PSP_DIAG_SEL
+    // the lane-resident band (qs) and the table band are separate uniform
+    // branches: a per-lane select between them made the compiler issue the
+    // table load anyway and wait for it (and for the IMU prefetch) every epoch.
+    // The water-velocity noise comes from four uniform values passed through an
+    // empty asm, so that the select is not turned back into a per-lane load.
+    double qw4[4] = {sh.q_wv[0], sh.q_wv[1], sh.q_wv[2], sh.q_wv[3]};
+#pragma unroll
+    for (int i = 0; i < 4; i++) asm volatile("" : "+s"(qw4[i]));
+    auto band = [&](auto QS) {
+      constexpr bool kQS = decltype(QS)::value;
+      double idk = ids;  // 1 / d'_{l-k}
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        if (k > 0) idk = dpp_d<0x138, 0xf, 0xf>(idk);  // wave_shr:1 -> lane l - k
+        const int j = l - k;
+        if (l >= R0 && l < DOF && j >= R0 && k <= bw) {
+          const int e = pidx(l, j);
+          double q;
+          if constexpr (kQS) q = k == 0 ? lq.q0 : (k == 1 ? lq.q1 : lq.q2);
+          else q = f2[e].y;
+          if (k == 0 && l >= L::d_wv && l < L::d_wv + 4) {
+            const int iw = l - L::d_wv;
+            const double qw = iw == 0 ? qw4[0] : (iw == 1 ? qw4[1] : (iw == 2 ? qw4[2] : qw4[3]));
+            q = dt2 * (qw + wv_add);
+          }
+          if (q != 0.0) sm.S[e] += q * (ids * idk);
+        }
+      }
+    };
+    if (qs)
+      band(std::true_type{});
+    else
+      band(std::false_type{});
+#else
     double idk = ids;  // 1 / d'_{l-k}
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -742,6 +808,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
         if (q != 0.0) sm.S[e] += q * (ids * idk);
       }
     }
+#endif
     for (int k = 3; k <= bw; k++) {  // uniform bound: wide Q bands only
       const double idj = shfl_d(ids, l - k >= 0 ? l - k : 0);
       const int j = l - k;

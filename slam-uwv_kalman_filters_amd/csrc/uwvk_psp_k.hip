@@ -80,6 +80,10 @@ UWVK_DEV void tail_signal(const EpochArgs& ea, int64_t t, int chunk) {
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifndef PSP_FLAG_VGPR
+#define PSP_FLAG_VGPR 0  // r02 A/B: no measurable gain, one more VGPR (168)
+#endif
+
 template <int DOF>
 UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
   using G = PG<DOF>;
@@ -325,7 +329,15 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
   uint32_t fl_n = 0;
   double g_n[3] = {0, 0, 0}, a_n[3] = {0, 0, 0};
   auto fetch = [&](int64_t e) {
+#if PSP_FLAG_VGPR
+    // a lane-dependent (always zero) offset keeps the prefetched flag word in a
+    // VGPR until the next epoch reads it: from a uniform address the compiler
+    // moved it to an SGPR at once (readfirstlane + a spill-lane write), waiting
+    // out the load's latency at the top of every epoch
+    fl_n = ea.flags[e + (olane() >> 6)];
+#else
     fl_n = ea.flags[e];
+#endif
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       g_n[k] = ea.gyro[(e * B + inst) * 3 + k];
@@ -335,7 +347,11 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
   if (e_end > e_begin) fetch(e_begin);
 #pragma unroll 1
   for (int64_t e = e_begin; e < e_end; e++) {
+#if PSP_FLAG_VGPR
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(fl_n);
+#else
     const uint32_t fl = fl_n;
+#endif
     const double g[3] = {g_n[0], g_n[1], g_n[2]}, za[3] = {a_n[0], a_n[1], a_n[2]};
     if (e + 1 < e_end) fetch(e + 1);
     if (all_finite(g, 3)) {  // integrateMeasurement(RotationRate): checkMeasurment, then store
