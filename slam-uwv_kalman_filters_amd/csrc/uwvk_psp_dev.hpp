@@ -32,7 +32,7 @@
 #define PSP_RB 8          // rows per block of the row-block sweeps
 #endif
 #ifndef PSP_RBP
-#define PSP_RBP 8         // row pairs per block of the paired rank-M sweep (rankm_pairs)
+#define PSP_RBP 6         // row pairs per block of the paired rank-M sweep (rankm_pairs); 8 -> 6: 167 -> 150 VGPRs, A/B +0.3%
 #endif
 // ablation knobs for timing analysis only (results are invalid when set):
 // PSP_ABL = bitmask: 1 mean 1 iteration, 2 no rank-m pass, 4 no L Delta / X,
