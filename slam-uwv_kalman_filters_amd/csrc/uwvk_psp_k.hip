@@ -7,7 +7,9 @@
 //   [-> Velocity (DVL) -> Pressure -> ADCP cells]
 // The host splits a launch after each BodyEfforts epoch (this kernel runs that
 // epoch's predict and other updates) and runs the efforts update alone on the
-// literal k_pose_efforts_epoch, whose HBM layout is shared.
+// literal k_pose_efforts_epoch, whose HBM layout is shared.  With tail
+// spreading (EpochArgs::chunks > 1, plan_tail below) the last instances of
+// each XCD run as a few epoch chunks, one block each, handed on in order.
 #include <algorithm>
 #include <vector>
 
