@@ -400,6 +400,12 @@ int64_t uwvk_pose_resident_slots(int dof, int device);
 /* Kernel-timing helper: HIP events recorded on the handle's stream. */
 uwvk_status uwvk_pose_timer_start(uwvk_pose* h);
 uwvk_status uwvk_pose_timer_stop(uwvk_pose* h, float* elapsed_ms);
+/* Split form of uwvk_pose_timer_stop: _mark records the stop event without
+ * waiting, so work queued after it (the ensemble statistics) follows the
+ * timed launches with no host round trip; _elapsed waits for that event and
+ * returns the time since uwvk_pose_timer_start. */
+uwvk_status uwvk_pose_timer_mark(uwvk_pose* h);
+uwvk_status uwvk_pose_timer_elapsed(uwvk_pose* h, float* elapsed_ms);
 
 /* ---- recorded-mission ingestion (host only, no device needed) ---------- */
 /* The reference is driven by its caller's stream aligner (Rock orogen task,

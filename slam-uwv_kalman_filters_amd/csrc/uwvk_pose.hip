@@ -656,15 +656,13 @@ uwvk_status uwvk_pose_ensemble_allreduce(uwvk_pose* h, const double* truth, doub
   const int s = h->store;
   const int nout = 3 * s + 2;
   double* d_out = h->d_scratch;
-  double* d_truth = h->d_scratch + 192;
-  std::vector<double> t(s, 0.0);
-  if (truth) std::memcpy(t.data(), truth, s * 8);
-  else t[3] = 1.0;
+  StatTruth t{};  // by value in the kernel arguments: no upload in front of the kernel
+  if (truth) std::memcpy(t.v, truth, s * 8);
+  else t.v[3] = 1.0;
   // ensemble partials after the rotation-rate area: d_scratch + 256 + 3 batch
   double* d_part = h->d_scratch + 256 + 3 * h->batch;
-  HIPCHK(hipMemcpyAsync(d_truth, t.data(), s * 8, hipMemcpyHostToDevice, h->stream));
   PoseBufs b = bufs(h);
-  HIPCHK(launch_pose_stats(h->dof, h->stream, b, d_truth, d_out, d_part));
+  HIPCHK(launch_pose_stats(h->dof, h->stream, b, t, d_out, d_part));
   if (comm) {  // RCCL sum across the ranks' shards, stream-ordered after the stats kernel
     const uwvk_status st = uwvk_comm_allreduce_sum_device(comm, d_out, nout, (void*)h->stream);
     if (st != UWVK_OK) return st;
@@ -708,6 +706,17 @@ uwvk_status uwvk_pose_timer_start(uwvk_pose* h) {
 uwvk_status uwvk_pose_timer_stop(uwvk_pose* h, float* ms) {
   if (!h || !ms) return UWVK_EINVAL;
   HIPCHK(hipEventRecord(h->ev1, h->stream));
+  HIPCHK(hipEventSynchronize(h->ev1));
+  HIPCHK(hipEventElapsedTime(ms, h->ev0, h->ev1));
+  return UWVK_OK;
+}
+uwvk_status uwvk_pose_timer_mark(uwvk_pose* h) {
+  if (!h) return UWVK_EINVAL;
+  HIPCHK(hipEventRecord(h->ev1, h->stream));
+  return UWVK_OK;
+}
+uwvk_status uwvk_pose_timer_elapsed(uwvk_pose* h, float* ms) {
+  if (!h || !ms) return UWVK_EINVAL;
   HIPCHK(hipEventSynchronize(h->ev1));
   HIPCHK(hipEventElapsedTime(ms, h->ev0, h->ev1));
   return UWVK_OK;

@@ -20,7 +20,7 @@ hipError_t launch_pose_rotation_rate(int dof, hipStream_t st, const PoseBufs& b,
   return hipGetLastError();
 }
 
-hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const double* truth, double* out,
+hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const StatTruth& truth, double* out,
                              double* part) {
   const int64_t nb = (b.batch + 63) / 64;
   const int nout = 3 * (dof == 53 ? Lay<53>::store : Lay<26>::store) + 2;

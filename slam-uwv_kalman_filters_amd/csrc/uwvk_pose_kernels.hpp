@@ -69,8 +69,12 @@ hipError_t launch_pose_epoch(int dof, hipStream_t st, const PoseBufs& b, const P
 hipError_t launch_pose_efforts_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                                      const EpochArgs& ea);
 hipError_t launch_pose_rotation_rate(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double* out);
-// part: ceil(batch / 64) x (3 store + 1) doubles of device scratch
-hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const double* truth, double* out,
+// the truth store-vector of the ensemble statistics, passed by value (kernarg)
+struct StatTruth {
+  double v[54];
+};
+// part: ceil(batch / 64) x (3 store + 2) doubles of device scratch
+hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const StatTruth& truth, double* out,
                              double* part);
 
 #ifdef UWVK_POSE_KERNEL_BODIES
@@ -409,62 +413,100 @@ __global__ __launch_bounds__(64) void k_pose_rotation_rate(PoseBufs b, PoseShare
   if (lane_id() < 3) out[i * 3 + lane_id()] = o[lane_id()];
 }
 
-// ensemble statistics: one block per 64 instances, atomics into out
 // Ensemble statistics, deterministic two-stage reduction (no atomics): one wave
-// per 64 instances writes its partial sums (butterfly shuffles, the same value
-// in every lane), then k_pose_stats_sum adds the partials in a fixed order.
+// per 64 instances writes one partial row, then k_pose_stats_sum adds the rows
+// in a fixed order.  The 64 instances' mu rows are contiguous in HBM, so the
+// wave copies them into LDS in one coalesced sweep; lane l then works on
+// instance l (SO3 log error, 9x9 NEES solve) and lane s sums column s over the
+// instances in order, so no cross-lane reduction tree is needed.
 // Layout of out (nout = 3 store + 2): sum mu, sum mu^2, sum err^2 (orientation
 // slots 3..5 hold the squared SO3 log error, slot 6 is 0), NEES over
 // (position, orientation, velocity) summed over the instances whose 9x9 block
 // is positive definite, and the number of instances left out of that sum.
 template <int DOF>
-__global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, const double* truth, double* part) {
+__global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, StatTruth truth, double* part) {
   using L = Lay<DOF>;
   constexpr int S = L::store, NOUT = 3 * S + 2;
-  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const bool live = i < b.batch;
-  const double* x = b.mu + (live ? i : 0) * S;
-  const double* P = b.sigma + (live ? i : 0) * (int64_t)tri_n<DOF>();
-  double* o = part + (int64_t)blockIdx.x * NOUT;
-  auto put = [&](int slot, double v) {
-    v = live ? v : 0.0;
+  static_assert(S + 2 <= 64, "one lane per output column");
+  __shared__ double xs[64 * S];  // the block's mu rows, as stored
+  __shared__ double pe[64 * 5];  // per instance: squared rotation-vector error (3), NEES, excluded
+  const int l = threadIdx.x;
+  const int64_t i0 = (int64_t)blockIdx.x * 64;
+  const int nl = (int)(b.batch - i0 < 64 ? b.batch - i0 : 64);
+  const double* tv = truth.v;
+  const double* xg = b.mu + i0 * S;
+#pragma unroll 6
+  for (int k = l; k < nl * S; k += 64) xs[k] = xg[k];
+  __syncthreads();
+  if (l < nl) {
+    const double* x = xs + l * S;
+    const double* P = b.sigma + (i0 + l) * (int64_t)tri_n<DOF>();
+    double r[3];
+    qboxminus(x + 3, tv + 3, r);
+    // NEES over (position, orientation, velocity): e^T P_sub^-1 e via a 9x9 Cholesky solve
+    double err[9];
+    for (int k = 0; k < 3; k++) { err[k] = x[k] - tv[k]; err[3 + k] = r[k]; err[6 + k] = x[7 + k] - tv[7 + k]; }
+    double A[45], id[9];  // packed lower triangle (Sigma's first 45 entries); reciprocal pivots
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-    if (threadIdx.x == 0) o[slot] = v;
-  };
-  double r[3];
-  qboxminus(x + 3, truth + 3, r);
-  for (int s = 0; s < S; s++) {
-    const double xs = x[s], e = xs - truth[s];
-    put(s, xs);
-    put(S + s, xs * xs);
-    put(2 * S + s, (s >= 3 && s < 6) ? r[s - 3] * r[s - 3] : (s == 6 ? 0.0 : e * e));
-  }
-  // NEES over (position, orientation, velocity): e^T P_sub^-1 e via a 9x9 Cholesky solve
-  double err[9];
-  for (int k = 0; k < 3; k++) { err[k] = x[k] - truth[k]; err[3 + k] = r[k]; err[6 + k] = x[7 + k] - truth[7 + k]; }
-  double A[81];
-  for (int a = 0; a < 9; a++)
-    for (int c = 0; c <= a; c++) A[a * 9 + c] = P[pidx(a, c)];  // the lower triangle is all the solve reads
-  bool pd = true;  // a non-positive pivot (or a NaN) leaves the instance out of the NEES sum
-  for (int a = 0; a < 9; a++) {
-    for (int c = 0; c <= a; c++) {
-      double s = A[a * 9 + c];
-      for (int k = 0; k < c; k++) s -= A[a * 9 + k] * A[c * 9 + k];
-      if (a == c) pd = pd && (s > 0.0);
-      A[a * 9 + c] = (a == c) ? sqrt(s > 0.0 ? s : 1.0) : s / A[c * 9 + c];
+    for (int k = 0; k < 45; k++) A[k] = P[k];
+    bool pd = true;  // a non-positive pivot (or a NaN) leaves the instance out of the NEES sum
+#pragma unroll
+    for (int c = 0; c < 9; c++) {
+      double s = A[pidx(c, c)];
+#pragma unroll
+      for (int k = 0; k < c; k++) s -= A[pidx(c, k)] * A[pidx(c, k)];
+      pd = pd && (s > 0.0);
+      const double dg = sqrt(s > 0.0 ? s : 1.0);
+      A[pidx(c, c)] = dg;
+      id[c] = 1.0 / dg;
+#pragma unroll
+      for (int a = c + 1; a < 9; a++) {
+        double t = A[pidx(a, c)];
+#pragma unroll
+        for (int k = 0; k < c; k++) t -= A[pidx(a, k)] * A[pidx(c, k)];
+        A[pidx(a, c)] = t * id[c];
+      }
     }
+    double y[9], nees = 0;
+#pragma unroll
+    for (int a = 0; a < 9; a++) {
+      double s = err[a];
+#pragma unroll
+      for (int k = 0; k < a; k++) s -= A[pidx(a, k)] * y[k];
+      y[a] = s * id[a];
+      nees += y[a] * y[a];
+    }
+    pd = pd && isfinite(nees);
+    pe[l * 5 + 0] = r[0] * r[0];
+    pe[l * 5 + 1] = r[1] * r[1];
+    pe[l * 5 + 2] = r[2] * r[2];
+    pe[l * 5 + 3] = pd ? nees : 0.0;
+    pe[l * 5 + 4] = pd ? 0.0 : 1.0;
   }
-  double y[9], nees = 0;
-  for (int a = 0; a < 9; a++) {
-    double s = err[a];
-    for (int k = 0; k < a; k++) s -= A[a * 9 + k] * y[k];
-    y[a] = s / A[a * 9 + a];
-    nees += y[a] * y[a];
+  __syncthreads();
+  double* o = part + (int64_t)blockIdx.x * NOUT;
+  if (l < S) {
+    const double t = tv[l];
+    double sx = 0.0, sxx = 0.0, see = 0.0;
+    for (int k = 0; k < nl; k++) {
+      const double v = xs[k * S + l], e = v - t;
+      sx += v;
+      sxx += v * v;
+      see += e * e;
+    }
+    if (l >= 3 && l < 7) {
+      see = 0.0;  // orientation: the rotation-vector error (slot 6 stays 0)
+      if (l < 6)
+        for (int k = 0; k < nl; k++) see += pe[k * 5 + (l - 3)];
+    }
+    o[l] = sx;
+    o[S + l] = sxx;
+    o[2 * S + l] = see;
+  } else if (l < S + 2) {
+    double a = 0.0;
+    for (int k = 0; k < nl; k++) a += pe[k * 5 + 3 + (l - S)];
+    o[3 * S + (l - S)] = a;
   }
-  pd = pd && isfinite(nees);
-  put(3 * S, pd ? nees : 0.0);
-  put(3 * S + 1, pd ? 0.0 : 1.0);
 }
 
 // out[s] = sum over the nblk partial rows, block s: thread t takes rows t, t + 256, ...

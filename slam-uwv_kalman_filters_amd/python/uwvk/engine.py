@@ -43,7 +43,7 @@ SYMBOLS = [
     "uwvk_ipose_create", "uwvk_ipose_destroy", "uwvk_ipose_stream", "uwvk_ipose_init",
     "uwvk_ipose_set_pose_reference", "uwvk_ipose_predict", "uwvk_ipose_update_visual",
     "uwvk_ipose_get_corrected_pose", "uwvk_ipose_get_state", "uwvk_ipose_get_status",
-    "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots",
+    "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots", "uwvk_pose_timer_mark", "uwvk_pose_timer_elapsed",
 ]
 
 _LIB = None
@@ -280,6 +280,16 @@ class PoseUKFBatch:
     def timer_stop(self):
         ms = C.c_float(0)
         _chk(self.L.uwvk_pose_timer_stop(self.h, C.byref(ms)), "timer_stop")
+        return ms.value
+
+    def timer_mark(self):
+        """Record the stop event without waiting (uwvk_pose_timer_mark)."""
+        _chk(self.L.uwvk_pose_timer_mark(self.h), "timer_mark")
+
+    def timer_elapsed(self):
+        """Wait for the event timer_mark recorded; ms since timer_start."""
+        ms = C.c_float(0)
+        _chk(self.L.uwvk_pose_timer_elapsed(self.h, C.byref(ms)), "timer_elapsed")
         return ms.value
 
 

@@ -130,3 +130,34 @@ def test_device_buffer_read_after_async_run_log():
     assert counts[0].sum() > 0
     np.testing.assert_array_equal(counts[1], counts[0])
     np.testing.assert_array_equal(counts[2], counts[0])
+
+
+def test_split_timer_and_stats_after_async_run_log():
+    """bench.py's timed region: timer_mark records the stop event without a
+    host wait, the statistics kernels queue behind the epoch launch on the
+    same stream, and timer_elapsed waits for the event.  The statistics equal
+    those of the blocking sequence (timer_stop, then ensemble_stats) bitwise."""
+    B, E = 4096, 60
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(B, E, "C3")
+    truth = log["truth"].state(E, 53)
+    out = []
+    for split in (False, True):
+        f = engine.PoseUKFBatch(B)
+        f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+        f.set_process_noise_from_config(cfg, log["dt"])
+        d = f.upload_log(log)
+        f.synchronize()
+        f.timer_start()
+        f.run_log(d, sync=not split)
+        if split:
+            f.timer_mark()
+            st = f.ensemble_stats(truth)
+            ms = f.timer_elapsed()
+        else:
+            ms = f.timer_stop()
+            st = f.ensemble_stats(truth)
+        assert ms > 0.0
+        out.append(st)
+    np.testing.assert_array_equal(out[1], out[0])
+    assert out[0][-1] == 0.0 and np.isfinite(out[0]).all()
