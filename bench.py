@@ -311,9 +311,13 @@ def main():
     rccl_check = None
     same_dev = os.environ.get("UWVK_BENCH_SAME_DEVICE") == "1"  # RCCL refuses two ranks on one GPU
     if dist is not None and comm is None and not same_dev and os.environ.get("UWVK_BENCH_RCCL_CHECK", "1") == "1":
-        comm = make_comm()
-        rs = f.ensemble_stats(truth, comm)
-        rccl_check = bool(np.allclose(rs, stats, rtol=1e-12, atol=1e-12))
+        try:  # a cross-check after timing: its failure is reported, it does not void the line
+            comm = make_comm()
+            rs = f.ensemble_stats(truth, comm)
+            rccl_check = bool(np.allclose(rs, stats, rtol=1e-12, atol=1e-12))
+        except Exception as ex:  # noqa: BLE001
+            print("warning: RCCL cross-check failed: %r" % (ex,), file=sys.stderr)
+            rccl_check = False
     status = f.get_status()
     if status.any():
         print("warning: %d instances flagged (status bits)" % int((status != 0).sum()), file=sys.stderr)
