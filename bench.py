@@ -101,6 +101,10 @@ def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance, c4_c
     # shift the start so that a DVL epoch (k % 200 == 0) lands mid-window
     target = warmup + min(steps, 200) // 2
     shift = (200 - (target + 1) % 200) % 200
+    # diagnostic only (never the headline): UWVK_BENCH_WINDOW_OFFSET moves the window
+    # off the DVL epoch (100: no DVL update in a window of < 100 epochs); the line
+    # reports dvl_epochs_in_window either way
+    shift += int(os.environ.get("UWVK_BENCH_WINDOW_OFFSET", "0"))
     log = synth.make_pose_log(batch, total + shift, mode=mode, dof=dof, first_instance=first_instance,
                               dropout_on=c4_cycle[0], dropout_off=c4_cycle[1])
     return log, shift
