@@ -2,16 +2,23 @@
 """bench.py — batched PoseUKF predict+update throughput on MI355X.
 
 Metric (BASELINE.json): UKF predict+update steps/sec at batch = 65536 PoseUKF
-instances (config C3: full 53-DOF PoseState, 1 kHz IMU + 5 Hz DVL).
-One "step" = one IMU epoch of ONE filter instance: RotationRate store ->
-predictionStep(1 ms) -> Acceleration update, plus the DVL velocity update
-when the 5 Hz schedule is due.  `value` counts
-instance-epochs per second over the whole job (all ranks).
+instances (config C3: full 53-DOF PoseState, 1 kHz IMU + 5 Hz DVL) on 1 GPU,
+and 1,048,576 instances on 8 GPUs (config C5: 131,072 per GPU, RCCL
+all-reduce of the ensemble statistics).  One "step" = one IMU epoch of ONE
+filter instance: RotationRate store -> predictionStep(1 ms) -> Acceleration
+update, plus the DVL velocity update when the 5 Hz schedule is due
+(SURVEY.md §3, §8d).  `value` counts instance-epochs per second over the whole
+job (all ranks).
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-instances are sharded across ranks (weak scaling: --batch-per-gpu instances on
-every GPU, no data-path collective); the only collective is the RCCL
-all-reduce of the ensemble statistics at the end of the timed region.
+Multi-GPU: one process per GPU.  `python3 bench.py --gpus N` starts the N rank
+processes itself (subprocesses, before any GPU call in the parent); under
+`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N` the
+launcher's ranks are used (and --gpus must equal WORLD_SIZE).  Instances are
+sharded contiguously (weak scaling: --batch-per-gpu instances on every GPU, no
+data-path collective); the engine's RCCL communicator exists for the whole run
+and sums the ensemble statistics every --stats-every epochs and at the end of
+the timed region, inside it (C5).  A gloo process group is the host control
+plane (barriers, the RCCL id, the max of the per-rank times).
 
 Inputs are synthetic (uwvk.synth) and resident in HBM before timing starts.
 Timing: barrier + device sync on both sides of the timed region, max over
@@ -22,6 +29,8 @@ bounded sample of the same workload, on rank 0 at N = 1 only.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -78,10 +87,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200, help="timed epochs")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch-per-gpu", type=int, default=0, help="0: 65536 (C3/C4), 4096 (C2)")
+    ap.add_argument("--batch-per-gpu", type=int, default=0,
+                    help="0: 65536 (C3/C4 at N = 1), 131072 (C5: N > 1), 4096 (C2)")
     ap.add_argument("--dof", type=int, default=53)
-    ap.add_argument("--mode", default="C3", choices=["C2", "C3", "C4"],
-                    help="C3 (headline) / C4: PoseUKF; C2: VelocityUKF (secondary line)")
+    ap.add_argument("--mode", default="auto", choices=["auto", "C2", "C3", "C4", "C5"],
+                    help="auto: C3 at N = 1 (headline), C5 at N > 1; C4: ADCP + drop-outs; C2: VelocityUKF")
+    ap.add_argument("--stats-every", type=int, default=1000,
+                    help="epochs between ensemble-statistics all-reduces inside the timed region (C5: 1000); "
+                         "one more at its end")
     ap.add_argument("--c4-cycle", default="30,10",
                     help="C4 DVL drop-out cycle 'on,off' in s; e.g. 0.3,0.1 keeps every event rate of the 30/10 "
                          "cycle (0.25%% efforts epochs) inside a 2000-epoch window")
@@ -173,6 +186,10 @@ def cpu_baseline(synth, cfg, uwv, mode, dof, threads):
     o.run_log(log, nthreads=threads)
     dt = time.perf_counter() - t0
     return {"value": batch * epochs / dt, "unit": "steps/s", "cores": threads, "kind": "port",
+            "algorithm": "literal ukfom (all 2n+1 sigma points: LLT, 107 model evaluations, iterative manifold "
+                         "mean, covariance GEMM, literal apply_delta re-spread); the GPU runs PSP, an exact O(n^2) "
+                         "reformulation (DESIGN.md 4.3) with ~3.4% of those flops, so the GPU/CPU ratio mixes an "
+                         "algorithmic gain (~30x) with the hardware gain",
             "sample": "%d PoseUKF instances x %d epochs (%s, incl. %d DVL updates each), %d pthreads, %.2f s wall; "
                       "oracle timing build -O3 -march=x86-64-v4" % (batch, epochs, mode,
                                                                    int(((log["flags"] & 2) != 0).sum()), threads, dt),
@@ -210,46 +227,100 @@ def launched_by_torchrun():
     return "TORCHELASTIC_RUN_ID" in os.environ or ("LOCAL_RANK" in os.environ and "WORLD_SIZE" in os.environ)
 
 
-def init_dist(world, local, backend):
-    """One process per GPU: the process group is made whenever the job runs
-    under torch.distributed.run (world size 1 included) or with WORLD_SIZE > 1.
-    It is a host-side control plane (gloo by default): barriers, the id of the
-    RCCL check communicator and the 163-double statistics sum.  An RCCL
-    communicator in the process (torch's nccl group or the engine's own) slows
-    the concurrently running epoch kernel by 6-7% on the GPU (r02: 9.20 ->
-    9.88 ms per 20-epoch launch, rocprofv3 kernel trace),
-    so none exists during the timed region."""
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def rank_env(base, rank, world, port):
+    """Environment of rank `rank` of a self-launched N-rank job."""
+    env = dict(base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), UWVK_BENCH_SPAWNED="1")
+    return env
+
+
+def spawn_ranks(argv, world, timeout=None, script=None):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this
+    script (subprocesses, never an exec; the parent makes no GPU call) and
+    return the worst exit code.  If a rank fails, the others are stopped
+    (their exact PIDs) instead of waiting at a barrier forever."""
+    port = _free_port()
+    script = script or os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv),
+                              env=rank_env(os.environ, r, world, port)) for r in range(world)]
+    t0 = time.time()
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in procs:
+                    q.terminate()
+        if timeout is not None and time.time() - t0 > timeout:
+            for q in procs:
+                q.kill()
+            rc = rc or 124
+            break
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def resolve_world(a, env=os.environ):
+    """(world, rank, local) of this process; raises SystemExit when --gpus and
+    a launcher's WORLD_SIZE disagree."""
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if a.gpus != world:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (the launcher's rank count); pass --gpus %d"
+                             % (a.gpus, world, world))
+        return world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+    return 1, 0, 0
+
+
+def workload_of(a, world):
+    """(mode, batch per GPU): C3 at N = 1, C5 (131,072 per GPU) at N > 1."""
+    mode = a.mode if a.mode != "auto" else ("C3" if world == 1 else "C5")
+    if a.batch_per_gpu:
+        return mode, a.batch_per_gpu
+    return mode, {"C2": 4096, "C5": 131072}.get(mode, 65536)
+
+
+def init_dist(world):
+    """The host control plane of a multi-rank job (gloo): barriers, the RCCL
+    id, the max of the per-rank times.  None for a single-process run."""
     if world == 1 and not launched_by_torchrun():
         return None
-    import torch
     import torch.distributed as dist
-    if backend == "nccl":
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        dist.init_process_group("gloo")
+    dist.init_process_group("gloo")
     return dist
 
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = os.environ.get("UWVK_BENCH_BACKEND", "gloo")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(sys.argv[1:], a.gpus))
+    world, rank, local = resolve_world(a)
     # UWVK_BENCH_SAME_DEVICE=1: rehearsal of the N-rank path on one GPU (all ranks on device 0)
-    if os.environ.get("UWVK_BENCH_SAME_DEVICE") == "1":
+    same_dev = os.environ.get("UWVK_BENCH_SAME_DEVICE") == "1"
+    if same_dev:
         local = 0
-    stat_dev = "cuda" if backend == "nccl" else None
-    dist = init_dist(world, local, backend)
+    dist = init_dist(world)
     from uwvk import engine, ensemble, synth
-
-    if a.mode == "C2":
-        return bench_vel(a, engine, synth, world, rank, local, dist)
-    B = a.batch_per_gpu or 65536
+    mode, B = workload_of(a, world)
+    if mode == "C2":
+        return bench_vel(a, engine, synth, world, rank, local, dist, B)
+    log_mode = "C3" if mode == "C5" else mode
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     cyc = tuple(float(v) for v in a.c4_cycle.split(","))
-    log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, a.mode, a.dof, first_instance=rank * B, c4_cycle=cyc)
+    log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, log_mode, a.dof, first_instance=rank * B, c4_cycle=cyc)
     f = engine.PoseUKFBatch(B, a.dof, device=local)
     f.set_tail_slots(a.tail_slots)
     if a.dense:
@@ -265,26 +336,33 @@ def main():
     e0 = shift + a.warmup
     window = flags[e0:e0 + a.steps]
     n_dvl = int(((window & 2) != 0).sum())
-    truth = log["truth"].state(e0 + a.steps, a.dof)
-    # the collective of the timed region: the per-rank statistics summed over the
-    # process group (host side, 163 doubles).  UWVK_BENCH_COLL=rccl sums them with
-    # the engine's RCCL communicator on the handle's stream instead (slower, see
-    # init_dist); by default RCCL runs after the timed region as a cross-check.
+    # The collective (C5): the per-rank ensemble statistics summed over the
+    # engine's RCCL communicator on the handle's stream (uwvk_pose_ensemble_
+    # allreduce), every --stats-every epochs and at the end of the window.  The
+    # communicator is made before the timed region and lives through it: an
+    # RCCL communicator costs the running epoch kernel ~6% of its clock (DVFS,
+    # DESIGN.md section 8), part of C5's cost.  RCCL refuses two ranks on one
+    # GPU, so the one-GPU rehearsal (UWVK_BENCH_SAME_DEVICE) sums over gloo;
+    # UWVK_BENCH_COLL=host does the same on purpose (A/B).
+    coll = "host" if (same_dev or os.environ.get("UWVK_BENCH_COLL") == "host") else "rccl"
     comm = None
-    coll = os.environ.get("UWVK_BENCH_COLL", "host")
-
-    def make_comm():
+    if dist is not None and world > 1 and coll == "rccl":
         uid = [engine.RcclComm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        return engine.RcclComm(world, uid[0], rank, local)
+        comm = engine.RcclComm(world, uid[0], rank, local)
 
-    if dist is not None and coll == "rccl":
-        comm = make_comm()
-    # warm the statistics kernels and the collective (module load, communicator
-    # set-up) outside the timed region
-    st_w = f.ensemble_stats(truth, comm)
-    if dist is not None and comm is None:
-        ensemble.allreduce_stats(st_w, dist, device=stat_dev)
+    def reduce_stats(truth):
+        st = f.ensemble_stats(truth, comm)
+        if dist is not None and world > 1 and comm is None:
+            st = ensemble.allreduce_stats(st, dist)
+        return st
+
+    # statistics points inside the window: every --stats-every epochs, and its end
+    every = max(1, a.stats_every)
+    cuts = sorted({min(a.steps, k) for k in range(every, a.steps, every)} | {a.steps})
+    # warm the statistics kernels and the collective (module load, RCCL
+    # channel set-up) outside the timed region
+    reduce_stats(log["truth"].state(e0, a.dof))
 
     def barrier():
         if dist is not None:
@@ -294,65 +372,72 @@ def main():
     f.synchronize()
     t0 = time.perf_counter()
     f.timer_start()
-    f.run_log(dlog, e0, a.steps, sync=False)
-    f.timer_mark()  # HIP events on the handle's stream around the epoch launches (no host wait)
-    # synchronous; RCCL over xGMI (comm) is the only collective of the workload
-    stats = f.ensemble_stats(truth, comm)
-    if dist is not None and comm is None:
-        stats = ensemble.allreduce_stats(stats, dist, device=stat_dev)
+    prev = 0
+    stats = None
+    for k, cut in enumerate(cuts):
+        f.run_log(dlog, e0 + prev, cut - prev, sync=False)
+        if k == len(cuts) - 1:
+            f.timer_mark()  # HIP events on the handle's stream around the epoch launches (no host wait)
+        stats = reduce_stats(log["truth"].state(e0 + cut, a.dof))  # synchronous
+        prev = cut
     f.synchronize()
     barrier()
     wall = time.perf_counter() - t0
     kernel_ms = f.timer_elapsed()
     if dist is not None:
         import torch
-        w = torch.tensor([wall], dtype=torch.float64)
-        if stat_dev:
-            w = w.cuda()
+        w = torch.tensor([wall, kernel_ms], dtype=torch.float64)
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
-        wall = float(w.item())
-    # untimed: the same sum through the engine's RCCL path (uwvk_pose_ensemble_allreduce)
-    rccl_check = None
-    same_dev = os.environ.get("UWVK_BENCH_SAME_DEVICE") == "1"  # RCCL refuses two ranks on one GPU
-    if dist is not None and comm is None and not same_dev and os.environ.get("UWVK_BENCH_RCCL_CHECK", "1") == "1":
-        try:  # a cross-check after timing: its failure is reported, it does not void the line
-            comm = make_comm()
-            rs = f.ensemble_stats(truth, comm)
-            rccl_check = bool(np.allclose(rs, stats, rtol=1e-12, atol=1e-12))
-        except Exception as ex:  # noqa: BLE001
-            print("warning: RCCL cross-check failed: %r" % (ex,), file=sys.stderr)
-            rccl_check = False
+        wall, kernel_ms = float(w[0]), float(w[1])
+    # untimed check of the collective: the RCCL sum equals the gloo sum of the
+    # per-rank statistics (same fixed-order kernel sums on every rank)
+    coll_check = None
+    if dist is not None and world > 1:
+        local_st = f.ensemble_stats(log["truth"].state(e0 + a.steps, a.dof))
+        host_sum = ensemble.allreduce_stats(local_st, dist)
+        coll_check = bool(np.allclose(host_sum, stats, rtol=1e-12, atol=1e-12))
+        if not coll_check:
+            print("error: the all-reduced ensemble statistics differ from the host sum", file=sys.stderr)
     status = f.get_status()
     if status.any():
         print("warning: %d instances flagged (status bits)" % int((status != 0).sum()), file=sys.stderr)
 
     steps_total = B * world * a.steps
     value = steps_total / wall
-    # launches in the timed window: the PSP path runs the whole window in one
-    # k_psp_epoch launch (efforts epochs split it); the literal path one per epoch
+    # launches in the timed window: the PSP path runs each statistics interval
+    # in one k_psp_epoch launch (efforts epochs split it); the literal path one per epoch
     n_eff = int(((window & 0x10) != 0).sum())
-    launches = a.steps if a.dense else 1 + 2 * n_eff
+    launches = a.steps if a.dense else len(cuts) + 2 * n_eff
     per_launch_ms = kernel_ms / launches
     # reference-equivalent work (the literal ukfom algorithm)
     flops_ref = B * (F_STEP * a.steps + F_UPD3 * n_dvl)
-    # the engine's own flop model
+    # the engine's own flop model: the useful work it does
     flops_model = B * ((F_STEP_EXEC * a.steps + F_UPD3_EXEC * n_dvl) if a.dense
                        else (F_STEP_PSP * a.steps + F_UPD3_PSP * n_dvl))
     eff_tf = flops_ref / (kernel_ms * 1e-3) / 1e12
     model_tf = flops_model / (kernel_ms * 1e-3) / 1e12
     kname = ("k_pose_epoch<%d>" if a.dense else "k_psp_epoch<%d>") % a.dof
-    workload = "%s-dof%d-b%d%s" % (a.mode, a.dof, B, "-dense" if a.dense else "")
+    workload = "%s-dof%d-b%d%s" % (log_mode, a.dof, B, "-dense" if a.dense else "")
     pmc = pmc_entry(workload, a.steps)
     cr = None if a.dense or launches != 1 else counter_roofline(pmc, B, a.steps, kernel_ms)
-    traffic = pmc.get("bytes_per_launch") if pmc.get("epochs_per_launch") == a.steps else None
-    achieved = cr["achieved_tflops"] if cr else model_tf
-    roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
+    traffic = pmc.get("bytes_per_launch") if pmc.get("epochs_per_launch") == a.steps and launches == 1 else None
+    frac_useful = model_tf / PEAK_FP64_TFLOPS
+    frac_issued = cr["achieved_tflops"] / PEAK_FP64_TFLOPS if cr else None
+    lanes = ((cr or {}).get("active_lanes") or {}).get("thread_cycles_per_valu_quad_cycle")
+    frac_active = frac_issued * lanes / 64.0 if (frac_issued is not None and lanes) else None
+    roof = {"bound": "valu-fp64", "achieved": model_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+            "frac": frac_useful, "traffic": traffic,
+            "frac_useful": frac_useful, "frac_active": frac_active, "frac_issued": frac_issued,
             "kernel": kname, "launches": launches, "kernel_ms_per_launch": per_launch_ms,
-            "achieved_source": ("fp64 VALU lane-flops from SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 of the committed PMC "
-                                "passes of this launch shape (%s), over this run's HIP-event kernel time"
-                                % (cr or {}).get("source") if cr else
-                                "the engine's flop model (no PMC pass of this shape committed)"),
+            "achieved_source": "the engine's useful-flop model (bench.py psp_flops: k-column partial Cholesky, "
+                               "2k+1 model evaluations, O(n^2) covariance algebra per step, DESIGN.md 4.3) over this "
+                               "run's HIP-event kernel time; frac = frac_useful",
+            "frac_issued_source": ("fp64 VALU lane-slot flops, 64 x (2 SQ_INSTS_VALU_FMA_F64 + SQ_INSTS_VALU_MUL_F64 "
+                                   "+ SQ_INSTS_VALU_ADD_F64) per wave-epoch from the committed PMC passes of this "
+                                   "launch shape (%s), over this run's kernel time: counts masked lanes, an upper "
+                                   "bound" % (cr or {}).get("source")) if cr else None,
+            "frac_active_source": ("frac_issued x SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / 64 (%.1f of 64 lanes "
+                                   "active per VALU cycle)" % lanes) if frac_active is not None else None,
             "counters": cr,
             "model_flop_per_step": (F_STEP_EXEC if a.dense else F_STEP_PSP),
             "model_tflops": model_tf,
@@ -362,45 +447,57 @@ def main():
                               "same result with ~3.4% of those flops (DESIGN.md 4.3), so this is not a roofline",
             "traffic_source": ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes, the timed launch of this shape "
                                "(%s)" % pmc.get("source")) if traffic else None}
+    if mode == "C5":
+        desc = "C5: %d Monte-Carlo PoseUKF %d-DOF instances, %d per GPU, 1 kHz IMU + 5 Hz DVL, ensemble statistics " \
+               "all-reduced every %d epochs and at the window's end" % (B * world, a.dof, B, every)
+    else:
+        desc = "%s: PoseUKF %d-DOF, batch %d per GPU, 1 kHz IMU + 5 Hz DVL%s" % (
+            mode, a.dof, B, " + ADCP x4 + DVL drop-out/efforts + pressure" if mode == "C4" else "")
+    if dist is None or world == 1:
+        coll_desc = None
+    elif comm is not None:
+        coll_desc = "RCCL all_reduce of the ensemble statistics on the handle's stream (uwvk_pose_ensemble_allreduce)"
+    else:
+        coll_desc = "gloo all_reduce of the ensemble statistics (host)%s" % (
+            ": RCCL refuses two ranks on one GPU (UWVK_BENCH_SAME_DEVICE rehearsal)" if same_dev else "")
     out = {
         "metric": METRIC, "value": value, "unit": "steps/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": "%s: PoseUKF %d-DOF, batch %d per GPU, 1 kHz IMU + 5 Hz DVL%s"
-                               % (a.mode, a.dof, B, " + ADCP x4 + DVL drop-out/efforts + pressure"
-                                  if a.mode == "C4" else ""),
+        "config": {"workload": desc,
                    "global_batch": B * world, "batch_per_gpu": B, "step": "one IMU epoch per instance",
                    "dvl_epochs_in_window": n_dvl,
                    "efforts_epochs_in_window": n_eff,
                    "adcp_epochs_in_window": int(((window & 8) != 0).sum()),
-                   "c4_cycle_s": list(cyc) if a.mode == "C4" else None,
+                   "c4_cycle_s": list(cyc) if mode == "C4" else None,
                    "parallelism": "instance-sharded x%d (no data-path collective)" % world,
-                   "collective": (("RCCL all_reduce of the ensemble statistics on the handle's stream "
-                                   "(uwvk_pose_ensemble_allreduce)") if coll == "rccl" else
-                                  ("%s all_reduce of the ensemble statistics (host); untimed RCCL cross-check: %s"
-                                   % (backend, rccl_check))) if dist else None,
+                   "collective": coll_desc,
+                   "stats_allreduces_in_window": len(cuts) if world > 1 else 0,
+                   "same_device_rehearsal": same_dev,
                    "path": "dense (all 2n+1 sigma points)" if a.dense else "PSP (partitioned sigma points)",
                    "kernel": kname},
+        "collective_check": coll_check,
         "roofline": roof,
         "timing": {"wall_ms": wall * 1e3, "kernel_ms": kernel_ms, "outside_kernel_ms": wall * 1e3 - kernel_ms},
         "ensemble": {"nees_mean_pos_ori_vel": float(stats[-2] / max(1.0, B * world - stats[-1])),
                      "nees_excluded_instances": int(stats[-1])},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(synth, cfg, uwv, a.mode, a.dof, a.cpu_threads or available_cores())
+        out["cpu_baseline"] = cpu_baseline(synth, cfg, uwv, log_mode, a.dof, a.cpu_threads or available_cores())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:
         comm.close()
     if dist is not None:
         dist.destroy_process_group()
+    if coll_check is False:
+        sys.exit(3)
 
 
-def bench_vel(a, engine, synth, world, rank, local, dist):
+def bench_vel(a, engine, synth, world, rank, local, dist, B):
     """Config C2: VelocityUKF (VelocityUKF.cpp:79-130), batch 4096 per GPU,
     1 kHz gyro + efforts, 5 Hz DVL, 10 Hz pressure.  One step = one epoch of
     one instance (gyro/efforts store, predict, due updates)."""
-    B = a.batch_per_gpu or 4096
     log = synth.make_vel_log(B, a.warmup + a.steps, first_instance=rank * B)
     f = engine.VelocityUKFBatch(B, device=local)
     f.set_lane_groups(a.vel_groups)
@@ -438,7 +535,7 @@ def bench_vel(a, engine, synth, world, rank, local, dist):
         "config": {"workload": "C2: VelocityUKF 4-DOF, batch %d per GPU, 1 kHz gyro + efforts, 5 Hz DVL, 10 Hz depth"
                                % B, "global_batch": B * world, "batch_per_gpu": B,
                    "layout": "16 lanes per filter" if groups else "one filter per lane", "kernel": kname},
-        "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+        "roofline": {"bound": "valu-fp64", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                      "frac": tf / PEAK_FP64_TFLOPS, "traffic": None, "kernel": kname, "launches": launches,
                      "kernel_ms_per_launch": kernel_ms / launches, "algorithmic_flop_per_step": F_VEL_STEP},
     }

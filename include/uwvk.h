@@ -34,7 +34,14 @@
 extern "C" {
 #endif
 
-#define UWVK_ABI_VERSION 1
+/* ABI history.  A caller checks uwvk_abi_version() == UWVK_ABI_VERSION of the
+ * header it was built against (the Python binding and the C++ facade do).
+ *   1  round 1.
+ *   2  uwvk_pose_ensemble_stats / _allreduce write 3*store+2 doubles (was
+ *      3*store+1: the count of instances left out of the NEES sum was added);
+ *      uwvk_pose_init_from_state reads only the lower triangle of P;
+ *      uwvk_memcpy_h2d / _d2h wait for the buffer's own device only. */
+#define UWVK_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum uwvk_status {
@@ -171,8 +178,10 @@ int uwvk_device_available(int device);
 const char* uwvk_status_string(uwvk_status s);
 
 /* device memory helpers for device-resident logs (bench / run_log).
- * uwvk_memcpy_h2d / _d2h are synchronous with ALL device work (they wait for
- * every stream, the handles' non-blocking ones included, then copy).
+ * uwvk_memcpy_h2d / _d2h are synchronous with all work on the device that owns
+ * the device-side buffer (they make that device current, wait for every
+ * stream on it, the handles' non-blocking ones included, then copy); work
+ * queued on OTHER devices is not waited for.
  * uwvk_memcpy_*_on are ordered on one stream (a handle's uwvk_*_stream) and
  * return once the copy has completed. */
 uwvk_status uwvk_device_malloc(int device, size_t bytes, void** out);
@@ -181,6 +190,14 @@ uwvk_status uwvk_memcpy_h2d(void* dst, const void* src, size_t bytes);
 uwvk_status uwvk_memcpy_d2h(void* dst, const void* src, size_t bytes);
 uwvk_status uwvk_memcpy_h2d_on(void* dst, const void* src, size_t bytes, void* stream);
 uwvk_status uwvk_memcpy_d2h_on(void* dst, const void* src, size_t bytes, void* stream);
+
+/* Synthetic-log noise (host only, no device work): out[j * count + k] is the
+ * k-th standard normal variate of stream `stream` (< 256) of global instance
+ * first_instance + j, a pure function of (seed, instance, stream, k):
+ * Philox4x32-10 blocks, Box-Muller (csrc/uwvk_synth.cpp).  Instance-sharded
+ * runs therefore draw bitwise the rows of the full batch. */
+uwvk_status uwvk_synth_normal(uint64_t seed, int64_t first_instance, int64_t batch, uint32_t stream, int64_t count,
+                              double* out);
 
 /* ======================================================================== */
 /* PoseUKF                                                                   */
@@ -387,6 +404,11 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   for that many resident blocks per XCD (tests); < 0: off.  Needs
  *   batch % 8 == 0. */
 #define UWVK_OPT_TAIL_SLOTS 3
+/* UWVK_OPT_TAIL_CHUNKS: 0 (default) the planner picks the chunk count; 2..8
+ *   forces that many chunks per tail instance whenever the launch allows it
+ *   (chunks x slots <= batch / 8, chunks <= epochs), for tests.  Spreading of
+ *   any kind runs only where uwvk_xcd_round_robin(device) is 1. */
+#define UWVK_OPT_TAIL_CHUNKS 4
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
 /* Host-only query (no device work): the chunks per tail instance the
  * UWVK_OPT_TAIL_SLOTS planner picks for one XCD's instances over its resident
@@ -396,6 +418,12 @@ int uwvk_pose_tail_chunks(int64_t instances_per_xcd, int64_t slots_per_xcd, int6
  * device (occupancy x CUs / 8; what UWVK_OPT_TAIL_SLOTS = 0 plans for), 0 if
  * unknown. */
 int64_t uwvk_pose_resident_slots(int dof, int device);
+/* 1 when a probe grid on device showed round-robin workgroup placement over 8
+ * XCCs (block b on the XCC of block b % 8, read from the hardware XCC_ID
+ * register): the placement tail spreading's hand-off order relies on.  0 on a
+ * partitioned device (or any other placement): spreading is then off.  The
+ * probe runs once per device and process. */
+int uwvk_xcd_round_robin(int device);
 
 /* Kernel-timing helper: HIP events recorded on the handle's stream. */
 uwvk_status uwvk_pose_timer_start(uwvk_pose* h);

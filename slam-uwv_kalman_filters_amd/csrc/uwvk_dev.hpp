@@ -17,6 +17,25 @@
 
 namespace uwvk {
 
+// Host side: every C-ABI entry point that takes a handle makes the handle's
+// device current for the duration of the call (allocations, launches, copies)
+// and restores the caller's device on return, so one thread may drive handles
+// on several GPUs.  device < 0 (a null handle): no-op.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int device) {
+    int cur = -1;
+    if (device < 0 || hipGetDevice(&cur) != hipSuccess || cur == device) return;
+    if (hipSetDevice(device) == hipSuccess) prev = cur;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+#define UWVK_DEVICE_GUARD(h) ::uwvk::DeviceGuard uwvk_device_guard_((h) ? (h)->device : -1)
+
 constexpr double kEarthW = 7.292115e-5;  // pose_estimation::EARTHW [EXT] (PoseUKF.cpp:30)
 constexpr double kD2P95 = 5.991;         // PoseUKF.cpp:275-286
 

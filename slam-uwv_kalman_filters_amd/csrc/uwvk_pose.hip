@@ -55,6 +55,7 @@ struct uwvk_pose {
   int dense = 0;  // UWVK_OPT_DENSE_SIGMA
   // last-generation spreading of the PSP epoch launch (UWVK_OPT_TAIL_SLOTS)
   int64_t tail_slots = 0;  // resident blocks per XCD to plan for: 0 auto, < 0 off
+  int tail_force = 0;      // UWVK_OPT_TAIL_CHUNKS: >= 2 forces that many chunks (tests)
   std::map<std::array<int64_t, 3>, int> tail_chunks;  // (instances per XCD, slots, epochs) -> chunks
   uint32_t* d_tail_flag = nullptr;  // per tail instance (batch / 8 - 1 per XCD at most)
   double* d_tail_carry = nullptr;   // per tail instance: 64 x (ds, ids)
@@ -187,6 +188,7 @@ static bool finite_all(const double* a, size_t n) {
 extern "C" {
 
 uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out) {
+  ::uwvk::DeviceGuard uwvk_device_guard_(device);
   if (!out || batch <= 0 || (dof != 53 && dof != 26)) return UWVK_EINVAL;
   *out = nullptr;
   if (!uwvk_device_available(device)) return UWVK_EDEVICE;
@@ -227,6 +229,7 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
 }
 
 void uwvk_pose_destroy(uwvk_pose* h) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_Q, (void*)h->d_rot, (void*)h->d_off,
@@ -245,6 +248,7 @@ int64_t uwvk_pose_batch(const uwvk_pose* h) { return h ? h->batch : 0; }
 int uwvk_pose_dof(const uwvk_pose* h) { return h ? h->dof : 0; }
 void* uwvk_pose_stream(const uwvk_pose* h) { return h ? (void*)h->stream : nullptr; }
 uwvk_status uwvk_pose_synchronize(uwvk_pose* h) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   return hipStreamSynchronize(h->stream) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
 }
@@ -287,6 +291,7 @@ static uwvk_status upload_state(uwvk_pose* h, const std::vector<double>& x, cons
 uwvk_status uwvk_pose_init_from_config(uwvk_pose* h, const double* pos, const double* pos_cov, const double* rot,
                                        const double* rot_cov, const uwvk_pose_config* cfg, const uwvk_uwv_params* uwv,
                                        const double imu_in_body[7]) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !pos || !pos_cov || !rot || !rot_cov || !cfg || !uwv) return UWVK_EINVAL;
   const int64_t B = h->batch;
   const int n = h->dof, s = h->store;
@@ -304,6 +309,7 @@ uwvk_status uwvk_pose_init_from_config(uwvk_pose* h, const double* pos, const do
 
 uwvk_status uwvk_pose_init_from_state(uwvk_pose* h, const double* x, const double* P, const uwvk_location* loc,
                                       const uwvk_uwv_params* uwv, const uwvk_pose_parameter* param) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !x || !P || !loc || !uwv || !param) return UWVK_EINVAL;
   const int64_t B = h->batch;
   const int n = h->dof, s = h->store;
@@ -318,6 +324,7 @@ uwvk_status uwvk_pose_init_from_state(uwvk_pose* h, const double* x, const doubl
 
 uwvk_status uwvk_pose_set_process_noise_from_config(uwvk_pose* h, const uwvk_pose_config* cfg, double imu_delta_t,
                                                     const double q_imu_in_body[4]) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !cfg || !(imu_delta_t > 0)) return UWVK_EINVAL;
   std::vector<double> Q(h->dof * h->dof);
   host::pose_process_noise(h->dof, *cfg, imu_delta_t, q_imu_in_body, Q.data());
@@ -325,6 +332,7 @@ uwvk_status uwvk_pose_set_process_noise_from_config(uwvk_pose* h, const uwvk_pos
 }
 
 uwvk_status uwvk_pose_set_process_noise(uwvk_pose* h, const double* Q) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !Q) return UWVK_EINVAL;
   HIPCHK(hipMemcpyAsync(h->d_Q, Q, (size_t)h->dof * h->dof * 8, hipMemcpyHostToDevice, h->stream));
   h->Qh.assign(Q, Q + (size_t)h->dof * h->dof);
@@ -341,6 +349,7 @@ uwvk_status uwvk_pose_set_process_noise(uwvk_pose* h, const double* Q) {
 }
 
 uwvk_status uwvk_pose_set_rotation_rate(uwvk_pose* h, const double* w, const double* cov) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !w) return UWVK_EINVAL;
   if (!finite_all(w, (size_t)h->batch * 3) || (cov && !finite_all(cov, (size_t)h->batch * 9))) return UWVK_ENAN;
   HIPCHK(hipMemcpyAsync(h->d_rot, w, (size_t)h->batch * 3 * 8, hipMemcpyHostToDevice, h->stream));
@@ -349,6 +358,7 @@ uwvk_status uwvk_pose_set_rotation_rate(uwvk_pose* h, const double* w, const dou
 }
 
 uwvk_status uwvk_pose_predict(uwvk_pose* h, double dt) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   PoseBufs b = bufs(h);
@@ -420,36 +430,44 @@ extern "C" {
 
 uwvk_status uwvk_pose_update_acceleration(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
                                           const uint8_t* mask, uint8_t* acc) {
+  UWVK_DEVICE_GUARD(h);
   return launch_update<MK_ACC>(h, 3, mu, cov, sc, mask, acc, nullptr, 0, nullptr, 0);
 }
 uwvk_status uwvk_pose_update_velocity(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
                                       const uint8_t* mask, uint8_t* acc) {
+  UWVK_DEVICE_GUARD(h);
   return launch_update<MK_VEL>(h, 3, mu, cov, sc, mask, acc, nullptr, 0, nullptr, 0);
 }
 uwvk_status uwvk_pose_update_pressure(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
                                       const double sensor_in_imu[3], const uint8_t* mask, uint8_t* acc) {
+  UWVK_DEVICE_GUARD(h);
   const double zero[3] = {0, 0, 0};
   return launch_update<MK_PRESSURE>(h, 1, mu, cov, sc, mask, acc, nullptr, 0, sensor_in_imu ? sensor_in_imu : zero, 0);
 }
 uwvk_status uwvk_pose_update_water_velocity(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
                                             const double* cw, const uint8_t* mask, uint8_t* acc) {
+  UWVK_DEVICE_GUARD(h);
   if (!cw) return UWVK_EINVAL;
   return launch_update<MK_WATER>(h, 2, mu, cov, sc, mask, acc, cw, 1, nullptr, 0);
 }
 uwvk_status uwvk_pose_update_efforts(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
                                      int only_affect_velocity, const uint8_t* mask, uint8_t* acc) {
+  UWVK_DEVICE_GUARD(h);
   return launch_update<MK_EFFORTS>(h, 6, mu, cov, sc, mask, acc, nullptr, 0, nullptr, only_affect_velocity ? 1 : 0);
 }
 uwvk_status uwvk_pose_update_xy(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
                                 const uint8_t* mask, uint8_t* acc) {
+  UWVK_DEVICE_GUARD(h);
   return launch_update<MK_XY>(h, 2, mu, cov, sc, mask, acc, nullptr, 0, nullptr, 0);
 }
 uwvk_status uwvk_pose_update_z(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
                                const uint8_t* mask, uint8_t* acc) {
+  UWVK_DEVICE_GUARD(h);
   return launch_update<MK_Z>(h, 1, mu, cov, sc, mask, acc, nullptr, 0, nullptr, 0);
 }
 uwvk_status uwvk_pose_update_geographic(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
                                         const double gps_in_body[3], const uint8_t* mask, uint8_t* acc) {
+  UWVK_DEVICE_GUARD(h);
   const double zero[3] = {0, 0, 0};
   return launch_update<MK_GEO>(h, 2, mu, cov, sc, mask, acc, nullptr, 0, gps_in_body ? gps_in_body : zero, 0);
 }
@@ -461,6 +479,7 @@ uwvk_status uwvk_pose_update_visual_landmark(uwvk_pose* h, int32_t n_features, c
                                              int marker_pose_per_instance, const double cov_marker_pose[36],
                                              const double camera[4], const double camera_in_imu[7],
                                              const uint8_t* mask) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   aug::VisArgs va{};
@@ -478,11 +497,13 @@ uwvk_status uwvk_pose_update_visual_landmark(uwvk_pose* h, int32_t n_features, c
 
 uwvk_status uwvk_pose_update_delayed_xy(uwvk_pose* h, const double* mu, const double* cov, const double* sc,
                                         const double* delayed_xy, const uint8_t* mask, uint8_t* acc) {
+  UWVK_DEVICE_GUARD(h);
   if (!delayed_xy) return UWVK_EINVAL;
   return launch_update<MK_DELAYED>(h, 2, mu, cov, sc, mask, acc, delayed_xy, 2, nullptr, 0);
 }
 
 uwvk_status uwvk_pose_reset_with_external_pose(uwvk_pose* h, const double* pose) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !pose) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   const int64_t B = h->batch;
@@ -496,6 +517,7 @@ uwvk_status uwvk_pose_reset_with_external_pose(uwvk_pose* h, const double* pose)
 }
 
 uwvk_status uwvk_pose_get_state(uwvk_pose* h, double* x, double* P) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !x) return UWVK_EINVAL;
   HIPCHK(hipMemcpyAsync(x, h->d_mu, (size_t)h->batch * h->store * 8, hipMemcpyDeviceToHost, h->stream));
   if (!P) {
@@ -517,6 +539,7 @@ uwvk_status uwvk_pose_get_state(uwvk_pose* h, double* x, double* P) {
 }
 
 uwvk_status uwvk_pose_get_rotation_rate(uwvk_pose* h, double* out) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !out) return UWVK_EINVAL;
   PoseBufs b = bufs(h);
   PoseShared sh = h->sh;
@@ -528,6 +551,7 @@ uwvk_status uwvk_pose_get_rotation_rate(uwvk_pose* h, double* out) {
 }
 
 uwvk_status uwvk_pose_get_status(uwvk_pose* h, uint32_t* status, int clear) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !status) return UWVK_EINVAL;
   HIPCHK(hipMemcpyAsync(status, h->d_status, (size_t)h->batch * 4, hipMemcpyDeviceToHost, h->stream));
   if (clear) HIPCHK(hipMemsetAsync(h->d_status, 0, (size_t)h->batch * 4, h->stream));
@@ -540,7 +564,7 @@ uwvk_status uwvk_pose_get_status(uwvk_pose* h, uint32_t* status, int clear) {
 static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
   ea.chunks = 1;
   grid = 0;
-  if (h->tail_slots < 0 || h->batch % 8 != 0) return hipSuccess;
+  if (h->tail_slots < 0 || h->batch % 8 != 0 || !xcd_round_robin(h->device)) return hipSuccess;
   const int64_t n = h->batch / 8;
   const int64_t s = h->tail_slots > 0 ? h->tail_slots : psp_epoch_slots_per_xcd(h->dof, h->device);
   const std::array<int64_t, 3> key{n, s, ea.count};
@@ -549,7 +573,9 @@ static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
     if (h->tail_chunks.size() >= 64) h->tail_chunks.clear();
     it = h->tail_chunks.emplace(key, plan_tail(n, s, ea.count)).first;
   }
-  const int c = it->second;
+  int c = it->second;
+  if (h->tail_force >= 2)  // forced (tests): every chunk count, where the shape allows it
+    c = (s > 0 && h->tail_force <= 8 && h->tail_force * s <= n && h->tail_force <= ea.count) ? h->tail_force : 1;
   if (c <= 1) return hipSuccess;
   const int64_t r = c * s;
   if (8 * r > h->tail_inst_cap) {  // sized once for the largest plan (8 chunks) of these slots
@@ -581,12 +607,17 @@ static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
   ea.r_x = r;
   ea.chunks = c;
   ea.tag = h->tail_tag;
+  // a chunk waits at most for its predecessors' (c - 1) / c of the launch's
+  // epochs; one sleep is ~1.7 us and an epoch ~20 us per wave at full
+  // occupancy: 64 sleeps per epoch is a wide margin, plus ~2 s of slack
+  ea.wait_bound = (uint32_t)std::min<uint64_t>(0xffffffffull, (1ull << 20) + 64ull * (uint64_t)ea.count);
   grid = 8 * (n + (c - 1) * r);
   return hipSuccess;
 }
 
 uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t first, int64_t count,
                               uint32_t* accept_counts) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !log || first < 0 || count < 0 || first + count > log->epochs || log->adcp_cells > 8) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   EpochArgs ea{};
@@ -648,10 +679,12 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
 }
 
 uwvk_status uwvk_pose_ensemble_stats(uwvk_pose* h, const double* truth, double* out) {
+  UWVK_DEVICE_GUARD(h);
   return uwvk_pose_ensemble_allreduce(h, truth, out, nullptr);
 }
 
 uwvk_status uwvk_pose_ensemble_allreduce(uwvk_pose* h, const double* truth, double* out, void* comm) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !out) return UWVK_EINVAL;
   const int s = h->store;
   const int nout = 3 * s + 2;
@@ -673,6 +706,7 @@ uwvk_status uwvk_pose_ensemble_allreduce(uwvk_pose* h, const double* truth, doub
 }
 
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   if (option == UWVK_OPT_LITERAL_APPLY_DELTA) {
     h->sh.literal_apply_delta = value ? 1 : 0;
@@ -686,6 +720,11 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
     h->tail_slots = value;
     return UWVK_OK;
   }
+  if (option == UWVK_OPT_TAIL_CHUNKS) {
+    if (value < 0 || value > 8) return UWVK_EINVAL;
+    h->tail_force = value;
+    return UWVK_OK;
+  }
   return UWVK_EINVAL;
 }
 
@@ -694,16 +733,20 @@ int64_t uwvk_pose_resident_slots(int dof, int device) {
   return psp_epoch_slots_per_xcd(dof, device);
 }
 
+int uwvk_xcd_round_robin(int device) { return xcd_round_robin(device); }
+
 int uwvk_pose_tail_chunks(int64_t instances_per_xcd, int64_t slots_per_xcd, int64_t epochs) {
   return plan_tail(instances_per_xcd, slots_per_xcd, epochs);
 }
 
 uwvk_status uwvk_pose_timer_start(uwvk_pose* h) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   HIPCHK(hipEventRecord(h->ev0, h->stream));
   return UWVK_OK;
 }
 uwvk_status uwvk_pose_timer_stop(uwvk_pose* h, float* ms) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !ms) return UWVK_EINVAL;
   HIPCHK(hipEventRecord(h->ev1, h->stream));
   HIPCHK(hipEventSynchronize(h->ev1));
@@ -711,11 +754,13 @@ uwvk_status uwvk_pose_timer_stop(uwvk_pose* h, float* ms) {
   return UWVK_OK;
 }
 uwvk_status uwvk_pose_timer_mark(uwvk_pose* h) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   HIPCHK(hipEventRecord(h->ev1, h->stream));
   return UWVK_OK;
 }
 uwvk_status uwvk_pose_timer_elapsed(uwvk_pose* h, float* ms) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !ms) return UWVK_EINVAL;
   HIPCHK(hipEventSynchronize(h->ev1));
   HIPCHK(hipEventElapsedTime(ms, h->ev0, h->ev1));

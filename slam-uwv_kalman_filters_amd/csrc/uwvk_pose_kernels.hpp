@@ -59,6 +59,7 @@ struct EpochArgs {
   int64_t r_x;          // tail instances per XCD (chunks x resident blocks)
   int chunks;
   uint32_t tag;         // per launch
+  uint32_t wait_bound;  // tail_wait: sleeps before a hand-off counts as lost
 };
 
 // host-callable launchers (grid = one workgroup per instance)

@@ -15,4 +15,7 @@ int64_t psp_epoch_slots_per_xcd(int dof, int device);
 // chunks per tail instance for one XCD's n instances over s resident blocks in
 // a count-epoch launch (1: no tail spreading)
 int plan_tail(int64_t n, int64_t s, int64_t count);
+// 1 once a probe grid has shown round-robin block placement over 8 XCCs on
+// device (what tail spreading relies on), else 0; cached per device
+int xcd_round_robin(int device);
 }  // namespace uwvk

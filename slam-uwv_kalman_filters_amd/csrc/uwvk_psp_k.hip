@@ -34,8 +34,9 @@ UWVK_DEV void tl_mark(int64_t w, int k) {
 // tail-chunk hand-off (EpochArgs::chunks > 1).  Chunk k of a tail instance is
 // placed later in its XCD's block order than chunk k - 1 (plan_tail), and
 // blocks are dispatched in order, so the block waited for is resident or done:
-// the wait cannot deadlock.  The bound (about 4 s) only keeps a broken
-// ordering from hanging the device; it flags the instance and goes on.
+// the wait cannot deadlock.  The host enables spreading only after
+// xcd_round_robin() has seen, on this device, that block b runs on XCC b % 8
+// (the hardware XCC_ID register), the placement the plan relies on.
 struct TailUnit {
   int64_t inst, e0, e1, tslot;
   int chunk;  // >= 0: a chunk of a tail instance
@@ -59,17 +60,24 @@ UWVK_DEV TailUnit tail_unit(const EpochArgs& ea, int64_t B) {
   return u;
 }
 
-__device__ __attribute__((noinline)) void tail_wait(const EpochArgs& ea, int64_t t, int chunk, uint32_t* status) {
+// Waits for the predecessor chunk's signal.  The bound (ea.wait_bound sleeps
+// of ~1.7 us, scaled by the host with the launch's epoch count) only keeps a
+// broken ordering from hanging the device: past it the instance is flagged
+// UWVK_ST_SCHEDULE and false is returned, and the caller skips the whole chunk
+// (no load, no epochs, no store, no signal), so nothing races the late
+// predecessor; every later chunk of the instance then times out the same way.
+// (scalar arguments: with the EpochArgs reference the caller kept a copy of
+// the kernel arguments in scratch, 150 -> 173 VGPRs and 800 B/lane)
+__device__ __attribute__((noinline)) bool tail_wait(uint32_t* f, uint32_t want, uint32_t bound) {
+  uint32_t n = 0;
   if (lane_id() == 0) {
-    const uint32_t want = ea.tag * 16u + (uint32_t)chunk;
-    uint32_t* f = ea.tail_flag + t;
-    int n = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want && ++n < (1 << 20))
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want && ++n < bound)
       __builtin_amdgcn_s_sleep(64);
-    if (n >= (1 << 20)) *status |= UWVK_ST_SCHEDULE;
   }
+  n = __builtin_amdgcn_readfirstlane(n);  // lane 0's count, wave-uniform
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous chunk's stores, from any CU
+  return n < bound;
 }
 __device__ __attribute__((noinline)) double2 tail_carry_in(const EpochArgs& ea, int64_t t) {
   return reinterpret_cast<const double2*>(ea.tail_carry)[t * 64 + lane_id()];
@@ -288,7 +296,11 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
   const int64_t B = b.batch;
   TailUnit tu = tail_unit(ea, B);
   const int64_t inst = tu.inst, e_begin = tu.e0, e_end = tu.e1;
-  if (tu.chunk > 0) tail_wait(ea, tu.tslot, tu.chunk, b.status + inst);
+  if (tu.chunk > 0 && !tail_wait(ea.tail_flag + tu.tslot, ea.tag * 16u + (uint32_t)tu.chunk, ea.wait_bound)) {
+    if (lane_id() == 0)  // atomic: the late predecessor may still flag the same word
+      __hip_atomic_fetch_or(b.status + inst, UWVK_ST_SCHEDULE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
 #ifdef UWVK_STAMPS
   Stamper stamper;
   Stamper* st = &stamper;
@@ -405,8 +417,9 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
     }
   }
   if (lane_id() == 0) {
-    if (!ok) b.status[inst] |= UWVK_ST_NOTPD;
-    if (nan) b.status[inst] |= UWVK_ST_NAN;
+    // atomic: a later chunk that timed out flags the same word
+    const uint32_t bits = (ok ? 0u : UWVK_ST_NOTPD) | (nan ? UWVK_ST_NAN : 0u);
+    if (bits) __hip_atomic_fetch_or(b.status + inst, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (e_end > e_begin) {
       b.rot[inst * 3] = w[0]; b.rot[inst * 3 + 1] = w[1]; b.rot[inst * 3 + 2] = w[2];
     }
@@ -475,6 +488,52 @@ hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const Po
   else
     hipLaunchKernelGGL(psp::k_psp_epoch<26>, g, dim3(64), 0, st, b, sh, ea);
   return hipGetLastError();
+}
+
+// XCC placement probe: block b writes the XCC it runs on (hardware XCC_ID).
+__global__ __launch_bounds__(64) void k_xcc_probe(uint32_t* out) {
+  if (threadIdx.x == 0) {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    out[blockIdx.x] = x & 0xfu;
+  }
+}
+
+// 1 when the blocks of a probe grid were placed round-robin over 8 distinct
+// XCCs (block b on the XCC of block b % 8: the placement of a single-partition MI355X, which the tail
+// plan and xcd_instance assume), else 0.  Measured once per device.
+int xcd_round_robin(int device) {
+  static int cache[64];
+  static bool init = false;
+  if (!init) {
+    for (int& c : cache) c = -1;
+    init = true;
+  }
+  if (device < 0 || device >= 64) return 0;
+  if (cache[device] >= 0) return cache[device];
+  DeviceGuard g(device);
+  constexpr int kBlocks = 8 * 1024;
+  uint32_t* d = nullptr;
+  std::vector<uint32_t> h(kBlocks, 0xffu);
+  int ok = 0;
+  if (hipMalloc(&d, kBlocks * 4) == hipSuccess) {
+    hipLaunchKernelGGL(k_xcc_probe, dim3(kBlocks), dim3(64), 0, 0, d);
+    if (hipGetLastError() == hipSuccess && hipMemcpy(h.data(), d, kBlocks * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+      // blocks b and b + 8 k share an XCC, and the 8 residues cover 8 XCCs
+      ok = 1;
+      bool seen[16] = {};
+      for (int b = 0; b < kBlocks; b++) {
+        if (h[b] >= 16 || h[b] != h[b % 8]) ok = 0;
+        if (b < 8 && h[b] < 16) seen[h[b]] = true;
+      }
+      int distinct = 0;
+      for (bool v : seen) distinct += v;
+      if (distinct != 8) ok = 0;
+    }
+    (void)hipFree(d);
+  }
+  cache[device] = ok;
+  return ok;
 }
 
 int64_t psp_epoch_slots_per_xcd(int dof, int device) {

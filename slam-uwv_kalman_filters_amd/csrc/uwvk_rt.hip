@@ -6,6 +6,7 @@
 #include <cstring>
 
 #include "../../include/uwvk.h"
+#include "uwvk_dev.hpp"
 
 __global__ void uwvk_probe_kernel(int* out) {
   if (threadIdx.x == 0) out[0] = 0x5a5a;
@@ -18,6 +19,7 @@ int uwvk_abi_version(void) { return UWVK_ABI_VERSION; }
 int uwvk_device_available(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return 0;
+  uwvk::DeviceGuard g(device);
   hipDeviceProp_t p;
   if (hipGetDeviceProperties(&p, device) != hipSuccess) return 0;
   if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0) return 0;
@@ -47,19 +49,31 @@ const char* uwvk_status_string(uwvk_status s) {
 }
 
 uwvk_status uwvk_device_malloc(int device, size_t bytes, void** out) {
+  int n = 0;
   if (!out) return UWVK_EINVAL;
-  if (hipSetDevice(device) != hipSuccess) return UWVK_EDEVICE;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return UWVK_EDEVICE;
+  uwvk::DeviceGuard g(device);
   return hipMalloc(out, bytes ? bytes : 16) == hipSuccess ? UWVK_OK : UWVK_ENOMEM;
 }
 uwvk_status uwvk_device_free(void* p) { return hipFree(p) == hipSuccess ? UWVK_OK : UWVK_EDEVICE; }
 // Synchronous with ALL device work: every handle launches on its own
 // non-blocking stream, which the null-stream hipMemcpy does not wait for, so
 // a read after run_log(sync = 0) would otherwise race the epoch kernels.
+// The device that owns the buffer is made current first (hipDeviceSynchronize
+// waits for the CURRENT device only, and a one-process multi-GPU caller may
+// have another device current).
+static int owner_device(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) return -1;
+  return a.type == hipMemoryTypeDevice ? a.device : -1;
+}
 uwvk_status uwvk_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  uwvk::DeviceGuard g(owner_device(dst));
   if (hipDeviceSynchronize() != hipSuccess) return UWVK_EDEVICE;
   return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
 }
 uwvk_status uwvk_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  uwvk::DeviceGuard g(owner_device(src));
   if (hipDeviceSynchronize() != hipSuccess) return UWVK_EDEVICE;
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
 }

@@ -308,6 +308,7 @@ extern "C" {
 
 // ---- BottomUKF -----------------------------------------------------------
 uwvk_status uwvk_bottom_create(int64_t batch, int device, uwvk_bottom** out) {
+  ::uwvk::DeviceGuard uwvk_device_guard_(device);
   if (!out || batch <= 0) return UWVK_EINVAL;
   *out = nullptr;
   if (!uwvk_device_available(device)) return UWVK_EDEVICE;
@@ -324,6 +325,7 @@ uwvk_status uwvk_bottom_create(int64_t batch, int device, uwvk_bottom** out) {
 }
 
 void uwvk_bottom_destroy(uwvk_bottom* h) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return;
   small_destroy(h);
   delete h;
@@ -332,6 +334,7 @@ void uwvk_bottom_destroy(uwvk_bottom* h) {
 void* uwvk_bottom_stream(const uwvk_bottom* h) { return h ? (void*)h->stream : nullptr; }
 
 uwvk_status uwvk_bottom_init(uwvk_bottom* h, const double* x, const double* P) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !x || !P) return UWVK_EINVAL;
   const int64_t B = h->batch;
   if (!finite_all(x, (size_t)B * 4) || !finite_all(P, (size_t)B * 9)) return UWVK_ENAN;
@@ -351,6 +354,7 @@ uwvk_status uwvk_bottom_init(uwvk_bottom* h, const double* x, const double* P) {
 }
 
 uwvk_status uwvk_bottom_set_process_noise(uwvk_bottom* h, const double Q[9]) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !Q) return UWVK_EINVAL;
   if (!finite_all(Q, 9)) return UWVK_ENAN;
   std::memcpy(h->Q.v, Q, sizeof(h->Q.v));
@@ -358,6 +362,7 @@ uwvk_status uwvk_bottom_set_process_noise(uwvk_bottom* h, const double Q[9]) {
 }
 
 uwvk_status uwvk_bottom_set_velocity(uwvk_bottom* h, const double* v) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !v) return UWVK_EINVAL;
   if (!finite_all(v, (size_t)h->batch * 3)) return UWVK_ENAN;
   HIPCHK(hipMemcpyAsync(h->d_aux, v, (size_t)h->batch * 3 * 8, hipMemcpyHostToDevice, h->stream));
@@ -366,6 +371,7 @@ uwvk_status uwvk_bottom_set_velocity(uwvk_bottom* h, const double* v) {
 }
 
 uwvk_status uwvk_bottom_predict(uwvk_bottom* h, double dt) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   hipLaunchKernelGGL(k_bottom_predict, dim3(grid_of(h->batch, BE::IPB)), dim3(BE::BLOCK), 0, h->stream, h->bufs(),
@@ -377,6 +383,7 @@ uwvk_status uwvk_bottom_predict(uwvk_bottom* h, double dt) {
 
 uwvk_status uwvk_bottom_update_range(uwvk_bottom* h, const double* mu, const double* cov, double shared_cov,
                                      const double unit_direction[3], const double origin[3], const uint8_t* mask) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !mu || !unit_direction || !origin) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   const int64_t B = h->batch;
@@ -405,6 +412,7 @@ uwvk_status uwvk_bottom_update_range(uwvk_bottom* h, const double* mu, const dou
 
 uwvk_status uwvk_bottom_update_normal(uwvk_bottom* h, const double* mu, const double* cov, const double* shared_cov,
                                       const uint8_t* mask) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !mu || (!cov && !shared_cov)) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   const int64_t B = h->batch;
@@ -430,13 +438,15 @@ uwvk_status uwvk_bottom_update_normal(uwvk_bottom* h, const double* mu, const do
   return UWVK_OK;
 }
 
-uwvk_status uwvk_bottom_get_state(uwvk_bottom* h, double* x, double* P) { return small_get_state(h, x, P); }
+uwvk_status uwvk_bottom_get_state(uwvk_bottom* h, double* x, double* P) { UWVK_DEVICE_GUARD(h); return small_get_state(h, x, P); }
 uwvk_status uwvk_bottom_get_status(uwvk_bottom* h, uint32_t* status, int clear) {
+  UWVK_DEVICE_GUARD(h);
   return small_get_status(h, status, clear);
 }
 
 // ---- IndirectPoseUKF -------------------------------------------------------
 uwvk_status uwvk_ipose_create(int64_t batch, int device, uwvk_ipose** out) {
+  ::uwvk::DeviceGuard uwvk_device_guard_(device);
   if (!out || batch <= 0) return UWVK_EINVAL;
   *out = nullptr;
   if (!uwvk_device_available(device)) return UWVK_EDEVICE;
@@ -459,6 +469,7 @@ uwvk_status uwvk_ipose_create(int64_t batch, int device, uwvk_ipose** out) {
 }
 
 void uwvk_ipose_destroy(uwvk_ipose* h) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return;
   small_destroy(h);
   delete h;
@@ -469,6 +480,7 @@ void* uwvk_ipose_stream(const uwvk_ipose* h) { return h ? (void*)h->stream : nul
 uwvk_status uwvk_ipose_init(uwvk_ipose* h, const double position_error_std[3], const double orientation_error_std[3],
                             double orientation_error_tau, const double* initial_position_error,
                             const double initial_position_error_std[3]) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !position_error_std || !orientation_error_std) return UWVK_EINVAL;
   if (!(orientation_error_tau > 0.0)) return UWVK_EINVAL;
   const int64_t B = h->batch;
@@ -498,6 +510,7 @@ uwvk_status uwvk_ipose_init(uwvk_ipose* h, const double position_error_std[3], c
 }
 
 uwvk_status uwvk_ipose_set_process_noise(uwvk_ipose* h, const double Q[36]) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !Q) return UWVK_EINVAL;
   if (!finite_all(Q, 36)) return UWVK_ENAN;
   std::memcpy(h->Q.v, Q, sizeof(h->Q.v));
@@ -505,6 +518,7 @@ uwvk_status uwvk_ipose_set_process_noise(uwvk_ipose* h, const double Q[36]) {
 }
 
 uwvk_status uwvk_ipose_set_pose_reference(uwvk_ipose* h, const double* pose) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !pose) return UWVK_EINVAL;
   if (!finite_all(pose, (size_t)h->batch * 7)) return UWVK_ENAN;
   HIPCHK(hipMemcpyAsync(h->d_aux, pose, (size_t)h->batch * 7 * 8, hipMemcpyHostToDevice, h->stream));
@@ -513,6 +527,7 @@ uwvk_status uwvk_ipose_set_pose_reference(uwvk_ipose* h, const double* pose) {
 }
 
 uwvk_status uwvk_ipose_predict(uwvk_ipose* h, double dt) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !(dt > 0.0)) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   hipLaunchKernelGGL(k_ipose_predict, dim3(grid_of(h->batch, IE::IPB)), dim3(IE::BLOCK), 0, h->stream, h->bufs(),
@@ -527,6 +542,7 @@ uwvk_status uwvk_ipose_update_visual(uwvk_ipose* h, int32_t n_features, const do
                                      const double* feature_positions, const double* marker_pose,
                                      int marker_pose_per_instance, const double cov_marker_pose[36],
                                      const double camera[4], const double camera_in_body[7], const uint8_t* mask) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   VisArgs va{};
@@ -547,6 +563,7 @@ uwvk_status uwvk_ipose_update_visual(uwvk_ipose* h, int32_t n_features, const do
 
 // getCorrectedPose (IndirectPoseUKF.cpp:137-142): pose_ref * pose_error, t(3) q(4)
 uwvk_status uwvk_ipose_get_corrected_pose(uwvk_ipose* h, double* out) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !out) return UWVK_EINVAL;
   const int64_t B = h->batch;
   std::vector<double> x((size_t)B * 7), ref((size_t)B * 7);
@@ -571,8 +588,9 @@ uwvk_status uwvk_ipose_get_corrected_pose(uwvk_ipose* h, double* out) {
   return UWVK_OK;
 }
 
-uwvk_status uwvk_ipose_get_state(uwvk_ipose* h, double* x, double* P) { return small_get_state(h, x, P); }
+uwvk_status uwvk_ipose_get_state(uwvk_ipose* h, double* x, double* P) { UWVK_DEVICE_GUARD(h); return small_get_state(h, x, P); }
 uwvk_status uwvk_ipose_get_status(uwvk_ipose* h, uint32_t* status, int clear) {
+  UWVK_DEVICE_GUARD(h);
   return small_get_status(h, status, clear);
 }
 

@@ -739,6 +739,7 @@ static bool vfinite(const double* a, size_t n) {
 extern "C" {
 
 uwvk_status uwvk_vel_create(int64_t batch, int device, uwvk_vel** out) {
+  ::uwvk::DeviceGuard uwvk_device_guard_(device);
   if (!out || batch <= 0) return UWVK_EINVAL;
   *out = nullptr;
   if (!uwvk_device_available(device)) return UWVK_EDEVICE;
@@ -773,6 +774,7 @@ uwvk_status uwvk_vel_create(int64_t batch, int device, uwvk_vel** out) {
 }
 
 void uwvk_vel_destroy(uwvk_vel* h) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_gyro, (void*)h->d_eff, (void*)h->d_model,
@@ -785,6 +787,7 @@ void uwvk_vel_destroy(uwvk_vel* h) {
 }
 
 uwvk_status uwvk_vel_set_option(uwvk_vel* h, int option, int value) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   if (option != UWVK_VEL_OPT_LANE_GROUPS || value < -1 || value > 1) return UWVK_EINVAL;
   h->groups = value;
@@ -792,6 +795,7 @@ uwvk_status uwvk_vel_set_option(uwvk_vel* h, int option, int value) {
 }
 
 uwvk_status uwvk_vel_set_process_noise(uwvk_vel* h, const double Q[16]) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !Q) return UWVK_EINVAL;
   if (!vfinite(Q, 16)) return UWVK_ENAN;
   std::memcpy(h->P.Q0, Q, sizeof(h->P.Q0));
@@ -799,11 +803,13 @@ uwvk_status uwvk_vel_set_process_noise(uwvk_vel* h, const double Q[16]) {
 }
 
 uwvk_status uwvk_vel_synchronize(uwvk_vel* h) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   return hipStreamSynchronize(h->stream) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
 }
 
 uwvk_status uwvk_vel_timer_start(uwvk_vel* h) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   if (!h->ev0 && hipEventCreate(&h->ev0) != hipSuccess) return UWVK_EDEVICE;
   if (!h->ev1 && hipEventCreate(&h->ev1) != hipSuccess) return UWVK_EDEVICE;
@@ -812,6 +818,7 @@ uwvk_status uwvk_vel_timer_start(uwvk_vel* h) {
 }
 
 uwvk_status uwvk_vel_timer_stop(uwvk_vel* h, float* ms) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !ms || !h->ev0 || !h->ev1) return UWVK_EINVAL;
   HIPCHK(hipEventRecord(h->ev1, h->stream));
   HIPCHK(hipEventSynchronize(h->ev1));
@@ -822,6 +829,7 @@ uwvk_status uwvk_vel_timer_stop(uwvk_vel* h, float* ms) {
 void* uwvk_vel_stream(const uwvk_vel* h) { return h ? (void*)h->stream : nullptr; }
 
 uwvk_status uwvk_vel_init(uwvk_vel* h, const double* x, const double* P) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !x || !P) return UWVK_EINVAL;
   HIPCHK(hipMemcpyAsync(h->d_mu, x, (size_t)h->batch * 4 * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d_sigma, P, (size_t)h->batch * 16 * 8, hipMemcpyHostToDevice, h->stream));
@@ -831,6 +839,7 @@ uwvk_status uwvk_vel_init(uwvk_vel* h, const double* x, const double* P) {
 }
 
 uwvk_status uwvk_vel_setup_motion_model(uwvk_vel* h, const uwvk_uwv_params* u) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !u) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   std::memcpy(h->P.M, u->inertia_matrix, 36 * 8);
@@ -851,6 +860,7 @@ uwvk_status uwvk_vel_setup_motion_model(uwvk_vel* h, const uwvk_uwv_params* u) {
 }
 
 uwvk_status uwvk_vel_set_gyro(uwvk_vel* h, const double* w, const double* cov) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !w) return UWVK_EINVAL;
   if (!vfinite(w, (size_t)h->batch * 3) || (cov && !vfinite(cov, (size_t)h->batch * 9))) return UWVK_ENAN;
   HIPCHK(hipMemcpyAsync(h->d_gyro, w, (size_t)h->batch * 3 * 8, hipMemcpyHostToDevice, h->stream));
@@ -863,6 +873,7 @@ uwvk_status uwvk_vel_set_gyro(uwvk_vel* h, const double* w, const double* cov) {
 }
 
 uwvk_status uwvk_vel_set_efforts(uwvk_vel* h, const double* tau, const double* cov) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !tau) return UWVK_EINVAL;
   if (!vfinite(tau, (size_t)h->batch * 6) || (cov && !vfinite(cov, (size_t)h->batch * 36))) return UWVK_ENAN;
   HIPCHK(hipMemcpyAsync(h->d_eff, tau, (size_t)h->batch * 6 * 8, hipMemcpyHostToDevice, h->stream));
@@ -871,6 +882,7 @@ uwvk_status uwvk_vel_set_efforts(uwvk_vel* h, const double* tau, const double* c
 }
 
 uwvk_status uwvk_vel_predict(uwvk_vel* h, double dt) {
+  UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
   if (!h->has_model) return UWVK_ENOMODEL;  // VelocityUKF.cpp:117-118
   hipLaunchKernelGGL(k_vel_predict, dim3(vgrid(h->batch)), dim3(64), 0, h->stream, vbufs(h), h->P, dt);
@@ -916,14 +928,17 @@ static uwvk_status vel_update(uwvk_vel* h, int m, const double* mu, const double
 
 uwvk_status uwvk_vel_update_dvl(uwvk_vel* h, const double* mu, const double* cov, const double* sc,
                                 const uint8_t* mask) {
+  UWVK_DEVICE_GUARD(h);
   return vel_update(h, 3, mu, cov, sc, mask);
 }
 uwvk_status uwvk_vel_update_pressure(uwvk_vel* h, const double* mu, const double* cov, const double* sc,
                                      const uint8_t* mask) {
+  UWVK_DEVICE_GUARD(h);
   return vel_update(h, 1, mu, cov, sc, mask);
 }
 
 uwvk_status uwvk_vel_get_state(uwvk_vel* h, double* x, double* P) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !x) return UWVK_EINVAL;
   HIPCHK(hipMemcpyAsync(x, h->d_mu, (size_t)h->batch * 4 * 8, hipMemcpyDeviceToHost, h->stream));
   if (P) HIPCHK(hipMemcpyAsync(P, h->d_sigma, (size_t)h->batch * 16 * 8, hipMemcpyDeviceToHost, h->stream));
@@ -932,6 +947,7 @@ uwvk_status uwvk_vel_get_state(uwvk_vel* h, double* x, double* P) {
 }
 
 uwvk_status uwvk_vel_get_model_state(uwvk_vel* h, double* out) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !out) return UWVK_EINVAL;
   HIPCHK(hipMemcpyAsync(out, h->d_model, (size_t)h->batch * 13 * 8, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -939,6 +955,7 @@ uwvk_status uwvk_vel_get_model_state(uwvk_vel* h, double* out) {
 }
 
 uwvk_status uwvk_vel_run_log(uwvk_vel* h, const uwvk_vel_log* log, int64_t first, int64_t count) {
+  UWVK_DEVICE_GUARD(h);
   if (!h || !log || first < 0 || count < 0 || first + count > log->epochs) return UWVK_EINVAL;
   if (!h->has_model) return UWVK_ENOMODEL;
   VelEpochArgs ea{};

@@ -30,6 +30,13 @@ inline void check(uwvk_status s, const char* where) {
   if (s != UWVK_OK) throw Error(s, where);
 }
 
+// the library must implement the ABI this header describes (include/uwvk.h)
+inline void check_abi() {
+  if (uwvk_abi_version() != UWVK_ABI_VERSION)
+    throw std::runtime_error("libuwvk.so ABI version " + std::to_string(uwvk_abi_version()) +
+                             ", this facade needs " + std::to_string(UWVK_ABI_VERSION));
+}
+
 // One measurement for every instance of the batch (reference: MEASUREMENT(Name, M)
 // = {mu, cov}, PoseUKF.hpp:79-88).  cov holds batch*M*M values, or is empty to use
 // shared_cov for all instances.  mask (optional, batch bytes) skips instances.
@@ -234,11 +241,32 @@ class PoseUKF {
     check(uwvk_pose_get_rotation_rate(h_, w.data()), "getRotationRate");
     return w;
   }
-  // mu() / sigma() [EXT base]: batch*store and batch*dof*dof
+  // batch*store (x) and batch*dof*dof (P, full symmetric)
   void getState(std::vector<double>& x, std::vector<double>* P = nullptr) {
     x.resize((size_t)batch() * store());
     if (P) P->resize((size_t)batch() * dof() * dof());
     check(uwvk_pose_get_state(h_, x.data(), P ? P->data() : nullptr), "getState");
+  }
+  // The inherited getters of pose_estimation::UnscentedKalmanFilter<State> [EXT]
+  // (used at VelocityUKF.cpp:70: `if (getCurrentState(current_state))`) and the
+  // ukf's mu() / sigma() (PoseUKF.cpp:448,453,516): true once initialised.
+  bool getCurrentState(std::vector<double>& state) {
+    getState(state);
+    return true;
+  }
+  bool getCurrentState(std::vector<double>& state, std::vector<double>& covariance) {
+    getState(state, &covariance);
+    return true;
+  }
+  std::vector<double> mu() {
+    std::vector<double> x;
+    getState(x);
+    return x;
+  }
+  std::vector<double> sigma() {
+    std::vector<double> x, P;
+    getState(x, &P);
+    return P;
   }
   // Ensemble statistics (layout: uwvk_pose_ensemble_stats); with an RCCL
   // communicator (uwvk_comm_init, void* ncclComm_t) summed over all ranks.
@@ -264,6 +292,7 @@ class PoseUKF {
 
  private:
   static uwvk_pose* create(int64_t batch, int dof, int device) {
+    check_abi();
     uwvk_pose* h = nullptr;
     check(uwvk_pose_create(batch, dof, device, &h), "uwvk_pose_create");
     return h;
@@ -306,6 +335,7 @@ class VelocityUKF {
  public:
   VelocityUKF(int64_t batch, const std::vector<double>& state, const std::vector<double>& cov, int device = 0)
       : batch_(batch) {
+    check_abi();
     check(uwvk_vel_create(batch, device, &h_), "uwvk_vel_create");
     if (state.size() != (size_t)batch * 4 || cov.size() != (size_t)batch * 16) {
       uwvk_vel_destroy(h_);
@@ -345,10 +375,56 @@ class VelocityUKF {
     if (P) P->resize((size_t)batch_ * 16);
     check(uwvk_vel_get_state(h_, x.data(), P ? P->data() : nullptr), "getState");
   }
+  // inherited getters [EXT] (VelocityUKF.cpp:70)
+  bool getCurrentState(std::vector<double>& state) {
+    getState(state);
+    return true;
+  }
+  bool getCurrentState(std::vector<double>& state, std::vector<double>& covariance) {
+    getState(state, &covariance);
+    return true;
+  }
+  std::vector<double> mu() {
+    std::vector<double> x;
+    getState(x);
+    return x;
+  }
+  std::vector<double> sigma() {
+    std::vector<double> x, P;
+    getState(x, &P);
+    return P;
+  }
 
  private:
   int64_t batch_;
   uwvk_vel* h_ = nullptr;
 };
+
+#if __has_include(<Eigen/Core>)
+}  // namespace uwv_kalman_filters_amd
+#include <Eigen/Core>
+namespace uwv_kalman_filters_amd {
+// Eigen overloads for the single-instance (batch = 1) drop-in: the reference's
+// MEASUREMENT types carry Eigen .mu / .cov (PoseUKF.hpp:79-88).  Eigen is not
+// installed in the build image, so this block is compiled only where it is.
+template <class Meas, int M>
+Meas from_eigen(const Eigen::Matrix<double, M, 1>& mu, const Eigen::Matrix<double, M, M>& cov) {
+  Meas m;
+  m.mu.assign(mu.data(), mu.data() + M);
+  m.cov.resize((size_t)M * M);
+  for (int r = 0; r < M; r++)
+    for (int c = 0; c < M; c++) m.cov[(size_t)r * M + c] = cov(r, c);  // row-major in the C ABI
+  return m;
+}
+inline Eigen::VectorXd state_eigen(PoseUKF& f) {
+  const std::vector<double> x = f.mu();
+  return Eigen::Map<const Eigen::VectorXd>(x.data(), (Eigen::Index)x.size());
+}
+inline Eigen::MatrixXd covariance_eigen(PoseUKF& f) {
+  const std::vector<double> P = f.sigma();
+  const Eigen::Index n = f.dof();
+  return Eigen::Map<const Eigen::Matrix<double, Eigen::Dynamic, Eigen::Dynamic, Eigen::RowMajor>>(P.data(), n, n);
+}
+#endif
 
 }  // namespace uwv_kalman_filters_amd

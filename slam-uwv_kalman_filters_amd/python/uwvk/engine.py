@@ -44,9 +44,11 @@ SYMBOLS = [
     "uwvk_ipose_set_pose_reference", "uwvk_ipose_predict", "uwvk_ipose_update_visual",
     "uwvk_ipose_get_corrected_pose", "uwvk_ipose_get_state", "uwvk_ipose_get_status",
     "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots", "uwvk_pose_timer_mark", "uwvk_pose_timer_elapsed",
+    "uwvk_xcd_round_robin", "uwvk_synth_normal",
 ]
 
 _LIB = None
+ABI_VERSION = 2  # include/uwvk.h UWVK_ABI_VERSION this binding is written against
 DP = C.POINTER(C.c_double)
 VP = C.c_void_p
 
@@ -62,6 +64,9 @@ def lib(path=None):
     global _LIB
     if _LIB is None or path:
         L = C.CDLL(path or LIB_PATH)
+        if L.uwvk_abi_version() != ABI_VERSION:
+            raise OSError("%s: ABI version %d, this binding needs %d (include/uwvk.h)"
+                          % (path or LIB_PATH, L.uwvk_abi_version(), ABI_VERSION))
         L.uwvk_status_string.restype = C.c_char_p
         L.uwvk_pose_batch.restype = C.c_int64
         L.uwvk_pose_stream.restype = VP
@@ -164,6 +169,10 @@ class PoseUKFBatch:
         the runtime's occupancy, > 0 for that many resident blocks per XCD, < 0 off."""
         _chk(self.L.uwvk_pose_set_option(self.h, 3, int(slots)), "set_option")
 
+    def set_tail_chunks(self, chunks):
+        """UWVK_OPT_TAIL_CHUNKS: 0 the planner's chunk count, 2..8 forced (tests)."""
+        _chk(self.L.uwvk_pose_set_option(self.h, 4, int(chunks)), "set_option")
+
     def set_literal_apply_delta(self, on=True):
         """ukfom's literal apply_delta re-spread instead of the exact T Sigma T^T form."""
         _chk(self.L.uwvk_pose_set_option(self.h, 1, int(bool(on))), "set_option")
@@ -237,6 +246,12 @@ class PoseUKFBatch:
         P = np.empty((self.batch, self.dof, self.dof))
         _chk(self.L.uwvk_pose_get_state(self.h, _p(x), _p(P)), "get_state")
         return x, P
+
+    def get_state_mu(self):
+        """The means only (uwvk_pose_get_state with P = NULL)."""
+        x = np.empty((self.batch, self.lay["store"]))
+        _chk(self.L.uwvk_pose_get_state(self.h, _p(x), None), "get_state")
+        return x
 
     def get_rotation_rate(self):
         out = np.empty((self.batch, 3))

@@ -40,26 +40,28 @@ def ensemble_stats_host(x, P, truth):
     sq[3:6] += (r * r).sum(0)
     out[2 * store:3 * store] = sq
     err = np.concatenate([x[:, 0:3] - truth[0:3], r, x[:, 7:10] - truth[7:10]], 1)
-    # instances whose 9x9 block is not positive definite are counted, not summed
+    # the same exclusion rule as k_pose_stats: an instance is left out of the
+    # NEES sum when its 9x9 block has a non-positive pivot or its NEES is not
+    # finite (a NaN / Inf state); it is counted in out[3 * store + 1]
     sub = np.ascontiguousarray(P[:, :9, :9])
-    try:
-        ok = np.ones(x.shape[0], bool)
-        Lc = np.linalg.cholesky(sub)
-    except np.linalg.LinAlgError:
-        ok = np.array([np.all(np.linalg.eigvalsh(m) > 0) and _chol_ok(m) for m in sub])
-        Lc = np.linalg.cholesky(np.where(ok[:, None, None], sub, np.eye(9)))
-    y = np.linalg.solve(Lc, err[..., None])[..., 0]
-    out[3 * store] = float(np.sum(np.where(ok, np.sum(y * y, 1), 0.0)))
+    with np.errstate(invalid="ignore", over="ignore"):
+        try:  # every block positive definite: one batched factorisation
+            Lc = np.linalg.cholesky(sub)
+            y = np.linalg.solve(Lc, err[..., None])[..., 0]
+            nees = np.sum(y * y, 1)
+        except np.linalg.LinAlgError:  # some block is not: instance by instance
+            nees = np.full(x.shape[0], np.nan)
+            for i in range(x.shape[0]):
+                try:
+                    Li = np.linalg.cholesky(sub[i])
+                except np.linalg.LinAlgError:
+                    continue
+                yi = np.linalg.solve(Li, err[i])
+                nees[i] = float(yi @ yi)
+    ok = np.isfinite(nees)
+    out[3 * store] = float(np.sum(np.where(ok, nees, 0.0)))
     out[3 * store + 1] = float((~ok).sum())
     return out
-
-
-def _chol_ok(m):
-    try:
-        np.linalg.cholesky(m)
-        return True
-    except np.linalg.LinAlgError:
-        return False
 
 
 def allreduce_stats(stats, dist, device=None):

@@ -9,9 +9,11 @@ module is that driver for benches and parity tests.  It builds
   structs (`abi.PoseConfig`, PoseUKFConfig.hpp:159-194),
 * a truth trajectory (lawnmower-like: 1 m/s surge, 10 m depth,
   yaw rate 0.1*sin(0.05 t) rad/s),
-* per-instance noisy IMU / DVL / pressure / ADCP / body-effort logs, seeded with
-  numpy's counter-based Philox generator (instance i, stream id) so a sub-batch
-  reproduces exactly the rows of the full batch.
+* per-instance noisy IMU / DVL / pressure / ADCP / body-effort logs whose noise
+  is a pure function of (seed, global instance id, stream, index):
+  Philox4x32-10 + Box-Muller (uwvk_synth_normal in libuwvk.so, multithreaded;
+  `_normal_np` is its numpy restatement), so a sub-batch reproduces exactly
+  the rows of the full batch.
 
 Epoch e (0-based) is: RotationRate(gyro[e]) -> predictionStep(dt) ->
 Acceleration(acc[e]) -> (DVL | Pressure | ADCP cells | BodyEfforts when flagged),
@@ -158,6 +160,64 @@ class Truth:
 
 MODES = ("C1", "C3", "C4")
 
+_M0, _M1, _W0, _W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+
+
+def _normal_np(seed, inst, stream, count):
+    """numpy restatement of uwvk_synth_normal (csrc/uwvk_synth.cpp): [len(inst), count]."""
+    inst = np.asarray(inst, np.uint64)
+    nb = (count + 1) // 2
+    m32 = np.uint64(0xFFFFFFFF)
+    b = np.arange(nb, dtype=np.uint64)[None, :]
+    c0 = np.broadcast_to(b, (len(inst), nb)).copy()
+    c1 = np.broadcast_to((inst >> np.uint64(32))[:, None], c0.shape).copy()
+    c2 = np.full(c0.shape, stream, np.uint64)
+    c3 = np.full(c0.shape, 0x5EED, np.uint64)
+    k0 = np.full((len(inst), 1), (seed ^ (seed >> 32)) & 0xFFFFFFFF, np.uint64)
+    k1 = ((inst & m32) ^ np.uint64(stream << 24))[:, None]
+    for _ in range(10):
+        p0 = np.uint64(_M0) * c0
+        p1 = np.uint64(_M1) * c2
+        hi0, lo0, hi1, lo1 = p0 >> np.uint64(32), p0 & m32, p1 >> np.uint64(32), p1 & m32
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0 = (k0 + np.uint64(_W0)) & m32
+        k1 = (k1 + np.uint64(_W1)) & m32
+    a = ((c0 << np.uint64(32)) | c1) >> np.uint64(11)
+    c = ((c2 << np.uint64(32)) | c3) >> np.uint64(11)
+    u1 = (a + np.uint64(1)).astype(np.float64) * 2.0 ** -53
+    u2 = c.astype(np.float64) * 2.0 ** -53
+    rad = np.sqrt(-2.0 * np.log(u1))
+    th = 2.0 * np.pi * u2
+    out = np.empty((len(inst), 2 * nb))
+    out[:, 0::2] = rad * np.cos(th)
+    out[:, 1::2] = rad * np.sin(th)
+    return out[:, :count]
+
+
+def _normal_lib(seed, first, batch, stream, count):
+    """uwvk_synth_normal through the C ABI, or None without libuwvk.so."""
+    import ctypes as C
+    try:
+        from . import engine
+        L = engine.lib()
+    except OSError:
+        return None
+    out = np.empty((batch, count))
+    rc = L.uwvk_synth_normal(C.c_uint64(seed), C.c_int64(first), C.c_int64(batch), C.c_uint32(stream),
+                             C.c_int64(count), out.ctypes.data_as(C.c_void_p))
+    if rc != 0:
+        raise ValueError("uwvk_synth_normal: status %d" % rc)
+    return out
+
+
+def normals(seed, first, batch, stream, shape_tail):
+    """[batch, *shape_tail] standard normals of instances first .. first + batch."""
+    count = int(np.prod(shape_tail, dtype=np.int64))
+    out = _normal_lib(seed, first, batch, stream, count)
+    if out is None:
+        out = _normal_np(seed, np.arange(first, first + batch), stream, count)
+    return out.reshape((batch,) + tuple(shape_tail))
+
 
 def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_instance=0, cfg=None,
                   dropout_on=30.0, dropout_off=10.0, adcp_every=1000, efforts_velocity_only=False):
@@ -197,15 +257,9 @@ def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_in
     a_index, a_k = idx_of(abi.EV_ADCP)
     e_index, e_k = idx_of(abi.EV_EFFORTS)
 
-    inst = np.arange(first_instance, first_instance + batch)
-
     def normal(stream, shape_tail):
-        # counter-based: one Philox stream per (instance, measurement kind)
-        out = np.empty((batch,) + shape_tail)
-        for j, i in enumerate(inst):
-            g = np.random.Generator(np.random.Philox(key=[seed, int(i) * 16 + stream]))
-            out[j] = g.standard_normal(shape_tail)
-        return out
+        # counter-based: one stream per (instance, measurement kind)
+        return normals(seed, first_instance, batch, stream, shape_tail)
 
     sg = 1e-4 / np.sqrt(dt)
     sa = 1e-3 / np.sqrt(dt)
@@ -279,14 +333,8 @@ def make_vel_log(batch, epochs, seed=SEED, dt=1e-3, first_instance=0):
     p_index = np.full(epochs, -1, np.int32)
     psel = (flags & abi.EV_PRESSURE) != 0
     p_index[psel] = np.arange(psel.sum())
-    inst = np.arange(first_instance, first_instance + batch)
-
     def normal(stream, shape_tail):
-        out = np.empty((batch,) + shape_tail)
-        for j, i in enumerate(inst):
-            g = np.random.Generator(np.random.Philox(key=[seed + 1, int(i) * 16 + stream]))
-            out[j] = g.standard_normal(shape_tail)
-        return out
+        return normals(seed + 1, first_instance, batch, 16 + stream, shape_tail)
 
     M, Dl, Dq = uwv_arrays(uwv)
     wv3 = np.zeros(3)

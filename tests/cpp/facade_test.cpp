@@ -122,6 +122,9 @@ int main() {
   }
   std::vector<double> x, P;
   f.getState(x, &P);
+  // the inherited getters return the same state (VelocityUKF.cpp:70, PoseUKF.cpp:448)
+  std::vector<double> xs, Ps;
+  const bool getters_ok = f.getCurrentState(xs, Ps) && xs == x && Ps == P && f.mu() == x && f.sigma() == P;
   double worst = 0;
   std::vector<double> xo(54), Po(53 * 53);
   for (int64_t b = 0; b < B; b++) {
@@ -146,7 +149,7 @@ int main() {
   } catch (const U::Error& e) {
     threw = true;
   }
-  std::printf("facade parity: worst %.3e (std units), gate mismatches %d, nan throws %d\n", worst, mismatch_gate,
-              (int)threw);
-  return (worst < 1e-7 && mismatch_gate == 0 && threw) ? 0 : 1;
+  std::printf("facade parity: worst %.3e (std units), gate mismatches %d, nan throws %d, getters %d\n", worst,
+              mismatch_gate, (int)threw, (int)getters_ok);
+  return (worst < 1e-7 && mismatch_gate == 0 && threw && getters_ok) ? 0 : 1;
 }

@@ -60,3 +60,76 @@ def test_bench_line_fields_documented():
         assert key in src
     d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     assert "C3-dof53-b65536-e20" in d
+
+
+# ---- multi-GPU launch logic (no GPU: spawned scripts stand in for the ranks) ----
+
+class _Args:
+    def __init__(self, gpus, mode="auto", batch_per_gpu=0):
+        self.gpus, self.mode, self.batch_per_gpu = gpus, mode, batch_per_gpu
+
+
+def test_workload_defaults_c3_single_c5_multi():
+    assert bench.workload_of(_Args(1), 1) == ("C3", 65536)
+    mode, b = bench.workload_of(_Args(8), 8)
+    assert (mode, b * 8) == ("C5", 1_048_576)  # BASELINE.json config 5
+    assert bench.workload_of(_Args(2), 2) == ("C5", 131072)
+    assert bench.workload_of(_Args(2, batch_per_gpu=1000), 2) == ("C5", 1000)
+    assert bench.workload_of(_Args(1, mode="C2"), 1) == ("C2", 4096)
+
+
+def test_resolve_world_checks_the_launcher():
+    assert bench.resolve_world(_Args(1), env={}) == (1, 0, 0)
+    env = {"WORLD_SIZE": "4", "RANK": "2", "LOCAL_RANK": "2"}
+    assert bench.resolve_world(_Args(4), env=env) == (4, 2, 2)
+    with pytest.raises(SystemExit):
+        bench.resolve_world(_Args(8), env=env)
+    with pytest.raises(SystemExit):
+        bench.resolve_world(_Args(1), env=env)
+
+
+def test_rank_env():
+    e = bench.rank_env({"X": "1"}, 3, 8, 12345)
+    assert (e["RANK"], e["LOCAL_RANK"], e["WORLD_SIZE"], e["MASTER_ADDR"], e["MASTER_PORT"]) == \
+        ("3", "3", "8", "127.0.0.1", "12345")
+    assert e["X"] == "1" and e["UWVK_BENCH_SPAWNED"] == "1"
+
+
+def test_spawn_ranks_runs_every_rank(tmp_path):
+    script = tmp_path / "rank.py"
+    out = tmp_path / "out"
+    out.mkdir()
+    script.write_text("import os, sys\n"
+                      "open(os.path.join(sys.argv[1], os.environ['RANK']), 'w').write(os.environ['WORLD_SIZE'])\n")
+    assert bench.spawn_ranks([str(out)], 3, timeout=60, script=str(script)) == 0
+    assert sorted(os.listdir(out)) == ["0", "1", "2"]
+    assert all((out / r).read_text() == "3" for r in "012")
+
+
+def test_spawn_ranks_stops_the_others_when_one_fails(tmp_path):
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\n"
+                      "if os.environ['RANK'] == '1':\n    sys.exit(7)\n"
+                      "time.sleep(120)\n")
+    import time
+    t0 = time.time()
+    assert bench.spawn_ranks([], 3, timeout=60, script=str(script)) == 7
+    assert time.time() - t0 < 30
+
+
+def test_gloo_control_plane_two_ranks(tmp_path):
+    """The self-launched ranks form the gloo process group bench.py uses
+    (barrier, broadcast of the RCCL id, max of the times) on 127.0.0.1."""
+    script = tmp_path / "rank.py"
+    script.write_text(
+        "import os, sys\n"
+        "sys.path.insert(0, %r)\n"
+        "import bench, torch\n"
+        "dist = bench.init_dist(int(os.environ['WORLD_SIZE']))\n"
+        "uid = [b'id' if dist.get_rank() == 0 else None]\n"
+        "dist.broadcast_object_list(uid, src=0)\n"
+        "w = torch.tensor([float(dist.get_rank())], dtype=torch.float64)\n"
+        "dist.all_reduce(w, op=dist.ReduceOp.MAX)\n"
+        "dist.barrier()\n"
+        "sys.exit(0 if (uid[0] == b'id' and float(w[0]) == 1.0) else 5)\n" % ROOT)
+    assert bench.spawn_ranks([], 2, timeout=120, script=str(script)) == 0

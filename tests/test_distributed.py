@@ -253,3 +253,35 @@ def test_ensemble_stats_excludes_non_pd_instances():
     assert np.all(np.isfinite(got))
     assert got[-1] == 2 and host[-1] == 2
     np.testing.assert_allclose(got, host, rtol=1e-9, atol=1e-12)
+    # a NaN state (velocity) is left out of the NEES sum by both (advisor r02);
+    # the plain sums of that component are NaN on both sides
+    x[20, 8] = np.nan
+    f.init_from_state(x, P, abi.Location(synth.LAT0, synth.LON0, 0.0), uwv, abi.PoseParameter())
+    got = f.ensemble_stats(truth)
+    host = ensemble.ensemble_stats_host(x, P, truth)
+    assert got[-1] == 3 and host[-1] == 3 and np.isfinite(got[-2])
+    np.testing.assert_allclose(got, host, rtol=1e-9, atol=1e-12, equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_self_launches_two_ranks():
+    """`bench.py --gpus 2` with no launcher starts its two rank processes itself
+    (one-GPU rehearsal: UWVK_BENCH_SAME_DEVICE puts both on device 0, where
+    RCCL refuses a second rank, so the statistics sum goes over gloo) and
+    reports the whole job: n_gpus 2, the global batch of both shards."""
+    import json
+    import subprocess
+    env = dict(os.environ, UWVK_BENCH_SAME_DEVICE="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup",
+                        "2", "--batch-per-gpu", "16384", "--no-cpu-baseline"], capture_output=True, text=True,
+                       timeout=500, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * 16384
+    assert d["config"]["workload"].startswith("C5") and d["collective_check"] is True
+    assert d["value"] > 0 and d["config"]["stats_allreduces_in_window"] == 1

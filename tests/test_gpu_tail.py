@@ -76,3 +76,46 @@ def test_tail_default_plan_repeat(eng):
     got = _run(eng, B, 53, log, cfg, uwv, 0, [(0, 30), (30, 30)])
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a, b)
+
+
+def test_xcd_round_robin_on_this_device(eng):
+    """The probe that gates tail spreading: the box's single-partition MI355X
+    places block b on the XCC of block b % 8 (hardware XCC_ID)."""
+    assert eng.lib().uwvk_xcd_round_robin(0) == 1
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("B", [65536, 131072])
+def test_every_chunk_count_at_full_batch(eng, B):
+    """C3 / C5-shard batches with the runtime's resident slots: each chunk
+    count 2..8 (forced, UWVK_OPT_TAIL_CHUNKS; the planner's choice is a host
+    unit test) run on a 20-epoch piece, then one unspread epoch, so that the
+    piece's final Sigma reaches the mean.  The means are bitwise those of a
+    handle that never spreads, with no status bits and equal accept counts."""
+    from uwvk import synth
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    piece = 20
+    E = 7 * (piece + 1)
+    log = synth.make_pose_log(B, E, "C3")
+    hs = []
+    for spread in (False, True):
+        g = eng.PoseUKFBatch(B, 53)
+        g.set_tail_slots(0 if spread else -1)
+        g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+        g.set_process_noise_from_config(cfg, 1e-3)
+        hs.append((g, g.upload_log(log), eng.DeviceBuffer(np.zeros((B, 4), np.uint32))))
+    e = 0
+    for c in range(2, 9):
+        for (g, d, acc), spread in zip(hs, (False, True)):
+            g.set_tail_chunks(c if spread else 0)
+            g.run_log(d, e, piece, accept_counts=acc)
+            g.set_tail_chunks(0)
+            g.set_tail_slots(-1)
+            g.run_log(d, e + piece, 1, accept_counts=acc)
+            g.set_tail_slots(0 if spread else -1)
+        e += piece + 1
+        (x0, _), (x1, _) = [(g.get_state_mu(), None) for g, _, _ in hs]
+        np.testing.assert_array_equal(x1, x0, err_msg="chunks=%d" % c)
+    for g, _, _ in hs:
+        assert not g.get_status().any()
+    np.testing.assert_array_equal(hs[1][2].read(np.uint32, (B, 4)), hs[0][2].read(np.uint32, (B, 4)))
