@@ -299,7 +299,17 @@ def init_dist(world):
     if world == 1 and not launched_by_torchrun():
         return None
     import torch.distributed as dist
-    dist.init_process_group("gloo")
+    # gloo prints its connection report on stdout, where the driver reads the
+    # one JSON line: send file descriptor 1 to stderr while the group forms
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo")
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
     return dist
 
 
