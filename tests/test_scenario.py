@@ -1,0 +1,50 @@
+"""The synthetic Monte-Carlo scenario (bench.py --init): on the CPU oracle the
+ensemble NEES of (position, orientation, velocity) reads near its chi-square
+mean of 9 from the Monte-Carlo start, and far above it from the first
+constructor's prior (v = 0 against a 1 m/s truth, yaw sd 0.05 rad, yaw
+unobservable: ukfom's axis-aligned sigma points miss the yaw-velocity coupling
+of the first DVL update).  Oracle only: the UKF itself, not the engine."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+from uwvk import ensemble, synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+B, E = 48, 300  # one DVL update at epoch 199
+
+
+def _nees(init):
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(B, E, "C3", first_instance=500)
+    o = O.OraclePoseBatch(B, 53)
+    bench.initialise(o, log, cfg, uwv, init, first_instance=500)
+    o.set_process_noise_from_config(cfg, log["dt"])
+    o.run_log(log, 0, E, nthreads=min(8, os.cpu_count() or 1))
+    x, P = o.get_state()
+    st = ensemble.ensemble_stats_host(x, P, log["truth"].state(E))
+    assert st[-1] == 0
+    return st[-2] / B
+
+
+def test_monte_carlo_start_is_consistent():
+    # 48 instances: the mean of chi-square(9) has sd sqrt(18 / 48) = 0.61
+    assert 9 - 2.5 < _nees("mc") < 9 + 2.5
+
+
+def test_first_constructor_prior_is_not():
+    assert _nees("config") > 20
+
+
+def test_mc_start_shards_bitwise():
+    full = synth.make_pose_log(10, 2, "C3")
+    part = synth.make_pose_log(4, 2, "C3", first_instance=6)
+    q_full, _ = synth.mc_rotation(full)
+    q_part, _ = synth.mc_rotation(part, first_instance=6)
+    np.testing.assert_array_equal(q_part, q_full[6:])
