@@ -241,3 +241,44 @@ def test_run_log_device_flags_only(eng, orc):
     dlog.s.host_flags = None
     g.run_log(dlog)
     _check(o, g, 53, TOL_LOG)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("groups,B", [(1, 4096), (0, 8192)])
+def test_velocity_ukf_config_batch(eng, orc, groups, B):
+    """Config C2 at its size (VelocityUKF.cpp:6-130): 4,096 instances over
+    2,000 epochs through the 16-lane-row kernel (k_vel_epoch_g), and the
+    lane-per-filter kernel (k_vel_epoch) at a larger batch.  16 instances
+    spread over the batch are checked against the oracle, each generated ALONE
+    (its own one-instance log: counter-based noise, so the same numbers), and
+    a second run of the whole batch is bitwise equal."""
+    from uwvk import synth
+    E = 2000
+    uwv = synth.default_uwv()
+    log = synth.make_vel_log(B, E)
+    runs = []
+    for _ in range(2):
+        g = eng.VelocityUKFBatch(B)
+        g.set_lane_groups(groups)
+        g.init(log["x0"], log["P0"])
+        g.set_gyro(log["gyro"][0])
+        g.setup_motion_model(uwv)
+        g.run_log(g.upload_log(log))
+        runs.append(g.get_state(model=True))
+    for a, b in zip(*runs):
+        np.testing.assert_array_equal(a, b)
+    xg, Pg, mg = runs[0]
+    picks = np.unique(np.linspace(0, B - 1, 16).astype(int))
+    for i in picks:
+        li = synth.make_vel_log(1, E, first_instance=int(i))
+        np.testing.assert_array_equal(li["gyro"][:, 0], log["gyro"][:, i])
+        o = orc.OracleVelBatch(1)
+        o.init(li["x0"], li["P0"])
+        o.set_gyro(li["gyro"][0])
+        o.setup_motion_model(uwv)
+        o.run_log(li)
+        xo, Po, mo = o.get_state(model=True)
+        sd = np.sqrt(np.diagonal(Po, axis1=1, axis2=2))
+        assert np.max(np.abs(xg[i] - xo[0]) / sd[0]) < TOL_LOG, i
+        assert cov_err(Pg[i:i + 1], Po).max() < TOL_LOG, i
+        assert np.max(np.abs(mg[i] - mo[0])) < 1e-9, i
