@@ -409,6 +409,15 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   (chunks x slots <= batch / 8, chunks <= epochs), for tests.  Spreading of
  *   any kind runs only where uwvk_xcd_round_robin(device) is 1. */
 #define UWVK_OPT_TAIL_CHUNKS 4
+/* UWVK_OPT_SO3_RIGHT: the side of the SO3 [+] / [-] [EXT MTK], SURVEY 8(c)
+ *   item 5, the largest unpinned semantic.  0 (default): nav frame (left),
+ *   q [+] d = exp(d) q, the convention the reference's usage implies
+ *   (PoseUKF.cpp:31-32, :451).  1: body frame (right, classic MTK
+ *   SO3::boxplus), q [+] d = q exp(d), in every orientation [+] / [-]: sigma
+ *   points, processModel's orientation step (PoseUKF.cpp:32), manifold mean,
+ *   apply_delta.  1 selects the literal kernels (the PSP kernels are
+ *   left-only).  The oracle's or_set_so3_right is the same switch. */
+#define UWVK_OPT_SO3_RIGHT 5
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
 /* Host-only query (no device work): the chunks per tail instance the
  * UWVK_OPT_TAIL_SLOTS planner picks for one XCD's instances over its resident

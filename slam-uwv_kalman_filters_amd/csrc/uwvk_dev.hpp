@@ -133,6 +133,40 @@ UWVK_DEV void qboxminus(const double a[4], const double b[4], double o[3]) {
   so3_log(r, o);
 }
 
+// SO3 [+] / [-] of either side [EXT MTK] (SURVEY 8(c) item
+// 5): right = 0 is the nav-frame (left) convention, q [+] d = exp(d) q and
+// a [-] b = log(a b^-1), the default everywhere; right = 1 the body-frame
+// (classic MTK SO3::boxplus) one, q [+] d = q exp(d) and a [-] b = log(b^-1 a).
+// The literal kernels take the side from the handle (UWVK_OPT_SO3_RIGHT); the
+// PSP kernels are left-only.  e = exp(d) is passed in; the branch is uniform.
+// One product with the operand order selected (no duplicated code paths: the
+// literal kernels are at the VGPR limit): q1 q2 = (w1 w2 - v1.v2, w1 v2 + w2 v1
+// + v1 x v2), so swapping the operands only flips the sign of the cross term.
+UWVK_DEV void qmul_side(const double a[4], const double b[4], double o[4], int swap) {
+  const double sg = swap ? -1.0 : 1.0;
+  const double cx = a[2] * b[3] - a[3] * b[2], cy = a[3] * b[1] - a[1] * b[3], cz = a[1] * b[2] - a[2] * b[1];
+  o[0] = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  o[1] = a[0] * b[1] + a[1] * b[0] + sg * cx;
+  o[2] = a[0] * b[2] + a[2] * b[0] + sg * cy;
+  o[3] = a[0] * b[3] + a[3] * b[0] + sg * cz;
+}
+UWVK_DEV void qplus_side(const double e[4], const double q[4], double o[4], int right) {
+  if (!right) {  // the default keeps qmul's exact expressions (bitwise the r02 results)
+    qmul(e, q, o);
+    return;
+  }
+  qmul_side(e, q, o, 1);  // q e
+}
+UWVK_DEV void qboxminus_side(const double a[4], const double b[4], double o[3], int right) {
+  double bc[4] = {b[0], -b[1], -b[2], -b[3]}, r[4];
+  if (!right) {
+    qmul(a, bc, r);
+  } else {
+    qmul_side(a, bc, r, 1);  // b^-1 a
+  }
+  so3_log(r, o);
+}
+
 // ---------------------------------------------------------------------------
 // wave-level primitives
 // ---------------------------------------------------------------------------

@@ -66,7 +66,8 @@ struct uwvk_pose {
 };
 
 // literal (all 2n+1 sigma points) kernels requested?
-static bool use_dense(const uwvk_pose* h) { return h->dense || h->sh.literal_apply_delta; }
+// (and the body-frame SO3 side, which only the literal kernels implement)
+static bool use_dense(const uwvk_pose* h) { return h->dense || h->sh.literal_apply_delta || h->sh.so3_right; }
 
 static PoseBufs bufs(const uwvk_pose* h) {
   PoseBufs b;
@@ -718,6 +719,10 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
   }
   if (option == UWVK_OPT_TAIL_SLOTS) {
     h->tail_slots = value;
+    return UWVK_OK;
+  }
+  if (option == UWVK_OPT_SO3_RIGHT) {
+    h->sh.so3_right = value ? 1 : 0;
     return UWVK_OK;
   }
   if (option == UWVK_OPT_TAIL_CHUNKS) {

@@ -42,6 +42,7 @@ struct PoseShared {
   int qlo[56], qoff[56], q_band;
   int q_bw;  // max band width below the diagonal over rows >= 9 (PSP keeps <= 2 in registers)
   int q_simple;  // PSP: lane-resident dt^2 Q suffices (see psp::LaneQ)
+  int so3_right;  // UWVK_OPT_SO3_RIGHT: body-frame SO3 [+]/[-] (literal kernels only; qplus_side)
 };
 
 struct PoseBufs {
@@ -355,7 +356,7 @@ UWVK_DEV bool chol_lds(Smem<DOF>& sm) {
 // sigma point p (0..N-1) of (mu, L) into x (store layout):
 // X0 = mu, X_{2j+1} = mu [+] L_j, X_{2j+2} = mu [+] -L_j
 template <int DOF>
-UWVK_DEV void gen_point(const Smem<DOF>& sm, int p, double x[Lay<DOF>::store]) {
+UWVK_DEV void gen_point(const Smem<DOF>& sm, int p, double x[Lay<DOF>::store], int right) {
   using L = Lay<DOF>;
 #pragma unroll
   for (int s = 0; s < L::store; s++) x[s] = sm.mu[s];
@@ -373,25 +374,25 @@ UWVK_DEV void gen_point(const Smem<DOF>& sm, int p, double x[Lay<DOF>::store]) {
 #pragma unroll
     for (int i = 0; i < 3; i++) v[i] = sg * ((3 + i >= j) ? sm.Lp[(3 + i) * (4 + i) / 2 + j] : 0.0);
     so3_exp(v, e);
-    qmul(e, sm.mu + L::s_quat, x + L::s_quat);
+    qplus_side(e, sm.mu + L::s_quat, x + L::s_quat, right);
   }
 }
 
 // x [-] m (store -> tangent), m read from LDS
 template <int DOF>
-UWVK_DEV void boxminus_lds(const double x[Lay<DOF>::store], const double* m, double d[DOF]) {
+UWVK_DEV void boxminus_lds(const double x[Lay<DOF>::store], const double* m, double d[DOF], int right) {
 #pragma unroll
   for (int k = 0; k < DOF; k++) {
     if (k >= 3 && k < 6) continue;
     d[k] = x[d2s(k)] - m[d2s(k)];
   }
   const double q[4] = {m[3], m[4], m[5], m[6]};
-  qboxminus(x + 3, q, d + 3);
+  qboxminus_side(x + 3, q, d + 3, right);
 }
 
 // x [+] delta (delta uniform, from LDS)
 template <int DOF>
-UWVK_DEV void boxplus_vec(double x[Lay<DOF>::store], const double* delta) {
+UWVK_DEV void boxplus_vec(double x[Lay<DOF>::store], const double* delta, int right) {
 #pragma unroll
   for (int k = 0; k < DOF; k++) {
     if (k >= 3 && k < 6) continue;
@@ -400,7 +401,7 @@ UWVK_DEV void boxplus_vec(double x[Lay<DOF>::store], const double* delta) {
   double e[4], q[4];
   const double dv[3] = {delta[3], delta[4], delta[5]};
   so3_exp(dv, e);
-  qmul(e, x + 3, q);
+  qplus_side(e, x + 3, q, right);
 #pragma unroll
   for (int i = 0; i < 4; i++) x[3 + i] = q[i];
 }
@@ -557,7 +558,7 @@ UWVK_DEV void process_point(double x[Lay<DOF>::store], const PoseShared& sh, con
   for (int i = 0; i < 3; i++) wn[i] = (wn[i] - er[i]) * dt;
   double e[4], q[4];
   so3_exp(wn, e);
-  qmul(e, x + L::s_quat, q);
+  qplus_side(e, x + L::s_quat, q, sh.so3_right);
 #pragma unroll
   for (int i = 0; i < 4; i++) x[L::s_quat + i] = q[i];
   // vector parts: every update reads only pre-step values of other blocks
@@ -627,7 +628,7 @@ UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& p
   const bool ok = chol_lds<DOF>(sm);
   UWVK_STAMP(0);
   double x[L::store];
-  gen_point<DOF>(sm, t, x);
+  gen_point<DOF>(sm, t, x, sh.so3_right);
   process_point<DOF>(x, sh, pc);
   // X0 (thread 0's point) as the first reference of the manifold mean
   if (t == 0) {
@@ -641,7 +642,7 @@ UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& p
   double dori[3];
   {
     double d[DOF];
-    boxminus_lds<DOF>(x, sm.ref, d);
+    boxminus_lds<DOF>(x, sm.ref, d, sh.so3_right);
     if (!mine) {
 #pragma unroll
       for (int k = 0; k < DOF; k++) d[k] = 0.0;
@@ -663,13 +664,13 @@ UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& p
     double e[4];
     const double q0[4] = {sm.ref[3], sm.ref[4], sm.ref[5], sm.ref[6]};
     so3_exp(dori, e);
-    qmul(e, q0, mq);
+    qplus_side(e, q0, mq, sh.so3_right);
   }
   int it = 0;
   while (sqrt(nrm2) > 1e-6 && ++it < 10000) {
     // orientation-only refinement: the vect parts are already the exact mean
     double la[3];
-    qboxminus(x + L::s_quat, mq, la);
+    qboxminus_side(x + L::s_quat, mq, la, sh.so3_right);
     if (!mine) la[0] = la[1] = la[2] = 0.0;
     block_sum<DOF, 3>(sm, la);
     nrm2 = 0.0;
@@ -680,7 +681,7 @@ UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& p
     }
     double e[4], q[4];
     so3_exp(la, e);
-    qmul(e, mq, q);
+    qplus_side(e, mq, q, sh.so3_right);
 #pragma unroll
     for (int i = 0; i < 4; i++) mq[i] = q[i];
   }
@@ -692,7 +693,7 @@ UWVK_DEV bool pose_predict(Smem<DOF>& sm, const PoseShared& sh, const ProcCtx& p
   d4_t acc[G::TPW];
   {
     double d[DOF];
-    boxminus_lds<DOF>(x, sm.ref, d);
+    boxminus_lds<DOF>(x, sm.ref, d, sh.so3_right);
     cov_gemm<DOF>(sm, d, acc);
   }
   auto qf = [&](int r, int c) -> double {
@@ -782,19 +783,19 @@ UWVK_DEV void small_inv(const double* A, double* X) {
 // delta (tangent) is in sm.vec.
 // ---------------------------------------------------------------------------
 template <int DOF>
-UWVK_DEV bool apply_delta_literal(Smem<DOF>& sm, Stamper* st = nullptr) {
+UWVK_DEV bool apply_delta_literal(Smem<DOF>& sm, int right, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   const int t = tid();
   const bool ok = chol_lds<DOF>(sm);
   UWVK_STAMP(8);
   double x[L::store];
-  gen_point<DOF>(sm, t, x);
-  boxplus_vec<DOF>(x, sm.vec);
+  gen_point<DOF>(sm, t, x, right);
+  boxplus_vec<DOF>(x, sm.vec, right);
   if (t == 0) {
     double m[L::store];
 #pragma unroll
     for (int s = 0; s < L::store; s++) m[s] = sm.mu[s];
-    boxplus_vec<DOF>(m, sm.vec);
+    boxplus_vec<DOF>(m, sm.vec, right);
 #pragma unroll
     for (int s = 0; s < L::store; s++) sm.ref[s] = m[s];
   }
@@ -803,7 +804,7 @@ UWVK_DEV bool apply_delta_literal(Smem<DOF>& sm, Stamper* st = nullptr) {
   d4_t acc[Geo<DOF>::TPW];
   {
     double d[DOF];
-    boxminus_lds<DOF>(x, sm.ref, d);
+    boxminus_lds<DOF>(x, sm.ref, d, right);
     cov_gemm<DOF>(sm, d, acc);
   }
   store_cov<DOF>(sm, acc, [](int, int) { return 0.0; });
@@ -820,9 +821,11 @@ UWVK_DEV bool apply_delta_literal(Smem<DOF>& sm, Stamper* st = nullptr) {
 // T (L L^T) T^T = T Sigma T^T.  So: mu <- mu [+] d, Sigma <- T Sigma T^T
 // (O(n) work instead of a Cholesky + sigma spread + GEMM).  Differences to the
 // literal form are rounding only; apply_delta_literal keeps the literal path.
+// With the right (body-frame) boxplus, X_p = mu exp(l): (X_p [+] d) [-] (mu [+] d)
+// = log(exp(-d) exp(l) exp(d)) = R(exp(d))^T l, so T carries R^T instead.
 // ---------------------------------------------------------------------------
 template <int DOF>
-UWVK_DEV bool apply_delta_rot(Smem<DOF>& sm, Stamper* st = nullptr) {
+UWVK_DEV bool apply_delta_rot(Smem<DOF>& sm, int right, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   const int t = tid();
   double R[9];
@@ -830,6 +833,7 @@ UWVK_DEV bool apply_delta_rot(Smem<DOF>& sm, Stamper* st = nullptr) {
     const double dv[3] = {sm.vec[3], sm.vec[4], sm.vec[5]};
     double e[4];
     so3_exp(dv, e);
+    if (right) e[1] = -e[1], e[2] = -e[2], e[3] = -e[3];  // R(exp(d))^T = R(exp(d)^-1)
     qmatrix(e, R);
   }
   // Sigma T^T: columns 3..5 of every row
@@ -849,7 +853,7 @@ UWVK_DEV bool apply_delta_rot(Smem<DOF>& sm, Stamper* st = nullptr) {
     double m[L::store];
 #pragma unroll
     for (int s = 0; s < L::store; s++) m[s] = sm.mu[s];
-    boxplus_vec<DOF>(m, sm.vec);
+    boxplus_vec<DOF>(m, sm.vec, right);
 #pragma unroll
     for (int s = 0; s < L::store; s++) sm.mu[s] = m[s];
   }
@@ -859,9 +863,9 @@ UWVK_DEV bool apply_delta_rot(Smem<DOF>& sm, Stamper* st = nullptr) {
 }
 
 template <int DOF>
-UWVK_DEV bool apply_delta(Smem<DOF>& sm, bool literal, Stamper* st = nullptr) {
-  if (literal) return apply_delta_literal<DOF>(sm, st);
-  return apply_delta_rot<DOF>(sm, st);
+UWVK_DEV bool apply_delta(Smem<DOF>& sm, bool literal, int right, Stamper* st = nullptr) {
+  if (literal) return apply_delta_literal<DOF>(sm, right, st);
+  return apply_delta_rot<DOF>(sm, right, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -879,7 +883,7 @@ struct HJmax {
 
 template <int DOF, int M, class H>
 UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)[M * M], int zmode, int gate, H h,
-                          bool* ok, Stamper* st = nullptr, bool literal = false) {
+                          bool* ok, Stamper* st, bool literal, int right) {
   using L = Lay<DOF>;
   using G = Geo<DOF>;
   const int t = tid();
@@ -887,7 +891,7 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
   const bool cok = chol_lds<DOF>(sm);
   UWVK_STAMP(4);
   double x[L::store];
-  gen_point<DOF>(sm, t, x);
+  gen_point<DOF>(sm, t, x, right);
   __syncthreads();  // L dead from here on
   double zp[M], zm[M];
   h(x, zp);
@@ -1053,7 +1057,7 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
   }
   __syncthreads();
   UWVK_STAMP(7);
-  const bool aok = apply_delta<DOF>(sm, literal, st);
+  const bool aok = apply_delta<DOF>(sm, literal, right, st);
   *ok = cok && aok;
   return true;
 }

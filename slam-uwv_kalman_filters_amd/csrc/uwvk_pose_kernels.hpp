@@ -133,23 +133,23 @@ UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, 
     double z[3], R[9];
     for (int k = 0; k < 3; k++) z[k] = zin[k];
     for (int k = 0; k < 9; k++) R[k] = Rin[k];
-    return pose_update<DOF, 3>(sm, z, R, 1, 0, HAcc<DOF>{}, ok, st, sh.literal_apply_delta != 0);
+    return pose_update<DOF, 3>(sm, z, R, 1, 0, HAcc<DOF>{}, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
   } else if constexpr (K == MK_VEL) {
     double z[3], R[9];
     for (int k = 0; k < 3; k++) z[k] = zin[k];
     for (int k = 0; k < 9; k++) R[k] = Rin[k];
-    return pose_update<DOF, 3>(sm, z, R, 1, 0, HVel<DOF>{}, ok, st, sh.literal_apply_delta != 0);
+    return pose_update<DOF, 3>(sm, z, R, 1, 0, HVel<DOF>{}, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
   } else if constexpr (K == MK_PRESSURE) {
     double z[1] = {zin[0]}, R[1] = {Rin[0]};
     HPressure<DOF> h;
     h.s[0] = ma.v3[0]; h.s[1] = ma.v3[1]; h.s[2] = ma.v3[2];
     h.patm = sh.p.atmospheric_pressure;
-    return pose_update<DOF, 1>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0);
+    return pose_update<DOF, 1>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
   } else if constexpr (K == MK_WATER) {
     double z[2] = {zin[0], zin[1]}, R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
     HWater<DOF> h;
     h.cw = ma.extra ? ma.extra[i] : 0.0;
-    return pose_update<DOF, 2>(sm, z, R, 1, 1, h, ok, st, sh.literal_apply_delta != 0);
+    return pose_update<DOF, 2>(sm, z, R, 1, 1, h, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
   } else if constexpr (K == MK_XY || K == MK_GEO || K == MK_DELAYED) {
     double z[2] = {zin[0], zin[1]}, R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
     int gate = 0;
@@ -166,10 +166,10 @@ UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, 
       z[0] = zin[0] + (sm.mu[L::s_pos] - ma.extra[2 * i]);
       z[1] = zin[1] + (sm.mu[L::s_pos + 1] - ma.extra[2 * i + 1]);
     }
-    return pose_update<DOF, 2>(sm, z, R, 0, gate, HXY<DOF>{}, ok, st, sh.literal_apply_delta != 0);
+    return pose_update<DOF, 2>(sm, z, R, 0, gate, HXY<DOF>{}, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
   } else if constexpr (K == MK_Z) {
     double z[1] = {zin[0]}, R[1] = {Rin[0]};
-    return pose_update<DOF, 1>(sm, z, R, 0, 0, HZ<DOF>{}, ok, st, sh.literal_apply_delta != 0);
+    return pose_update<DOF, 1>(sm, z, R, 0, 0, HZ<DOF>{}, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
   } else {  // MK_EFFORTS, PoseUKF.cpp:581-602
     double z[6], R[36];
     for (int k = 0; k < 6; k++) z[k] = zin[k];
@@ -195,7 +195,7 @@ UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, 
       cross3(wb, h.imu, cr);
       cross3(wb, cr, cc);
       for (int k = 0; k < 3; k++) h.ab[k] = ra[k] - cc[k];
-      return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0);
+      return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
     }
     HEfforts<DOF> h;
     h.ef = ef;
@@ -210,7 +210,7 @@ UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, 
         model[18 + l] = sm.mu[L::s_quad + l];
       }
     }
-    return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0);
+    return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
   }
 }
 
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_epoch(PoseBufs b, PoseShar
         double zz[2] = {z[0], z[1]}, R[4] = {ea.adcp_cov[0], ea.adcp_cov[1], ea.adcp_cov[2], ea.adcp_cov[3]};
         HWater<DOF> h;
         h.cw = ea.cw[c];
-        cnt[2] += pose_update<DOF, 2>(sm, zz, R, 1, 1, h, &sok, st, sh.literal_apply_delta != 0);
+        cnt[2] += pose_update<DOF, 2>(sm, zz, R, 1, 1, h, &sok, st, sh.literal_apply_delta != 0, sh.so3_right);
         ok = ok && sok;
       }
     }

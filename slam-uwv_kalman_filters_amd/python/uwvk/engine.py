@@ -169,6 +169,10 @@ class PoseUKFBatch:
         the runtime's occupancy, > 0 for that many resident blocks per XCD, < 0 off."""
         _chk(self.L.uwvk_pose_set_option(self.h, 3, int(slots)), "set_option")
 
+    def set_so3_right(self, on=True):
+        """UWVK_OPT_SO3_RIGHT: body-frame SO3 boxplus (literal kernels), like the oracle's or_set_so3_right."""
+        _chk(self.L.uwvk_pose_set_option(self.h, 5, int(bool(on))), "set_option")
+
     def set_tail_chunks(self, chunks):
         """UWVK_OPT_TAIL_CHUNKS: 0 the planner's chunk count, 2..8 forced (tests)."""
         _chk(self.L.uwvk_pose_set_option(self.h, 4, int(chunks)), "set_option")

@@ -1,0 +1,142 @@
+"""GPU parity with the body-frame (right) SO3 boxplus, the largest unpinned
+semantic (PoseUKF.cpp:31-32, :451): the engine's literal
+kernels under UWVK_OPT_SO3_RIGHT against the oracle under or_set_so3_right(1),
+for the predict, every update kind (both apply_delta forms) and multi-epoch
+logs.  Whichever side the real MTK uses, a GPU path reproduces it.  The PSP
+kernels are left-only; the option selects the literal
+kernels.  Tolerances as in test_gpu_parity.py."""
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+from helpers import cov_err, pose_setup, state_err
+
+pytestmark = pytest.mark.gpu
+
+TOL_STEP = 1e-9
+TOL_LOG = 1e-7
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from uwvk import engine
+    if not engine.device_available(0):
+        pytest.fail("no gfx950 device / libuwvk.so not loadable: the HIP path is mandatory")
+    return engine
+
+
+class RightOracle:
+    """OraclePoseBatch whose every call runs with the right boxplus (the
+    oracle's switch is process-wide: set for the call, restored after)."""
+
+    def __init__(self, *a):
+        self.o = O.OraclePoseBatch(*a)
+
+    def __getattr__(self, name):
+        fn = getattr(self.o, name)
+
+        def call(*a, **k):
+            with O.so3_right():
+                return fn(*a, **k)
+        return call
+
+
+def _pair(eng, batch, dof, mode="C3", epochs=10, literal=False):
+    cfg, uwv, log = pose_setup(batch, dof, mode, epochs)
+    o = RightOracle(batch, dof)
+    g = eng.PoseUKFBatch(batch, dof)
+    g.set_so3_right(True)
+    if literal:
+        g.set_literal_apply_delta(True)
+    for f in (o, g):
+        f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+        f.set_process_noise_from_config(cfg, 1e-3)
+    return cfg, uwv, log, o, g
+
+
+def _check(o, g, dof, tol):
+    (xo, Po), (xg, Pg) = o.get_state(), g.get_state()
+    assert np.all(np.isfinite(xg)) and np.all(np.isfinite(Pg))
+    se, ce = state_err(xg, xo, Po, dof).max(), cov_err(Pg, Po).max()
+    assert se < tol and ce < tol, (se, ce)
+
+
+@pytest.mark.parametrize("dof", [53, 26])
+def test_predict_right(eng, dof):
+    cfg, uwv, log, o, g = _pair(eng, 6, dof)
+    for k in range(3):
+        for f in (o, g):
+            f.set_rotation_rate(log["gyro"][k])
+            f.predict(1e-3)
+    _check(o, g, dof, TOL_STEP)
+
+
+@pytest.mark.parametrize("literal", [False, True])
+@pytest.mark.parametrize("kind", ["acceleration", "velocity", "pressure", "water_velocity", "xy", "z", "efforts",
+                                  "efforts_vel", "geographic", "delayed_xy"])
+def test_single_update_right(eng, kind, literal):
+    dof, B = 53, 5
+    cfg, uwv, log, o, g = _pair(eng, B, dof, literal=literal)
+    for f in (o, g):
+        f.set_rotation_rate(log["gyro"][0])
+        f.predict(1e-3)
+    x, _ = o.get_state()
+    rng = np.random.default_rng(11)
+    extra, only_vel = None, 0
+    if kind == "acceleration":
+        mu, cov = log["acc"][0], log["acc_cov"]
+    elif kind == "velocity":
+        mu, cov = x[:, 7:10] + 0.01 * rng.standard_normal((B, 3)), np.eye(3) * 1e-4
+    elif kind == "pressure":
+        mu, cov = (101325.0 + 10.0 * 9.81 * 1025 + 50 * rng.standard_normal(B))[:, None], np.array([[1e4]])
+        extra = np.array([0.1, -0.2, 0.3])
+    elif kind == "water_velocity":
+        mu, cov = 0.3 * rng.standard_normal((B, 2)), np.eye(2) * 0.05 ** 2
+        extra = np.array([0.0, 0.25, 0.5, 0.75, 1.0])
+    elif kind in ("xy", "delayed_xy"):
+        mu, cov = x[:, 0:2] + rng.standard_normal((B, 2)), np.eye(2) * 0.5
+        if kind == "delayed_xy":
+            extra = x[:, 0:2] - 0.3
+    elif kind == "z":
+        mu, cov = x[:, 2:3] + 0.1 * rng.standard_normal((B, 1)), np.array([[0.01]])
+    elif kind in ("efforts", "efforts_vel"):
+        mu, cov = 20 * rng.standard_normal((B, 6)), np.diag([25.0, 25, 25, 1, 1, 1])
+        only_vel = 1 if kind == "efforts_vel" else 0
+        kind = "efforts"
+    else:  # geographic
+        from uwvk import synth
+        lat = synth.LAT0 + (x[:, 0] + rng.standard_normal(B)) / 6.39e6
+        lon = synth.LON0 - (x[:, 1] + rng.standard_normal(B)) / 3.84e6
+        mu, cov = np.stack([lat, lon], 1), np.eye(2) * 4.0
+        extra = np.array([0.5, 0.0, -0.2])
+    np.testing.assert_array_equal(o.update(kind, mu, cov, extra=extra, only_vel=only_vel),
+                                  g.update(kind, mu, cov, extra=extra, only_vel=only_vel))
+    _check(o, g, dof, TOL_STEP)
+
+
+@pytest.mark.parametrize("dof,mode,epochs,literal", [(53, "C3", 400, False), (26, "C3", 400, False),
+                                                     (53, "C4", 1000, False), (53, "C3", 400, True)])
+def test_run_log_right(eng, dof, mode, epochs, literal):
+    cfg, uwv, log, o, g = _pair(eng, 4, dof, mode, epochs, literal=literal)
+    counts_o = o.run_log(log)
+    acc = eng.DeviceBuffer(np.zeros((4, 4), np.uint32))
+    g.run_log(g.upload_log(log), accept_counts=acc)
+    np.testing.assert_array_equal(counts_o, acc.read(np.uint32, (4, 4)))
+    assert not g.get_status().any()
+    _check(o, g, dof, TOL_LOG)
+
+
+def test_right_differs_from_left(eng):
+    """The switch reaches the kernels: the same 400-epoch C3 log on the left
+    and right engine paths differs by far more than the parity tolerance."""
+    cfg, uwv, log = pose_setup(2, 53, "C3", 400)
+    xs = []
+    for right in (False, True):
+        g = eng.PoseUKFBatch(2, 53)
+        g.set_dense_sigma(True)
+        g.set_so3_right(right)
+        g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+        g.set_process_noise_from_config(cfg, 1e-3)
+        g.run_log(g.upload_log(log))
+        xs.append(g.get_state())
+    assert state_err(xs[1][0], xs[0][0], xs[0][1], 53).max() > 0.1
