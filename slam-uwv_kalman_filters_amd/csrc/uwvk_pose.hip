@@ -656,6 +656,8 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     HIPCHK(hipStreamSynchronize(h->stream));
     hf = fl.data();
   }
+  std::memcpy(h->sh.log_acc_cov, log->acc_cov, sizeof(h->sh.log_acc_cov));
+  std::memcpy(h->sh.log_dvl_cov, log->dvl_cov, sizeof(h->sh.log_dvl_cov));
   HIPCHK(upload_shared(h, log->dt));
   const PoseShared sh = h->sh;  // after upload_shared (it refreshes the Q shape)
   int64_t e = first;

@@ -43,6 +43,11 @@ struct PoseShared {
   int q_bw;  // max band width below the diagonal over rows >= 9 (PSP keeps <= 2 in registers)
   int q_simple;  // PSP: lane-resident dt^2 Q suffices (see psp::LaneQ)
   int so3_right;  // UWVK_OPT_SO3_RIGHT: body-frame SO3 [+]/[-] (literal kernels only; qplus_side)
+  // run_log's per-log measurement covariances, read by the PSP epoch kernel
+  // through the per-epoch constant-space pointer (scalar loads where used):
+  // from the kernel arguments they were SGPRs live across the epoch loop,
+  // spilled to VGPR lanes and read back ~2x per epoch (tools/spill_report.py)
+  double log_acc_cov[9], log_dvl_cov[9];
 };
 
 struct PoseBufs {

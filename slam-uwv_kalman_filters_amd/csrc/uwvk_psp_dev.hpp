@@ -61,6 +61,12 @@
 #ifndef PSP_FAST
 #define PSP_FAST 7039
 #endif
+// PSP_DIAG_HOT (tools/isa_hot.py only, results invalid): the cold fallbacks
+// (library SO3 exp/log and sincos, the general-Q branches, the periodic fold)
+// compiled out, so that the static code of the epoch loop is the C3 hot path
+#ifndef PSP_DIAG_HOT
+#define PSP_DIAG_HOT 0
+#endif
 
 namespace uwvk {
 namespace psp {
@@ -157,7 +163,8 @@ UWVK_DEV void so3_exp_psp(const double v[3], double o[4]) {
     c = fma(c, u, 1.0);
     o[0] = c; o[1] = s * v[0]; o[2] = s * v[1]; o[3] = s * v[2];
   } else {
-    so3_exp(v, o);
+    if (PSP_DIAG_HOT) o[0] = 1.0, o[1] = o[2] = o[3] = 0.0;
+    else so3_exp(v, o);
   }
 }
 UWVK_DEV void so3_log_psp(const double q[4], double o[3]) {
@@ -186,7 +193,8 @@ UWVK_DEV void so3_log_psp(const double q[4], double o[3]) {
     const double k = 2.0 * a * iw;  // 2 atan2(|v|, w) / |v|
     o[0] = k * x; o[1] = k * y; o[2] = k * z;
   } else {
-    so3_log(q, o);
+    if (PSP_DIAG_HOT) o[0] = o[1] = o[2] = 0.0;
+    else so3_log(q, o);
   }
 }
 UWVK_DEV void qboxminus_psp(const double a[4], const double b[4], double o[3]) {
@@ -266,14 +274,29 @@ UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
 // acceleration and gravity keep d = 1.
 UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 
+#ifndef PSP_PIV_EARLY
+#define PSP_PIV_EARLY 0  // r03: fewer VALU (-56 per epoch) but 176 VGPRs (2 waves per SIMD), not kept
+#endif
 // column J broadcast through an LDS column (no readlanes); the rows the
 // sigma-point lanes need (RL::rows) are staged in the same step: lane r with
-// q = row_pos(r) writes L[r][J] to rows[q*K + J] (one write per column)
+// q = row_pos(r) writes L[r][J] to rows[q*K + J] (one write per column).
+// piv: this step's pivot (an SGPR pair from the look-ahead readlane); with
+// PSP_PIV_EARLY the look-ahead also takes the next pivot's rsqrt at once, so
+// only the VGPR result crosses the step: the SGPR pair, held across the
+// column update, was spilled to a VGPR lane and read back (2 v_writelane + 2
+// v_readlane per column step, tools/spill_report.py).  The sign test rides on
+// the rsqrt: rsqrt of a pivot <= 0 or NaN is NaN or +-inf, so chk += inv * 0
+// is NaN exactly when some pivot failed piv > 0 (pchol tests chk once).
 template <int K, int J>
-UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, double* rows, int q, double piv) {
+UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, double* rows, int q, double piv,
+                             double inv_in, double& chk) {
   if constexpr (J < K) {
+#if PSP_PIV_EARLY && (PSP_FAST & 16)
+    const double inv = inv_in;  // sign of piv already folded into ok
+#else
     ok = ok && (piv > 0.0);
     const double inv = rsqrt_f64(piv);
+#endif
 #if PSP_FAST & 16
     // lane J's own a[J] is the pivot (the look-ahead below evaluates the same
     // fma as the column update), so one product serves the diagonal too
@@ -283,8 +306,15 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
 #endif
     // look-ahead: the next pivot is lane J+1's a[J+1] - L[J+1][J]^2 (its own
     // registers), so its rsqrt need not wait for the column broadcast
-    double pnext = 0.0;
-    if constexpr (J + 1 < K) pnext = readlane_d(a[J + 1] - a[J] * a[J], J + 1);
+    double pnext = 0.0, invn = 0.0;
+    if constexpr (J + 1 < K) {
+      pnext = readlane_d(a[J + 1] - a[J] * a[J], J + 1);
+#if PSP_PIV_EARLY && (PSP_FAST & 16)
+      invn = rsqrt_f64(pnext);
+      asm volatile("" : "+v"(invn));  // here, not sunk to its use behind the column update
+      chk = fma(invn, 0.0, chk);
+#endif
+    }
     if (q >= 0) rows[q * K + J] = a[J];
     if constexpr (J + 1 < K) {
       // col aliases the LAST staged row's not-yet-written slots J+1 .. K-1:
@@ -299,7 +329,7 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
 #pragma unroll
       for (int c = J + 1; c < K; c++) asm volatile("" : "+v"(a[c]));
     }
-    pchol_step_lds<K, J + 1>(a, r, ok, col, rows, q, pnext);
+    pchol_step_lds<K, J + 1>(a, r, ok, col, rows, q, pnext, invn, chk);
   }
 }
 
@@ -328,7 +358,13 @@ UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* s
 #pragma unroll
   for (int k = 0; k < RL::NR; k++) q = (r == RL::rows[k]) ? k : q;
   static_assert(RL::NR >= 1 && STG_ROWS + RL::NR * K <= 115, "staging area (PG::STG)");
-  pchol_step_lds<K, 0>(a, r, ok, stg + STG_ROWS + (RL::NR - 1) * K, stg + STG_ROWS, q, readlane_d(a[0], 0));
+  const double p0 = readlane_d(a[0], 0);
+  const double inv0 = rsqrt_f64(p0);
+  double chk = fma(inv0, 0.0, 0.0);
+  pchol_step_lds<K, 0>(a, r, ok, stg + STG_ROWS + (RL::NR - 1) * K, stg + STG_ROWS, q, p0, inv0, chk);
+#if PSP_PIV_EARLY && (PSP_FAST & 16)
+  ok = chk == 0.0;
+#endif
   psync();  // the staged rows are read by the point lanes next
   return ok;
 }
@@ -400,7 +436,8 @@ UWVK_DEV void proc_orientation(const double x[Lay<DOF>::store], const PoseShared
     sl = sh.slat0 * cd + sh.clat0 * sd;
     cl = sh.clat0 * cd - sh.slat0 * sd;
   } else {
-    sincos(sh.lat0 + dl, &sl, &cl);
+    if (PSP_DIAG_HOT) sl = cl = 0.0;
+    else sincos(sh.lat0 + dl, &sl, &cl);
   }
   const double er[3] = {kEarthW * cl, 0.0, kEarthW * sl};
   double wb[3], wn[3];
@@ -742,7 +779,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       }
     }
   };
-  if (qs)
+  if (qs || PSP_DIAG_HOT)
     rows_lt9(std::true_type{});
   else
     rows_lt9(std::false_type{});
@@ -787,7 +824,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
         }
       }
     };
-    if (qs)
+    if (qs || PSP_DIAG_HOT)
       band(std::true_type{});
     else
       band(std::false_type{});
@@ -809,7 +846,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       }
     }
 #endif
-    for (int k = 3; k <= bw; k++) {  // uniform bound: wide Q bands only
+    for (int k = 3; k <= (PSP_DIAG_HOT ? 0 : bw); k++) {  // uniform bound: wide Q bands only
       const double idj = shfl_d(ids, l - k >= 0 ? l - k : 0);
       const int j = l - k;
       if (l >= R0 && l < DOF && j >= R0) {

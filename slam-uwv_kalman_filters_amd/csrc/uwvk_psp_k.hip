@@ -332,10 +332,26 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
   uint32_t cnt[4] = {0, 0, 0, 0};
   MeasArgs ma{};
   ma.v3[0] = ea.p_sens[0]; ma.v3[1] = ea.p_sens[1]; ma.v3[2] = ea.p_sens[2];
-  double w[3] = {b.rot[inst * 3], b.rot[inst * 3 + 1], b.rot[inst * 3 + 2]};
+  // the stored rotation rate (PoseUKF.cpp:492-496) lives in pc.w only (a
+  // second copy for the final store was a second set of loop-carried VGPRs)
   ProcCtx pc;
-  for (int k = 0; k < 3; k++) pc.w[k] = w[k];
+  for (int k = 0; k < 3; k++) pc.w[k] = b.rot[inst * 3 + k];
+#ifndef PSP_DT_VGPR
+#define PSP_DT_VGPR 1
+#endif
+#if PSP_DT_VGPR
+  // dt as a VGPR: a uniform kernel argument is an SGPR pair live across the
+  // whole epoch loop, which the allocator spilled to a VGPR lane and reloaded
+  // (four v_readlane, the whole 16-byte kernarg group) at each of its ~23
+  // uses per epoch (tools/isa_hot.py); as a VGPR each use is an operand
+  {
+    double dtv = ea.dt;
+    asm volatile("" : "+v"(dtv));
+    pc.dt = dtv;
+  }
+#else
   pc.dt = ea.dt;
+#endif
   pc.off = nullptr;
   lane_proc<DOF>(b, *b.shared, inst, lane_id(), pc);
   // the next epoch's IMU inputs are prefetched one epoch ahead (their load
@@ -367,29 +383,38 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
     const uint32_t fl = fl_n;
 #endif
     const double g[3] = {g_n[0], g_n[1], g_n[2]}, za[3] = {a_n[0], a_n[1], a_n[2]};
+#ifndef PSP_FETCH_LATE
+#define PSP_FETCH_LATE 0
+#endif
+#if !PSP_FETCH_LATE
     if (e + 1 < e_end) fetch(e + 1);
+#endif
     if (all_finite(g, 3)) {  // integrateMeasurement(RotationRate): checkMeasurment, then store
-      for (int k = 0; k < 3; k++) { w[k] = g[k]; pc.w[k] = g[k]; }
+      for (int k = 0; k < 3; k++) pc.w[k] = g[k];
     } else {
       nan = true;
     }
     const PoseShared& sh = shared_for_epoch(b);
     UWVK_STAMP(41);
-    if (((e - ea.first) & 1023) == 1023) psp_fold<DOF>(sm, ds, ids);  // keep d in range
+    if (!PSP_DIAG_HOT && ((e - ea.first) & 1023) == 1023) psp_fold<DOF>(sm, ds, ids);  // keep d in range
     bool sok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, st);
     ok = ok && sok;
+#if PSP_FETCH_LATE  // the next epoch's inputs issued after the predict: a shorter live range
+    if (e + 1 < e_end) fetch(e + 1);
+#endif
     if (fl & UWVK_EV_ACC) {
       if (all_finite(za, 3)) {
-        do_update<DOF, MK_ACC>(sm, sh, inst, za, ea.acc_cov, ma, &sok, ds, ids, st);
+        do_update<DOF, MK_ACC>(sm, sh, inst, za, sh.log_acc_cov, ma, &sok, ds, ids, st);
         ok = ok && sok;
       } else {
         nan = true;
       }
     }
+#ifndef PSP_HOT_ONLY  // diagnostic builds (tools/isa_hot.py): the C3 epoch's predict + acceleration update only
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + inst) * 3;
       if (all_finite(z, 3)) {
-        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, inst, z, ea.dvl_cov, ma, &sok, ds, ids, st);
+        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, inst, z, sh.log_dvl_cov, ma, &sok, ds, ids, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -415,13 +440,14 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
         ok = ok && sok;
       }
     }
+#endif
   }
   if (lane_id() == 0) {
     // atomic: a later chunk that timed out flags the same word
     const uint32_t bits = (ok ? 0u : UWVK_ST_NOTPD) | (nan ? UWVK_ST_NAN : 0u);
     if (bits) __hip_atomic_fetch_or(b.status + inst, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (e_end > e_begin) {
-      b.rot[inst * 3] = w[0]; b.rot[inst * 3 + 1] = w[1]; b.rot[inst * 3 + 2] = w[2];
+      b.rot[inst * 3] = pc.w[0]; b.rot[inst * 3 + 1] = pc.w[1]; b.rot[inst * 3 + 2] = pc.w[2];
     }
     if (ea.accept_counts)
       for (int k = 0; k < 4; k++) ea.accept_counts[inst * 4 + k] += cnt[k];
