@@ -31,6 +31,15 @@
 #ifndef PSP_RB
 #define PSP_RB 8          // rows per block of the row-block sweeps
 #endif
+#ifndef PSP_DELTA_LDS  // r03 A/B: the predict's Delta_j broadcast through LDS (one j at a time) instead of v_readlane
+#define PSP_DELTA_LDS 0
+#endif
+#ifndef PSP_RANKM_MFMA  // r03 A/B: the update's rank-M pass on v_mfma_f64_16x16x4_f64 tiles (rankm_mfma)
+#define PSP_RANKM_MFMA 0
+#endif
+#ifndef PSP_PAIR_MASK  // r03: rankm_pairs' half selection by lane-mask arithmetic (no exec branches)
+#define PSP_PAIR_MASK 1
+#endif
 #ifndef PSP_RBP
 #define PSP_RBP 6         // row pairs per block of the paired rank-M sweep (rankm_pairs); 8 -> 6: 167 -> 150 VGPRs, A/B +0.3%
 #endif
@@ -702,10 +711,38 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   double X[3];
   {
     double Y[3] = {0.0, 0.0, 0.0};
+#if PSP_DELTA_LDS
+    // Delta_j staged in stg (free after the ori x ori sums) by lane 2j and read
+    // back by every lane as a broadcast, one j at a time (a compiler memory
+    // barrier per j keeps at most two j's loads in flight: hoisted all at once
+    // they took 90 VGPRs); 45 LDS reads instead of 90 v_readlane
+    if ((l & 1) == 0 && l < 2 * K) {
+#pragma unroll
+      for (int i = 0; i < 3; i++) sm.stg[(l >> 1) * 3 + i] = dd[i];
+    }
+    wsync();
+    double dn[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) dn[i] = sm.stg[i];
+#pragma unroll
+    for (int j = 0; j < ((PSP_ABL & 4) ? 0 : K); j++) {
+      double dj[3] = {dn[0], dn[1], dn[2]};
+      if (j + 1 < K) {
+#pragma unroll
+        for (int i = 0; i < 3; i++) dn[i] = sm.stg[3 * (j + 1) + i];
+      }
+#pragma unroll
+      for (int i = 0; i < 3; i++) Y[i] += a[j] * dj[i];
+      // j's products before the barrier, j + 2's loads after it
+      asm volatile("" : "+v"(Y[0]), "+v"(Y[1]), "+v"(Y[2])::"memory");
+    }
+    wsync();  // stg is rewritten by the next phase's users
+#else
 #pragma unroll
     for (int j = 0; j < ((PSP_ABL & 4) ? 0 : K); j++)
 #pragma unroll
       for (int i = 0; i < 3; i++) Y[i] += a[j] * readlane_d(dd[i], 2 * j);
+#endif
     const int cp = proc_couple(l);
     const int src = cp >= 0 ? cp : l;
 #if PSP_DIAG_SEL
@@ -1030,8 +1067,28 @@ UWVK_DEV void rankm_rows(double* S, const double* stg, int i0, int c0, int l, co
 // Kx = K~ of column l & 31.
 template <int R, int M, int P>
 UWVK_DEV void rankm_pairs(double* S, const double* stg, int p0, int l, const double (&Kx)[M]) {
-  const bool hi = l >= 32;
   const int col = l & 31;
+#if PSP_PAIR_MASK
+  // the half's row and packed row offset as uniform (scalar) values blended
+  // with the lane mask hm = -(l >> 5) (bitwise and / add): written as
+  // `hi ? pb : pa` the compiler branched on the lane-divergent condition, two
+  // exec-masked paths per row with the offsets computed inside (r03 ISA)
+  const int hm = -(l >> 5);
+  double sv[R], cv[R][M];
+  int ad[R], row[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int pa = p0 + r, pb = P - 1 - pa;
+    const int ta = pa * (pa + 1) / 2, tb = pb * (pb + 1) / 2;
+    row[r] = pa + ((pb - pa) & hm);
+    ad[r] = ta + ((tb - ta) & hm) + col;
+    sv[r] = S[ad[r]];
+    const double* c = stg + M * row[r];
+#pragma unroll
+    for (int a = 0; a < M; a++) cv[r][a] = c[a];
+  }
+#else
+  const bool hi = l >= 32;
   double sv[R], cv[R][M];
   int ad[R], row[R];
 #pragma unroll
@@ -1043,12 +1100,75 @@ UWVK_DEV void rankm_pairs(double* S, const double* stg, int p0, int l, const dou
 #pragma unroll
     for (int a = 0; a < M; a++) cv[r][a] = stg[M * row[r] + a];
   }
+#endif
 #pragma unroll
   for (int r = 0; r < R; r++) {
     double s2 = sv[r];
 #pragma unroll
     for (int a = 0; a < M; a++) s2 = fma(-cv[r][a], Kx[a], s2);
     if (col <= row[r]) S[ad[r]] = s2;
+  }
+}
+
+// Sigma~ -= C~ K~^T on v_mfma_f64_16x16x4_f64 (PSP_RANKM_MFMA): the packed
+// lower triangle as the 16 x 16 tiles (I, J), J <= I, of a 16 NT frame.  Tile
+// D = A B + acc with A[r][k] = -C~[16 I + r][k], B[k][c] = K~[16 J + c][k]
+// (k < M, zero padded to K = 4) and acc the tile of Sigma~ (lane l holds rows
+// (l >> 4) + 4 i, column l & 15: the f64 C/D map, uwvk_dev.hpp).  The
+// operands are transposed through stg one 16-row block at a time (the rows'
+// lanes write C~ / K~, every lane reads component l >> 4 of row l & 15).
+// Rows >= DOF are clamped on load and never stored; in diagonal tiles only
+// column <= row is stored.  The per-entry flops and their summation order
+// differ from the FMA-chain row sweep only in rounding.
+template <int DOF, int M>
+UWVK_DEV void rankm_mfma(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
+  static_assert(M <= 3, "rank <= 3 (K = 4 with zero padding)");
+  constexpr int NT = (DOF + 15) / 16;
+  static_assert(2 * 16 * M <= PG<DOF>::STG, "operand blocks (PG::STG)");
+  // (the masks give the compiler the ranges: l is a laundered lane id)
+  const int q = (l >> 4) & 3, c = l & 15;
+  double Aop[NT], Bop[NT];
+#pragma unroll
+  for (int T = 0; T < NT; T++) {
+    if (q == T) {
+#pragma unroll
+      for (int k = 0; k < M; k++) {
+        stg[c * M + k] = Ct[k];
+        stg[16 * M + c * M + k] = Kt[k];
+      }
+    }
+    wsync();
+    const int qq = q < M ? q : 0;
+    const double a = stg[c * M + qq], b = stg[16 * M + c * M + qq];
+    Aop[T] = q < M ? -a : 0.0;
+    Bop[T] = q < M ? b : 0.0;
+    wsync();  // the next block's writes after every lane's reads
+  }
+#pragma unroll
+  for (int I = 0; I < NT; I++) {
+    // packed offsets of this lane's rows 16 I + q + 4 i (clamped into the triangle)
+    int base[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      unsigned R = 16 * I + q + 4 * i;
+      if (16 * I + 4 * i + 3 >= DOF) R = R < DOF ? R : DOF - 1;  // only the last rows can pass DOF
+      base[i] = (int)((R * (R + 1)) >> 1) + c;
+    }
+#pragma unroll
+    for (int J = 0; J <= I; J++) {
+      d4_t acc;
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[i] = (16 * I + 4 * i < DOF) ? S[base[i] + 16 * J] : 0.0;
+      acc = mfma_f64(Aop[I], Bop[J], acc);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if (16 * I + 4 * i >= DOF) continue;  // no row of this register is in the triangle
+        const int R = 16 * I + q + 4 * i;
+        const bool row_ok = (16 * I + 4 * i + 3 < DOF) || R < DOF;  // compile-time true but for the last rows
+        const bool st = row_ok && (I > J || c <= q + 4 * i);
+        if (st) S[base[i] + 16 * J] = acc[i];
+      }
+    }
   }
 }
 
@@ -1276,7 +1396,10 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     Ct[i] = C[i] * ids;
     Kt[i] = Kg[i] * ids;
   }
-#if PSP_FAST & 2048
+#if PSP_RANKM_MFMA
+  psync();
+  if (!(PSP_ABL & 2)) rankm_mfma<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
+#elif PSP_FAST & 2048
   {
     // rows [0, P) paired (rankm_pairs), then rows [P, DOF) one per step; the
     // C~ rows of each part are staged in stg in turn
