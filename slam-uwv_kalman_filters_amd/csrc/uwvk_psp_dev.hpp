@@ -34,6 +34,9 @@
 #ifndef PSP_DELTA_LDS  // r03 A/B: the predict's Delta_j broadcast through LDS (one j at a time) instead of v_readlane
 #define PSP_DELTA_LDS 0
 #endif
+#ifndef PSP_UPD_LDS  // r03 A/B: the update's P and Dz broadcast through LDS instead of v_readlane
+#define PSP_UPD_LDS 0
+#endif
 #ifndef PSP_RANKM_MFMA  // r03 A/B: the update's rank-M pass on v_mfma_f64_16x16x4_f64 tiles (rankm_mfma)
 #define PSP_RANKM_MFMA 0
 #endif
@@ -1334,6 +1337,53 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   // Glin_r = G_r - sum_j L[r][j] P[:, j]: row r of (Sigma - L_a L_a^T) H^T;
   // C_r = Glin_r + 1/2 sum_j L[r][j] Dz_j; S += H Glin + R  (H Glin = H Sigma H^T - P P^T)
   double Gl[M], C[M];
+#if PSP_UPD_LDS
+  if constexpr (K > 0) {
+    // P (lane i K + j) and Dz_j (lane 2 j) staged in stg (free after the sums)
+    // and read back as broadcasts one j at a time, as the predict's Delta
+    // (PSP_DELTA_LDS): LDS reads instead of 4 M K v_readlane
+    static_assert(2 * M * K <= PG<DOF>::STG, "P and Dz (PG::STG)");
+    if (l < M * K) sm.stg[(l % K) * M + l / K] = Pl;  // j-major: P[i][j] at j M + i
+    if ((l & 1) == 0 && l < 2 * K) {
+#pragma unroll
+      for (int i = 0; i < M; i++) sm.stg[M * K + (l >> 1) * M + i] = zd[i];
+    }
+    wsync();
+    double g[M], c[M];
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      g[i] = Gr[i];
+      c[i] = 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      double pj[M], zj[M];
+#pragma unroll
+      for (int i = 0; i < M; i++) {
+        pj[i] = sm.stg[j * M + i];
+        zj[i] = sm.stg[M * K + j * M + i];
+      }
+#pragma unroll
+      for (int i = 0; i < M; i++) {
+        g[i] -= a[j] * pj[i];
+        c[i] += a[j] * zj[i];
+        asm volatile("" : "+v"(g[i]), "+v"(c[i])::"memory");  // one j's loads in flight
+      }
+    }
+    wsync();  // stg is rewritten by the rank-M staging
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      Gl[i] = g[i];
+      C[i] = g[i] + 0.5 * c[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      Gl[i] = Gr[i];
+      C[i] = Gr[i];
+    }
+  }
+#else
 #pragma unroll
   for (int i = 0; i < M; i++) {
     double g = Gr[i], c = 0.0;
@@ -1347,6 +1397,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     Gl[i] = g;
     C[i] = g + 0.5 * c;
   }
+#endif
 #pragma unroll
   for (int i = 0; i < M; i++)
 #pragma unroll
