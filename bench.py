@@ -154,10 +154,16 @@ def counter_roofline(e, waves, epochs, kernel_ms):
     if not {"valu_fma_f64", "valu_mul_f64", "valu_add_f64"} <= set(pw):
         return None
     lane_flop = 64 * (2 * pw["valu_fma_f64"] + pw["valu_mul_f64"] + pw["valu_add_f64"])
-    out = {"fp64_lane_flop_per_wave_epoch": lane_flop,
-           "achieved_tflops": lane_flop * waves * epochs / (kernel_ms * 1e-3) / 1e12,
+    # f64 MFMA work (the update's rank-M tiles, r03): SQ_INSTS_VALU_MFMA_MOPS_F64 x 512,
+    # executed on the same fp64 pipe, so it adds to the VALU figure (0 without the pass)
+    mfma_flop = (e.get("mfma") or {}).get("flop_per_wave_epoch", 0.0)
+    out = {"fp64_lane_flop_per_wave_epoch": lane_flop, "fp64_mfma_flop_per_wave_epoch": mfma_flop,
+           "achieved_tflops": (lane_flop + mfma_flop) * waves * epochs / (kernel_ms * 1e-3) / 1e12,
            "epochs_profiled": e.get("epochs_per_launch"), "source": e.get("valu_source")}
-    for k in ("valu_busy", "active_lanes"):
+    lanes = (e.get("active_lanes") or {}).get("thread_cycles_per_valu_quad_cycle")
+    if lanes:  # VALU lane-slots scaled by the active-lane share; MFMA tiles count whole
+        out["active_tflops"] = (lane_flop * lanes / 64.0 + mfma_flop) * waves * epochs / (kernel_ms * 1e-3) / 1e12
+    for k in ("valu_busy", "active_lanes", "mfma"):
         if k in e:
             out[k] = e[k]
     return out
@@ -455,7 +461,7 @@ def main():
     frac_useful = model_tf / PEAK_FP64_TFLOPS
     frac_issued = cr["achieved_tflops"] / PEAK_FP64_TFLOPS if cr else None
     lanes = ((cr or {}).get("active_lanes") or {}).get("thread_cycles_per_valu_quad_cycle")
-    frac_active = frac_issued * lanes / 64.0 if (frac_issued is not None and lanes) else None
+    frac_active = cr["active_tflops"] / PEAK_FP64_TFLOPS if (cr and "active_tflops" in cr) else None
     roof = {"bound": "valu-fp64", "achieved": model_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
             "frac": frac_useful, "traffic": traffic,
             "frac_useful": frac_useful, "frac_active": frac_active, "frac_issued": frac_issued,
@@ -464,11 +470,11 @@ def main():
                                "2k+1 model evaluations, O(n^2) covariance algebra per step, DESIGN.md 4.3) over this "
                                "run's HIP-event kernel time; frac = frac_useful",
             "frac_issued_source": ("fp64 VALU lane-slot flops, 64 x (2 SQ_INSTS_VALU_FMA_F64 + SQ_INSTS_VALU_MUL_F64 "
-                                   "+ SQ_INSTS_VALU_ADD_F64) per wave-epoch from the committed PMC passes of this "
+                                   "+ SQ_INSTS_VALU_ADD_F64), plus 512 x SQ_INSTS_VALU_MFMA_MOPS_F64, per wave-epoch from the committed PMC passes of this "
                                    "launch shape (%s), over this run's kernel time: counts masked lanes, an upper "
                                    "bound" % (cr or {}).get("source")) if cr else None,
-            "frac_active_source": ("frac_issued x SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / 64 (%.1f of 64 lanes "
-                                   "active per VALU cycle)" % lanes) if frac_active is not None else None,
+            "frac_active_source": ("VALU lane-slot flops x SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / 64 (%.1f of 64 lanes "
+                                   "active per VALU cycle), plus the MFMA flops" % lanes) if frac_active is not None else None,
             "counters": cr,
             "model_flop_per_step": (F_STEP_EXEC if a.dense else F_STEP_PSP),
             "model_tflops": model_tf,

@@ -31,14 +31,14 @@
 #ifndef PSP_RB
 #define PSP_RB 8          // rows per block of the row-block sweeps
 #endif
-#ifndef PSP_DELTA_LDS  // r03 A/B: the predict's Delta_j broadcast through LDS (one j at a time) instead of v_readlane
-#define PSP_DELTA_LDS 0
+#ifndef PSP_DELTA_LDS  // r03: the predict's Delta_j broadcast through LDS (one j at a time) instead of v_readlane
+#define PSP_DELTA_LDS 1
 #endif
-#ifndef PSP_UPD_LDS  // r03 A/B: the update's P and Dz broadcast through LDS instead of v_readlane
-#define PSP_UPD_LDS 0
+#ifndef PSP_UPD_LDS  // r03: the update's P and Dz broadcast through LDS instead of v_readlane
+#define PSP_UPD_LDS 1
 #endif
-#ifndef PSP_RANKM_MFMA  // r03 A/B: the update's rank-M pass on v_mfma_f64_16x16x4_f64 tiles (rankm_mfma)
-#define PSP_RANKM_MFMA 0
+#ifndef PSP_RANKM_MFMA  // r03: the update's rank-M pass on v_mfma_f64_16x16x4_f64 tiles (rankm_mfma);
+#define PSP_RANKM_MFMA 1      // the three together: A/B 79.6 -> 73.4 ms per 200-epoch launch (profiles/r03/ab1)
 #endif
 #ifndef PSP_PAIR_MASK  // r03: rankm_pairs' half selection by lane-mask arithmetic (no exec branches)
 #define PSP_PAIR_MASK 1

@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Fold one tools/pmc_r02.sh run into profiles/pmc_traffic.json (key
 WORKLOAD-eSTEPS) and copy the summaries bench.py's roofline is computed from
-into profiles/r02/.  The timed launch is the LAST k_psp_epoch<53> dispatch of
+into profiles/ROUND_DIR/.  The timed launch is the LAST k_psp_epoch<53> dispatch of
 the bench (the alignment shift and the warm-up launches come first).
 
-usage: tools/pmc_fold.py TAG STEPS [WORKLOAD]"""
+usage: tools/pmc_fold.py TAG STEPS [WORKLOAD] [ROUND_DIR (default r03)]
+An optional "mfma" pass (tools/pmc_r03.sh) adds the f64 MFMA counters."""
 import csv
 import json
 import os
@@ -14,6 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag, steps = sys.argv[1], int(sys.argv[2])
 workload = sys.argv[3] if len(sys.argv) > 3 else "C3-dof53-b65536"
+rdir = sys.argv[4] if len(sys.argv) > 4 else "r03"
 base = os.path.join(ROOT, "gpurun_out", tag, "s%d" % steps)
 KERNEL = "k_psp_epoch<53>"
 N_SIMD = 1024
@@ -34,6 +36,8 @@ mix, d1, rows_mix = last("sq_mix")
 busy, d2, rows_busy = last("sq_busy")
 fetch, d3, rows_f = last("fetch")
 write, d4, rows_w = last("write")
+has_mfma = os.path.exists(os.path.join(base, "mfma", "run_counter_collection.csv"))
+mfma, d5, rows_m = last("mfma") if has_mfma else ({}, None, [])
 waves = mix["SQ_WAVES"]
 # normalised per instance-epoch: one wave per instance, except that the tail
 # instances of a spread launch (UWVK_OPT_TAIL_SLOTS) run as several chunk
@@ -67,24 +71,24 @@ e["active_lanes"] = {
     "thread_cycles_per_valu_quad_cycle": busy["SQ_THREAD_CYCLES_VALU"] / busy["SQ_ACTIVE_INST_VALU"],
     "note": "SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU; 64 would be every lane of every VALU cycle",
 }
-e["source"] = ("profiles/r02/pmc_%s_s%d.csv (rocprofv3 --pmc, one pass per counter group; dispatch %d = the %d-epoch "
-               "timed launch; FETCH_SIZE doubled per MI355X_MICROARCH.md)" % (tag, steps, d3, steps))
-e["valu_source"] = "profiles/r02/pmc_%s_s%d.csv (dispatch %d)" % (tag, steps, d1)
+e["source"] = ("profiles/%s/pmc_%s_s%d.csv (rocprofv3 --pmc, one pass per counter group; dispatch %d = the %d-epoch "
+               "timed launch; FETCH_SIZE doubled per MI355X_MICROARCH.md)" % (rdir, tag, steps, d3, steps))
+e["valu_source"] = "profiles/%s/pmc_%s_s%d.csv (dispatch %d)" % (rdir, tag, steps, d1)
 path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 d = json.load(open(path)) if os.path.exists(path) else {}
 d["%s-e%d" % (workload, steps)] = e
 json.dump(d, open(path, "w"), indent=1)
-os.makedirs(os.path.join(ROOT, "profiles", "r02"), exist_ok=True)
+os.makedirs(os.path.join(ROOT, "profiles", rdir), exist_ok=True)
 keep = ("Dispatch_Id", "Kernel_Name", "Grid_Size", "VGPR_Count", "SGPR_Count", "LDS_Block_Size", "Counter_Name",
         "Counter_Value", "Start_Timestamp", "End_Timestamp")
-with open(os.path.join(ROOT, "profiles", "r02", "pmc_%s_s%d.csv" % (tag, steps)), "w") as f:
+with open(os.path.join(ROOT, "profiles", rdir, "pmc_%s_s%d.csv" % (tag, steps)), "w") as f:
     w = csv.DictWriter(f, fieldnames=list(keep))
     w.writeheader()
-    for rows in (rows_mix, rows_busy, rows_f, rows_w):
+    for rows in (rows_mix, rows_busy, rows_f, rows_w, rows_m):
         for r in rows:
             w.writerow({k: r[k] for k in keep})
 shutil.copy(os.path.join(base, "trace", "run_kernel_stats.csv"),
-            os.path.join(ROOT, "profiles", "r02", "kernel_stats_%s_s%d.csv" % (tag, steps)))
-shutil.copy(os.path.join(base, "trace.json"), os.path.join(ROOT, "profiles", "r02", "bench_%s_s%d_traced.json" % (tag, steps)))
+            os.path.join(ROOT, "profiles", rdir, "kernel_stats_%s_s%d.csv" % (tag, steps)))
+shutil.copy(os.path.join(base, "trace.json"), os.path.join(ROOT, "profiles", rdir, "bench_%s_s%d_traced.json" % (tag, steps)))
 print(json.dumps({k: v for k, v in e.items() if k != "valu_busy"}, indent=1))
 print("valu_busy", e["valu_busy"]["frac"], "model", e["valu_busy"]["model_frac"])
