@@ -71,6 +71,17 @@ e["active_lanes"] = {
     "thread_cycles_per_valu_quad_cycle": busy["SQ_THREAD_CYCLES_VALU"] / busy["SQ_ACTIVE_INST_VALU"],
     "note": "SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU; 64 would be every lane of every VALU cycle",
 }
+if has_mfma:
+    # SQ_INSTS_VALU_MFMA_MOPS_F64 counts f64 MFMA work in units of 512 flops
+    # (v_mfma_f64_16x16x4: 16*16*4*2 = 2,048 flops = 4 units per wave instruction)
+    e["mfma"] = {
+        "insts_f64_per_wave_epoch": mfma["SQ_INSTS_VALU_MFMA_F64"] / we,
+        "mops_f64_per_wave_epoch": mfma["SQ_INSTS_VALU_MFMA_MOPS_F64"] / we,
+        "flop_per_wave_epoch": mfma["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512.0 / we,
+        "busy_frac": mfma["SQ_VALU_MFMA_BUSY_CYCLES"] / mfma["SQ_BUSY_CU_CYCLES"],
+        "busy_definition": "SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CU_CYCLES",
+        "counters": mfma,
+    }
 e["source"] = ("profiles/%s/pmc_%s_s%d.csv (rocprofv3 --pmc, one pass per counter group; dispatch %d = the %d-epoch "
                "timed launch; FETCH_SIZE doubled per MI355X_MICROARCH.md)" % (rdir, tag, steps, d3, steps))
 e["valu_source"] = "profiles/%s/pmc_%s_s%d.csv (dispatch %d)" % (rdir, tag, steps, d1)
