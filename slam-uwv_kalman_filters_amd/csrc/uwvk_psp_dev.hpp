@@ -37,8 +37,10 @@
 #ifndef PSP_UPD_LDS  // r03: the update's P and Dz broadcast through LDS instead of v_readlane
 #define PSP_UPD_LDS 1
 #endif
-#ifndef PSP_RANKM_MFMA  // r03: the update's rank-M pass on v_mfma_f64_16x16x4_f64 tiles (rankm_mfma);
-#define PSP_RANKM_MFMA 1      // the three together: A/B 79.6 -> 73.4 ms per 200-epoch launch (profiles/r03/ab1)
+#ifndef PSP_RANKM_MFMA  // r03: the update's rank-M pass on v_mfma_f64_16x16x4_f64 tiles: 1 rankm_mfma (16-aligned
+#define PSP_RANKM_MFMA 2      // frame), 2 rankm_mfma_o (frame shifted by DOF % 16, row-block MFMAs back to back),
+                              // 3 rankm_mfma_all (all tiles in flight).  DELTA_LDS + UPD_LDS + 1: A/B 79.6 -> 73.4 ms
+                              // per 200-epoch launch (profiles/r03/ab1); 2: 73.5-73.9 -> 72.5 (ab2), 3: 72.7-73.0
 #endif
 #ifndef PSP_PAIR_MASK  // r03: rankm_pairs' half selection by lane-mask arithmetic (no exec branches)
 #define PSP_PAIR_MASK 1
@@ -1175,6 +1177,181 @@ UWVK_DEV void rankm_mfma(double* S, double* stg, const double (&Ct)[M], const do
   }
 }
 
+// one row block I of rankm_mfma_o (tiles (I, J), J <= I), then block I + 1
+template <int DOF, int I, int NT>
+UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop)[NT], int q, int c) {
+  if constexpr (I < NT) {
+    constexpr int O = DOF - 16 * NT;
+    int base[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const unsigned R = O + 16 * I + q + 4 * i;
+      base[i] = (int)((R * (R + 1)) >> 1) + O + c;
+    }
+    d4_t acc[I + 1];
+#pragma unroll
+    for (int J = 0; J <= I; J++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[J][i] = S[base[i] + 16 * J];
+#pragma unroll
+    for (int J = 0; J <= I; J++) acc[J] = mfma_f64(Aop[I], Bop[J], acc[J]);
+    // one empty asm over every accumulator: all MFMAs issue before the first
+    // store waits for its result (otherwise: MFMA, s_nop 16, stores, MFMA ...)
+    if constexpr (I == 0) asm volatile("" : "+v"(acc[0]));
+    else if constexpr (I == 1) asm volatile("" : "+v"(acc[0]), "+v"(acc[1]));
+    else if constexpr (I == 2) asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]));
+    else asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
+#pragma unroll
+    for (int J = 0; J <= I; J++)
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (J < I || c <= q + 4 * i) S[base[i] + 16 * J] = acc[J][i];
+    rankm_block<DOF, I + 1, NT>(S, Aop, Bop, q, c);
+  }
+}
+
+// The same product on a frame shifted by O = DOF mod 16 (PSP_RANKM_MFMA == 2):
+// the NT = DOF / 16 full row blocks [O + 16 I, O + 16 I + 16) make NT (NT + 1) / 2
+// tiles with every row inside the triangle (53: 6 tiles instead of 10, whose
+// last row block held 5 rows of 16); the strip of columns < O (rows 0..DOF-1)
+// is a lane-per-row FMA chain with K~ of those columns as uniform values.
+// Within a row block all tiles' loads are issued first, then the MFMAs
+// back to back (independent accumulators), then the stores: the r03 ISA of
+// rankm_mfma ran load -> MFMA -> s_nop 16 -> store per tile, ~1,900 cycles per
+// instance-epoch with its latencies exposed.
+template <int DOF, int M>
+UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
+  static_assert(M <= 3, "rank <= 3 (K = 4 with zero padding)");
+  constexpr int NT = DOF / 16, O = DOF - 16 * NT;
+  static_assert(NT >= 1 && NT <= 4, "frame");
+  static_assert(2 * 16 * M <= PG<DOF>::STG, "operand blocks (PG::STG)");
+  const int q = (l >> 4) & 3, c = l & 15;
+  double Aop[NT], Bop[NT];
+#pragma unroll
+  for (int T = 0; T < NT; T++) {
+    // rows O + 16 T + c: their lanes stage C~ / K~, every lane reads component q
+    const int src = l - O - 16 * T;
+    if (src >= 0 && src < 16) {
+#pragma unroll
+      for (int k = 0; k < M; k++) {
+        stg[src * M + k] = Ct[k];
+        stg[16 * M + src * M + k] = Kt[k];
+      }
+    }
+    wsync();
+    const int qq = q < M ? q : 0;
+    const double a = stg[c * M + qq], b = stg[16 * M + c * M + qq];
+    Aop[T] = q < M ? -a : 0.0;
+    Bop[T] = q < M ? b : 0.0;
+    wsync();  // the next block's writes after every lane's reads
+  }
+  // strip: lane i (row i) updates columns 0 .. min(i, O - 1)
+  if constexpr (O > 0) {
+    double kc[O][M];
+#pragma unroll
+    for (int j = 0; j < O; j++)
+#pragma unroll
+      for (int k = 0; k < M; k++) kc[j][k] = readlane_d(Kt[k], j);
+    if (l < DOF) {
+      const int b0 = (l * (l + 1)) >> 1;
+      double sv[O];
+#pragma unroll
+      for (int j = 0; j < O; j++) sv[j] = S[b0 + (j <= l ? j : 0)];
+#pragma unroll
+      for (int j = 0; j < O; j++) {
+        double s2 = sv[j];
+#pragma unroll
+        for (int k = 0; k < M; k++) s2 = fma(-Ct[k], kc[j][k], s2);
+        if (j <= l) S[b0 + j] = s2;
+      }
+    }
+  }
+  rankm_block<DOF, 0, NT>(S, Aop, Bop, q, c);
+}
+
+// rankm_mfma_o with every tile in flight at once (PSP_RANKM_MFMA == 3): all
+// tiles' loads, all MFMAs, the strip's FMA chains while they run, the stores
+template <int N>
+UWVK_DEV void pin_acc(d4_t (&a)[N]) {
+  if constexpr (N == 1) asm volatile("" : "+v"(a[0]));
+  else if constexpr (N == 3) asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]));
+  else if constexpr (N == 6) asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]));
+  else static_assert(N == 1 || N == 3 || N == 6, "tile count");
+}
+template <int DOF, int M>
+UWVK_DEV void rankm_mfma_all(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
+  static_assert(M <= 3, "rank <= 3 (K = 4 with zero padding)");
+  constexpr int NT = DOF / 16, O = DOF - 16 * NT, NTL = NT * (NT + 1) / 2;
+  static_assert(NT >= 1 && NT <= 3, "frame");
+  static_assert(2 * 16 * M <= PG<DOF>::STG, "operand blocks (PG::STG)");
+  const int q = (l >> 4) & 3, c = l & 15;
+  double Aop[NT], Bop[NT];
+#pragma unroll
+  for (int T = 0; T < NT; T++) {
+    const int src = l - O - 16 * T;
+    if (src >= 0 && src < 16) {
+#pragma unroll
+      for (int k = 0; k < M; k++) {
+        stg[src * M + k] = Ct[k];
+        stg[16 * M + src * M + k] = Kt[k];
+      }
+    }
+    wsync();
+    const int qq = q < M ? q : 0;
+    const double a = stg[c * M + qq], b = stg[16 * M + c * M + qq];
+    Aop[T] = q < M ? -a : 0.0;
+    Bop[T] = q < M ? b : 0.0;
+    wsync();
+  }
+  int base[NT][4];
+#pragma unroll
+  for (int I = 0; I < NT; I++)
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const unsigned R = O + 16 * I + q + 4 * i;
+      base[I][i] = (int)((R * (R + 1)) >> 1) + O + c;
+    }
+  d4_t acc[NTL];
+#pragma unroll
+  for (int I = 0; I < NT; I++)
+#pragma unroll
+    for (int J = 0; J <= I; J++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[I * (I + 1) / 2 + J][i] = S[base[I][i] + 16 * J];
+#pragma unroll
+  for (int I = 0; I < NT; I++)
+#pragma unroll
+    for (int J = 0; J <= I; J++) acc[I * (I + 1) / 2 + J] = mfma_f64(Aop[I], Bop[J], acc[I * (I + 1) / 2 + J]);
+  if constexpr (O > 0) {  // the strip (columns < O) while the MFMAs run
+    double kc[O][M];
+#pragma unroll
+    for (int j = 0; j < O; j++)
+#pragma unroll
+      for (int k = 0; k < M; k++) kc[j][k] = readlane_d(Kt[k], j);
+    if (l < DOF) {
+      const int b0 = (l * (l + 1)) >> 1;
+      double sv[O];
+#pragma unroll
+      for (int j = 0; j < O; j++) sv[j] = S[b0 + (j <= l ? j : 0)];
+#pragma unroll
+      for (int j = 0; j < O; j++) {
+        double s2 = sv[j];
+#pragma unroll
+        for (int k = 0; k < M; k++) s2 = fma(-Ct[k], kc[j][k], s2);
+        if (j <= l) S[b0 + j] = s2;
+      }
+    }
+  }
+  pin_acc<NTL>(acc);
+#pragma unroll
+  for (int I = 0; I < NT; I++)
+#pragma unroll
+    for (int J = 0; J <= I; J++)
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (J < I || c <= q + 4 * i) S[base[I][i] + 16 * J] = acc[I * (I + 1) / 2 + J][i];
+}
+
 // ---------------------------------------------------------------------------
 // ukf::update [EXT], PSP form.  gate: 0 accept any, 1 d2p95.  Returns the gate
 // decision; *ok = false on a non-positive pivot of the partial Cholesky.
@@ -1449,7 +1626,13 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   }
 #if PSP_RANKM_MFMA
   psync();
+#if PSP_RANKM_MFMA == 3
+  if (!(PSP_ABL & 2)) rankm_mfma_all<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
+#elif PSP_RANKM_MFMA == 2
+  if (!(PSP_ABL & 2)) rankm_mfma_o<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
+#else
   if (!(PSP_ABL & 2)) rankm_mfma<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
+#endif
 #elif PSP_FAST & 2048
   {
     // rows [0, P) paired (rankm_pairs), then rows [P, DOF) one per step; the

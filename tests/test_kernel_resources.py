@@ -17,9 +17,17 @@ PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
+def psp_flags():
+    """The PSP translation unit's extra flags, from the Makefile's PSP_FLAGS line."""
+    for line in open(os.path.join(PKG, "Makefile")):
+        if line.startswith("PSP_FLAGS :="):
+            return line.split(":=", 1)[1].split()
+    raise AssertionError("PSP_FLAGS not found in the Makefile")
+
+
 def kernel_usage(src, mangled_prefix, extra=()):
     cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-           "-mllvm", "-disable-machine-licm", *extra, "-c", src, "-o", os.devnull,
+           *psp_flags(), *extra, "-c", src, "-o", os.devnull,
            "-Rpass-analysis=kernel-resource-usage"]
     r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -30,7 +38,7 @@ def kernel_usage(src, mangled_prefix, extra=()):
             cur = m.group(1)
             continue
         if cur and cur.startswith(mangled_prefix):
-            for key, pat in (("vgpr", r"\bVGPRs: (\d+)"), ("scratch", r"ScratchSize \[bytes/lane\]: (\d+)"),
+            for key, pat in (("vgpr", r"\bVGPRs: (\d+)"), ("agpr", r"\bAGPRs: (\d+)"), ("scratch", r"ScratchSize \[bytes/lane\]: (\d+)"),
                              ("occupancy", r"Occupancy \[waves/SIMD\]: (\d+)")):
                 m = re.search(pat, line)
                 if m:
@@ -42,4 +50,5 @@ def kernel_usage(src, mangled_prefix, extra=()):
 def test_psp_epoch_kernel_keeps_three_waves_per_simd():
     u = kernel_usage("csrc/uwvk_psp_k.hip", "_ZN4uwvk3psp11k_psp_epochILi53E")
     assert u, "k_psp_epoch<53> not found in the resource report"
-    assert u["vgpr"] <= 168 and u["scratch"] == 0 and u["occupancy"] >= 3, u
+    # VGPRs and AGPRs share one 512-entry file per SIMD lane: 3 waves need <= 168 together
+    assert u["vgpr"] + u.get("agpr", 0) <= 168 and u["scratch"] == 0 and u["occupancy"] >= 3, u

@@ -19,7 +19,7 @@ PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 def mix(extra=(), dof=53):
     out = "/tmp/psp_hot_%d.s" % os.getpid()
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-                    "-mllvm", "-disable-machine-licm", "-DPSP_HOT_ONLY", *extra, "-S", "-o", out,
+                    "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", "-DPSP_HOT_ONLY", *extra, "-S", "-o", out,
                     os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
     s = open(out).read().split("\n")
     os.unlink(out)

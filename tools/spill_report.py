@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 out = "/tmp/spill_%d.s" % os.getpid()
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-                "-mllvm", "-disable-machine-licm", "-DPSP_HOT_ONLY", "-DPSP_DIAG_HOT=1", *sys.argv[1:], "-S", "-o", out,
+                "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", "-DPSP_HOT_ONLY", "-DPSP_DIAG_HOT=1", *sys.argv[1:], "-S", "-o", out,
                 os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
 s = open(out).read().split("\n")
 os.unlink(out)
