@@ -542,6 +542,7 @@ struct ProcCtx {
   const double* off;  // per-instance offsets (global, uniform address)
   double off_lane;    // PSP: the one offset storage component `lane` decays towards
   double nt_lane;     // PSP: -1/tau of storage component `lane` (0: not a Markov state)
+  double nt_tan;      // PSP: -1/tau of tangent DOF `lane` if it is time-scaled (scaled_dof), else 0
   int vpart;          // PSP: storage index added times dt (pos <- vel, vel <- acc), or -1
 };
 

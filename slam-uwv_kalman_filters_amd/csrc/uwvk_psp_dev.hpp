@@ -69,6 +69,9 @@
 // Delta_j as LDS broadcasts instead of v_readlane (105.9), the same for Dz / P
 // (no change), lds_sums in the manifold-mean loop (+0.7%), s_setprio around
 // the Cholesky column chain (within noise).
+#ifndef PSP_NT_TAN  // r03: A_ll from a per-lane constant set once per launch (ProcCtx::nt_tan), not 8 selects per use
+#define PSP_NT_TAN 1
+#endif
 #ifndef PSP_DIAG_SEL  // per-lane decay factors and water-velocity noise by uniform selects (r02)
 #define PSP_DIAG_SEL 1
 #endif
@@ -539,7 +542,7 @@ UWVK_DEV double proc_diag(int d, const PoseShared& sh, double dt) {
 // index into sh.ntau was a per-lane global load whose s_waitcnt vmcnt(0) also
 // drained the next epoch's IMU prefetch on the predict's critical path
 template <int DOF>
-UWVK_DEV double proc_diag_sel(int d, const PoseShared& sh, double dt) {
+UWVK_DEV double tan_ntau_sel(int d, const PoseShared& sh) {
   using L = Lay<DOF>;
   double nt = 0.0;
   nt = (d >= L::d_bg && d < L::d_bg + 3) ? sh.ntau[0] : nt;
@@ -552,6 +555,11 @@ UWVK_DEV double proc_diag_sel(int d, const PoseShared& sh, double dt) {
   nt = (d >= L::d_wv && d < L::d_wv + 4) ? sh.ntau[5] : nt;
   nt = (d >= L::d_badcp && d < L::d_badcp + 2) ? sh.ntau[6] : nt;
   nt = (d == L::d_rho) ? sh.ntau[7] : nt;
+  return nt;
+}
+template <int DOF>
+UWVK_DEV double proc_diag_sel(int d, const PoseShared& sh, double dt) {
+  const double nt = tan_ntau_sel<DOF>(d, sh);
   const bool markov = scaled_dof(d) && d < DOF;
   return markov ? 1.0 + dt * nt : 1.0;
 }
@@ -750,7 +758,9 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #endif
     const int cp = proc_couple(l);
     const int src = cp >= 0 ? cp : l;
-#if PSP_DIAG_SEL
+#if PSP_NT_TAN
+    const double ar = 1.0 + dt * pc.nt_tan;  // proc_diag_sel's value (nt_tan = 0 off the scaled DOFs)
+#elif PSP_DIAG_SEL
     const double ar = proc_diag_sel<DOF>(l, sh, dt);
 #else
     const double ar = proc_diag<DOF>(l, sh, dt);
@@ -768,7 +778,9 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   double nv[6];
   const int jl = l < DOF ? l : DOF - 1;
   const int jc = proc_couple(jl);
-#if PSP_DIAG_SEL
+#if PSP_NT_TAN
+  const double aj = 1.0 + dt * pc.nt_tan;  // lanes >= DOF: 1 (their values are never stored)
+#elif PSP_DIAG_SEL
   const double aj = proc_diag_sel<DOF>(jl, sh, dt);
 #else
   const double aj = proc_diag<DOF>(jl, sh, dt);
@@ -1225,6 +1237,7 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
   constexpr int NT = DOF / 16, O = DOF - 16 * NT;
   static_assert(NT >= 1 && NT <= 4, "frame");
   static_assert(2 * 16 * M <= PG<DOF>::STG, "operand blocks (PG::STG)");
+  constexpr bool kStripLds = 2 * 16 * M + O * M <= PG<DOF>::STG;  // else readlane (26 DOF: O = 10)
   const int q = (l >> 4) & 3, c = l & 15;
   double Aop[NT], Bop[NT];
 #pragma unroll
@@ -1238,6 +1251,10 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
         stg[16 * M + src * M + k] = Kt[k];
       }
     }
+    if (kStripLds && T == 0 && l < O) {  // K~ of the strip columns, read back as broadcasts
+#pragma unroll
+      for (int k = 0; k < M; k++) stg[32 * M + l * M + k] = Kt[k];
+    }
     wsync();
     const int qq = q < M ? q : 0;
     const double a = stg[c * M + qq], b = stg[16 * M + c * M + qq];
@@ -1245,24 +1262,28 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
     Bop[T] = q < M ? b : 0.0;
     wsync();  // the next block's writes after every lane's reads
   }
-  // strip: lane i (row i) updates columns 0 .. min(i, O - 1)
+  // strip: lane i (row i) updates columns 0 .. min(i, O - 1).  Column j's
+  // address is clamped to the diagonal (min(j, i)) and the columns are stored
+  // in descending order, so a row i < O - 1 rewrites its diagonal with
+  // throw-away values first and the j = i store lands last (LDS stores of one
+  // wave are ordered): no exec-masked store per column
   if constexpr (O > 0) {
     double kc[O][M];
 #pragma unroll
     for (int j = 0; j < O; j++)
 #pragma unroll
-      for (int k = 0; k < M; k++) kc[j][k] = readlane_d(Kt[k], j);
+      for (int k = 0; k < M; k++) kc[j][k] = kStripLds ? stg[32 * M + j * M + k] : readlane_d(Kt[k], j);
     if (l < DOF) {
       const int b0 = (l * (l + 1)) >> 1;
       double sv[O];
 #pragma unroll
-      for (int j = 0; j < O; j++) sv[j] = S[b0 + (j <= l ? j : 0)];
+      for (int j = 0; j < O; j++) sv[j] = S[b0 + (j <= l ? j : l)];
 #pragma unroll
-      for (int j = 0; j < O; j++) {
+      for (int j = O - 1; j >= 0; j--) {
         double s2 = sv[j];
 #pragma unroll
         for (int k = 0; k < M; k++) s2 = fma(-Ct[k], kc[j][k], s2);
-        if (j <= l) S[b0 + j] = s2;
+        S[b0 + (j <= l ? j : l)] = s2;
       }
     }
   }
@@ -1352,6 +1373,17 @@ UWVK_DEV void rankm_mfma_all(double* S, double* stg, const double (&Ct)[M], cons
         if (J < I || c <= q + 4 * i) S[base[I][i] + 16 * J] = acc[I * (I + 1) / 2 + J][i];
 }
 
+// acc + h x for an entry h of a measurement Jacobian: the structural zeros of
+// H (e.g. the identity block of the acceleration model's bias columns) are
+// compile-time constants after inlining, and their terms are dropped.  For
+// finite x the sum is bitwise the same (fma(0, x, acc) == acc); the
+// multiply-by-zero FMAs were issued, since IEEE fma(0, x, acc) is not acc for x
+// inf / NaN.
+UWVK_DEV double hfma(double h, double x, double acc) {
+  if (__builtin_constant_p(h) && h == 0.0) return acc;
+  return acc + h * x;
+}
+
 // ---------------------------------------------------------------------------
 // ukf::update [EXT], PSP form.  gate: 0 accept any, 1 d2p95.  Returns the gate
 // decision; *ok = false on a non-positive pivot of the partial Cholesky.
@@ -1373,7 +1405,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
 #endif
   }
   PSP_PHASE(30);
-  const bool pt = l < 2 * K;
+  [[maybe_unused]] const bool pt = l < 2 * K;  // the non-lds_sums path (PSP_FAST & 256 off)
   double zp[M];
   {
     double x[L::store];
@@ -1506,7 +1538,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     double s = sm.S[pidx(rl, HM::cols[t])];
     if (scaled_dof(HM::cols[t])) s = s * readlane_d(ds, HM::cols[t]);
 #pragma unroll
-    for (int i = 0; i < M; i++) Gr[i] += s * Hs[i][t];
+    for (int i = 0; i < M; i++) Gr[i] = hfma(Hs[i][t], s, Gr[i]);
   }
 #pragma unroll
   for (int i = 0; i < M; i++) Gr[i] = Gr[i] * ds;  // Sigma[r][c] = d_r d_c Sigma~[r][c]
@@ -1581,7 +1613,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     for (int j = 0; j <= i; j++) {
       double hg = 0.0;
 #pragma unroll
-      for (int t = 0; t < NC; t++) hg += Hs[i][t] * readlane_d(Gl[j], HM::cols[t]);
+      for (int t = 0; t < NC; t++) hg = hfma(Hs[i][t], readlane_d(Gl[j], HM::cols[t]), hg);
       const double s = S[i * M + j] + hg;
       S[i * M + j] = s + Rm[i * M + j];
       if (j != i) S[j * M + i] = s + Rm[j * M + i];

@@ -137,6 +137,10 @@ UWVK_DEV void lane_proc(const PoseBufs& b, const PoseShared& sh, int64_t inst, i
   if (s >= L::s_badcp && s < L::s_badcp + 2) pc.nt_lane = sh.ntau[6];
   if (s == L::s_rho) { k = 27; pc.nt_lane = sh.ntau[7]; }
   if (k >= 0) pc.off_lane = b.off[inst * 28 + k];
+  // tangent DOF `s` (the lane): its decay rate when it is time-scaled, so that
+  // A_ll = 1 + dt nt_tan is one FMA per predict (0 keeps A_ll = 1 exactly)
+  pc.nt_tan = 0.0;
+  if (s < DOF && scaled_dof(s)) pc.nt_tan = tan_ntau_sel<DOF>(s, sh);
 }
 
 template <int DOF>

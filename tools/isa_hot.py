@@ -25,7 +25,7 @@ def mix(extra=(), dof=53):
     os.unlink(out)
     name = "_ZN4uwvk3psp11k_psp_epochILi%dEEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % dof
     st = [i for i, l in enumerate(s) if l.startswith(name + ":")][0]
-    en = [i for i, l in enumerate(s) if i > st and l.strip().startswith("s_endpgm")][0]
+    en = [i for i, l in enumerate(s) if i > st and l.startswith(".Lfunc_end")][0]
     body = s[st:en + 1]
     hdr = [l for l in body if "This Loop Header: Depth=1" in l]
     lab = hdr[0].split(":")[0] if hdr else None

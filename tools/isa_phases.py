@@ -22,7 +22,7 @@ subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-
 s = open(out).read().split("\n")
 name = "_ZN4uwvk3psp11k_psp_epochILi%sEEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % dof
 st = [i for i, l in enumerate(s) if l.startswith(name + ":")][0]
-en = [i for i, l in enumerate(s) if i > st and l.strip().startswith("s_endpgm")][0]
+en = [i for i, l in enumerate(s) if i > st and l.startswith(".Lfunc_end")][0]
 INT = re.compile(r"v_(add|sub|subrev|mul_lo|mul_hi|mad|lshl|lshr|ashr|and|or|xor|bfe|bfi|max|min|cvt|mul_u32|"
                  r"lshlrev|lshrrev|ashrrev|not|perm|alignbit|add3|lshl_add|lshl_or|and_or|or3|xad)_")
 segs, cur = [], collections.Counter()

@@ -23,7 +23,7 @@ s = open(out).read().split("\n")
 os.unlink(out)
 name = "_ZN4uwvk3psp11k_psp_epochILi53EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE"
 a = [i for i, l in enumerate(s) if l.startswith(name + ":")][0]
-b = [i for i, l in enumerate(s) if i > a and l.strip().startswith("s_endpgm")][0]
+b = [i for i, l in enumerate(s) if i > a and l.startswith(".Lfunc_end")][0]
 L = s[a:b + 1]
 hdr = [i for i, l in enumerate(L) if "This Loop Header: Depth=1" in l][0]
 lab = L[hdr].split(":")[0]

@@ -64,7 +64,7 @@ def main():
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 8
     L = open(path).read().split("\n")
     st = [i for i, l in enumerate(L) if l.startswith(sym + ":")][0]
-    en = [i for i, l in enumerate(L) if i > st and l.strip().startswith("s_endpgm")][0]
+    en = [i for i, l in enumerate(L) if i > st and l.startswith(".Lfunc_end")][0]
     ins, labels = [], {}
     for i in range(st + 1, en + 1):
         t = L[i].split(";")[0].strip()
