@@ -18,6 +18,13 @@
 #include "uwvk_psp_dev.hpp"
 #include "uwvk_psp.hpp"
 
+#ifndef PSP_PAD_MOV
+#define PSP_PAD_MOV 0
+#endif
+#ifndef PSP_PAD_F64
+#define PSP_PAD_F64 0
+#endif
+
 namespace uwvk {
 namespace psp {
 
@@ -400,6 +407,22 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
     }
     const PoseShared& sh = shared_for_epoch(b);
     UWVK_STAMP(41);
+#if PSP_PAD_MOV > 0 || PSP_PAD_F64 > 0
+    {  // diagnostic (A/B only): N independent VALU instructions per epoch, to
+       // measure what one more 32-bit / fp64 instruction costs the loop
+      double pz[4];
+      int pi[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        pz[i] = (double)(lane_id() + i);
+        pi[i] = lane_id() + i;
+      }
+#pragma unroll
+      for (int i = 0; i < PSP_PAD_MOV; i++) asm volatile("v_mov_b32 %0, %0" : "+v"(pi[i & 3]));
+#pragma unroll
+      for (int i = 0; i < PSP_PAD_F64; i++) asm volatile("v_add_f64 %0, %0, 0" : "+v"(pz[i & 3]));
+    }
+#endif
     if (!PSP_DIAG_HOT && ((e - ea.first) & 1023) == 1023) psp_fold<DOF>(sm, ds, ids);  // keep d in range
     bool sok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, st);
     ok = ok && sok;
