@@ -930,12 +930,27 @@ UWVK_DEV void psp_fold(PspSmem<DOF>& sm, double& ds, double& ids) {
   const int l = olane();
   psync();
   const double dl = l < DOF ? ds : 1.0;
-#pragma unroll 4
-  for (int i = 12; i < DOF; i++) {  // rows < 12 and columns < 12 of them are unscaled
-    const double di = readlane_d(ds, i);
-    if (l <= i) {
-      const int e = i * (i + 1) / 2 + l;
-      sm.S[e] = sm.S[e] * (di * dl);
+  // blocks of FB rows, branch-free: every lane loads (its column clamped to the
+  // diagonal), then stores to its entry or, for l > i, to a throw-away slot of
+  // the staging area (free between epochs): the loads of a block are in flight
+  // together instead of one masked read-modify-write per row (r03)
+  constexpr int R0 = 12, FB = 4;  // rows < 12 and columns < 12 of them are unscaled
+#pragma unroll 1
+  for (int i0 = R0; i0 < DOF; i0 += FB) {
+    double v[FB];
+    int e[FB];
+#pragma unroll
+    for (int r = 0; r < FB; r++) {
+      const int i = i0 + r < DOF ? i0 + r : DOF - 1;
+      e[r] = i * (i + 1) / 2 + (l <= i ? l : i);
+      v[r] = sm.S[e[r]];
+    }
+#pragma unroll
+    for (int r = 0; r < FB; r++) {
+      const int i = i0 + r;
+      const double di = readlane_d(ds, i < DOF ? i : DOF - 1);
+      double* dst = (i < DOF && l <= i) ? sm.S + e[r] : sm.stg + (l & 63);
+      *dst = v[r] * (di * dl);
     }
   }
   psync();
