@@ -6,7 +6,7 @@ used as SGPR spill lanes, and lists the spill slots by the number of reloads
 defined the spilled SGPR before the loop (a kernarg s_load offset names the
 kernel argument) or "loop" when the slot is rewritten inside the loop.
 
-usage: tools/spill_report.py [extra hipcc flags...]"""
+usage: tools/spill_report.py [extra hipcc flags...]   (FULL=1: the shipped build, cold paths included)"""
 import collections
 import os
 import re
@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 out = "/tmp/spill_%d.s" % os.getpid()
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-                "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", "-DPSP_HOT_ONLY", "-DPSP_DIAG_HOT=1", *sys.argv[1:], "-S", "-o", out,
+                "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", *([] if os.environ.get("FULL") == "1" else ["-DPSP_HOT_ONLY", "-DPSP_DIAG_HOT=1"]), *sys.argv[1:], "-S", "-o", out,
                 os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
 s = open(out).read().split("\n")
 os.unlink(out)
