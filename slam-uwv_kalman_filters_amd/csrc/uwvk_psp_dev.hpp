@@ -291,6 +291,9 @@ UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
 // acceleration and gravity keep d = 1.
 UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 
+#ifndef PSP_STAGE_LATE  // r03: the L_a rows staged after the last column step (pchol)
+#define PSP_STAGE_LATE 1
+#endif
 #ifndef PSP_PIV_EARLY
 #define PSP_PIV_EARLY 0  // r03: fewer VALU (-56 per epoch) but 176 VGPRs (2 waves per SIMD), not kept
 #endif
@@ -332,7 +335,9 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
       chk = fma(invn, 0.0, chk);
 #endif
     }
+#if !PSP_STAGE_LATE
     if (q >= 0) rows[q * K + J] = a[J];
+#endif
     if constexpr (J + 1 < K) {
       // col aliases the LAST staged row's not-yet-written slots J+1 .. K-1:
       // only L[c][J] for c > J is read, and that row's own L[.][c] lands in
@@ -378,7 +383,19 @@ UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* s
   const double p0 = readlane_d(a[0], 0);
   const double inv0 = rsqrt_f64(p0);
   double chk = fma(inv0, 0.0, 0.0);
+#if PSP_STAGE_LATE
+  // the column buffer anywhere in the (not yet written) rows area; the rows are
+  // staged after the last step, one lane-addressed run of K stores per row
+  // lane, instead of one masked store (and its address product) per step
+  pchol_step_lds<K, 0>(a, r, ok, stg + STG_ROWS, stg + STG_ROWS, q, p0, inv0, chk);
+  if (q >= 0) {
+    double* rp = stg + STG_ROWS + q * K;
+#pragma unroll
+    for (int J = 0; J < K; J++) rp[J] = a[J];
+  }
+#else
   pchol_step_lds<K, 0>(a, r, ok, stg + STG_ROWS + (RL::NR - 1) * K, stg + STG_ROWS, q, p0, inv0, chk);
+#endif
 #if PSP_PIV_EARLY && (PSP_FAST & 16)
   ok = chk == 0.0;
 #endif
