@@ -231,6 +231,9 @@ UWVK_DEV double sel6(double v0, double v1, double v2, double v3, double v4, doub
   return i < 3 ? sel3(v0, v1, v2, i) : sel3(v3, v4, v5, i - 3);
 }
 
+// pidx(p, j) for a compile-time p and lane-varying j, given Tj = j (j + 1) / 2
+UWVK_DEV int pidx_sel(int p, int j, int Tj) { return j >= p ? Tj + p : p * (p + 1) / 2 + j; }
+
 UWVK_DEV void wsync() {  // LDS ordering point between the lanes of one wave
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -291,6 +294,9 @@ UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
 // acceleration and gravity keep d = 1.
 UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 
+#ifndef PSP_PIDX_SEL  // r03: packed indices of the predict's rows < 12 by pidx_sel
+#define PSP_PIDX_SEL 1
+#endif
 #ifndef PSP_STAGE_LATE  // r03: the L_a rows staged after the last column step (pchol)
 #define PSP_STAGE_LATE 1
 #endif
@@ -802,6 +808,22 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #else
   const double aj = proc_diag<DOF>(jl, sh, dt);
 #endif
+  const int Tl = (jl * (jl + 1)) >> 1;  // (unused without PSP_PIDX_SEL)
+#if PSP_PIDX_SEL
+  // packed (p, j) for a compile-time row p < 12 and a lane column j as a select
+  // between two sums (tri(j) once per lane): pidx's max / min / product per
+  // access were 7 integer instructions; the coupled column is clamped so its
+  // loads need no exec branch (their products are selected away)
+  const int jcc = jc >= 0 ? jc : jl;
+  const int Tc = (jcc * (jcc + 1)) >> 1;
+#pragma unroll
+  for (int q = 0; q < 6; q++) {
+    const int r = pv[q], rc = proc_couple(r);
+    const double t0 = aj * (ds * sm.S[pidx_sel(r, jl, Tl)]) + (jc >= 0 ? dt * sm.S[pidx_sel(r, jcc, Tc)] : 0.0);
+    const double t1 = aj * (ds * sm.S[pidx_sel(rc, jl, Tl)]) + (jc >= 0 ? dt * sm.S[pidx_sel(rc, jcc, Tc)] : 0.0);
+    nv[q] = t0 + dt * t1;  // A_rr = 1 for pos/vel rows
+  }
+#else
 #pragma unroll
   for (int q = 0; q < 6; q++) {
     const int r = pv[q], rc = proc_couple(r);
@@ -809,6 +831,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     const double t1 = aj * (ds * sm.S[pidx(rc, jl)]) + (jc >= 0 ? dt * sm.S[pidx(rc, jc)] : 0.0);
     nv[q] = t0 + dt * t1;  // A_rr = 1 for pos/vel rows
   }
+#endif
   // new time scale d' = A_ll d (A_ll = 1 on the unscaled DOFs)
   if (l < DOF && scaled_dof(l)) {
     ds = aj * ds;
@@ -836,7 +859,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #pragma unroll
       for (int q = 0; q < 6; q++)
         if (!jpv || l <= pv[q]) {
-          const int e = pidx(pv[q], l);
+          const int e = PSP_PIDX_SEL ? pidx_sel(pv[q], l, Tl) : pidx(pv[q], l);  // l < DOF: jl == l
           double qq;
           if constexpr (kQS) qq = (l == pv[q]) ? lq.q0 : 0.0;
           else qq = f2[e].y;
@@ -844,7 +867,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
         }
 #pragma unroll
       for (int i = 0; i < 3; i++) {
-        const int e = pidx(3 + i, l);
+        const int e = PSP_PIDX_SEL ? pidx_sel(3 + i, l, Tl) : pidx(3 + i, l);
         if constexpr (kQS) sm.S[e] = X[i] * ids;
         else sm.S[e] = (X[i] + f2[e].y) * ids;
       }
