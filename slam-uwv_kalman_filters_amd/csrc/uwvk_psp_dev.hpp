@@ -1585,12 +1585,13 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
 #endif
   PSP_PHASE(31);
   const int rl = l < DOF ? l : DOF - 1;
+  const int Trl = (rl * (rl + 1)) >> 1;
   double Gr[M];
 #pragma unroll
   for (int i = 0; i < M; i++) Gr[i] = 0.0;
 #pragma unroll
   for (int t = 0; t < NC; t++) {
-    double s = sm.S[pidx(rl, HM::cols[t])];
+    double s = sm.S[PSP_PIDX_SEL ? pidx_sel(HM::cols[t], rl, Trl) : pidx(rl, HM::cols[t])];
     if (scaled_dof(HM::cols[t])) s = s * readlane_d(ds, HM::cols[t]);
 #pragma unroll
     for (int i = 0; i < M; i++) Gr[i] = hfma(Hs[i][t], s, Gr[i]);
@@ -1799,9 +1800,16 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     }
     // rows 3..5 of every column j outside the block
     if (l < DOF && !(l >= 3 && l < 6)) {
-      const double s0 = sm.S[pidx(3, l)], s1 = sm.S[pidx(4, l)], s2 = sm.S[pidx(5, l)];
+#if PSP_PIDX_SEL
+      const int Tl = (l * (l + 1)) >> 1;
+      const int e0 = pidx_sel(3, l, Tl), e1 = pidx_sel(4, l, Tl), e2 = pidx_sel(5, l, Tl);
+#else
+      const int e0 = pidx(3, l), e1 = pidx(4, l), e2 = pidx(5, l);
+#endif
+      const double s0 = sm.S[e0], s1 = sm.S[e1], s2 = sm.S[e2];
+      const int e[3] = {e0, e1, e2};
 #pragma unroll
-      for (int i = 0; i < 3; i++) sm.S[pidx(3 + i, l)] = R[i * 3] * s0 + R[i * 3 + 1] * s1 + R[i * 3 + 2] * s2;
+      for (int i = 0; i < 3; i++) sm.S[e[i]] = R[i * 3] * s0 + R[i * 3 + 1] * s1 + R[i * 3 + 2] * s2;
     }
     // ori x ori: R B R^T
     double nb = 0.0;
