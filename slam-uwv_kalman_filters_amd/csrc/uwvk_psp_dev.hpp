@@ -297,6 +297,12 @@ UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 #ifndef PSP_PIDX_SEL  // r03: packed indices of the predict's rows < 12 by pidx_sel
 #define PSP_PIDX_SEL 1
 #endif
+#ifndef PSP_ROWS_SEL  // r03 A/B: the predict's rows < 9 and Q-band stores branch-free (throw-away slots)
+#define PSP_ROWS_SEL 0
+#endif
+#ifndef PSP_COL_SEL  // r03: the Cholesky column broadcast stored branch-free (pchol_step_lds)
+#define PSP_COL_SEL 1
+#endif
 #ifndef PSP_STAGE_LATE  // r03: the L_a rows staged after the last column step (pchol)
 #define PSP_STAGE_LATE 1
 #endif
@@ -348,7 +354,14 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
       // col aliases the LAST staged row's not-yet-written slots J+1 .. K-1:
       // only L[c][J] for c > J is read, and that row's own L[.][c] lands in
       // slot c at step c, after this step's reads (one wave: LDS in order)
+#if PSP_STAGE_LATE && PSP_COL_SEL
+      // lanes outside (J, K) store to their own throw-away slot past the column
+      // (the rows area is written only after the last step): no exec-masked branch
+      static_assert(K + 64 <= 115, "throw-away slots (PG::STG)");
+      col[(r > J && r < K) ? r : K + (r & 63)] = a[J];
+#else
       if (r > J && r < K) col[r] = a[J];
+#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -853,6 +866,29 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   // was issued anyway and waited for on the critical path)
   auto rows_lt9 = [&](auto QS) {
     constexpr bool kQS = decltype(QS)::value;
+#if PSP_ROWS_SEL && PSP_PIDX_SEL
+    if constexpr (kQS) {
+      // branch-free: a lane whose entry is not written stores to its own slot
+      // of the staging area (free from the Delta broadcast to the next epoch)
+      const bool lane_ok = l < DOF && !(l >= 3 && l < 6);
+      const bool jpv = jc >= 0;
+      double* const dump = sm.stg + 16 + (l & 63);
+      static_assert(16 + 64 <= PG<DOF>::STG, "throw-away slots (PG::STG)");
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        const int e = pidx_sel(pv[q], jl, Tl);
+        const double qq = (l == pv[q]) ? lq.q0 : 0.0;
+        double* d = (lane_ok && (!jpv || l <= pv[q])) ? sm.S + e : dump;
+        *d = (nv[q] + qq) * ids;
+      }
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        double* d = lane_ok ? sm.S + pidx_sel(3 + i, jl, Tl) : dump;
+        *d = X[i] * ids;
+      }
+      return;
+    }
+#endif
     if (l < DOF && !(l >= 3 && l < 6)) {
       const bool jpv = jc >= 0;
       const double2* f2 = reinterpret_cast<const double2*>(fq);
@@ -904,6 +940,26 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       for (int k = 0; k < 3; k++) {
         if (k > 0) idk = dpp_d<0x138, 0xf, 0xf>(idk);  // wave_shr:1 -> lane l - k
         const int j = l - k;
+#if PSP_ROWS_SEL
+        if constexpr (kQS) {
+          // branch-free read-modify-write: entry (l, j) clamped into the
+          // triangle for the load; a lane without a band entry (or with q == 0)
+          // stores to its own slot of the staging area
+          const bool w = l >= R0 && l < DOF && j >= R0 && k <= bw;
+          const int lc = l < DOF ? l : DOF - 1;
+          const int e = (lc * (lc + 1)) / 2 + (j >= 0 ? (j <= lc ? j : lc) : 0);
+          double q = k == 0 ? lq.q0 : (k == 1 ? lq.q1 : lq.q2);
+          if (k == 0 && l >= L::d_wv && l < L::d_wv + 4) {
+            const int iw = l - L::d_wv;
+            const double qw = iw == 0 ? qw4[0] : (iw == 1 ? qw4[1] : (iw == 2 ? qw4[2] : qw4[3]));
+            q = dt2 * (qw + wv_add);
+          }
+          const double v = sm.S[e] + q * (ids * idk);
+          double* d = (w && q != 0.0) ? sm.S + e : sm.stg + 16 + (l & 63);
+          *d = v;
+          continue;
+        }
+#endif
         if (l >= R0 && l < DOF && j >= R0 && k <= bw) {
           const int e = pidx(l, j);
           double q;
