@@ -436,7 +436,11 @@ def main():
     if dist is not None and world > 1:
         local_st = f.ensemble_stats(log["truth"].state(e0 + a.steps, a.dof))
         host_sum = ensemble.allreduce_stats(local_st, dist)
-        coll_check = bool(np.allclose(host_sum, stats, rtol=1e-12, atol=1e-12))
+        # the two sums add the same per-rank values in different orders: they
+        # agree to world x eps x the sum of the magnitudes (elementwise), which
+        # also covers components whose total nearly cancels
+        mag = ensemble.allreduce_stats(np.abs(local_st), dist)
+        coll_check = bool(np.all(np.abs(host_sum - stats) <= 4.0 * world * np.finfo(np.float64).eps * mag + 1e-300))
         if not coll_check:
             print("error: the all-reduced ensemble statistics differ from the host sum", file=sys.stderr)
     status = f.get_status()
