@@ -602,37 +602,12 @@ UWVK_DEV bool vg_update(double mu[4], double S[16], const double z[M], const dou
 
 constexpr int VG = 16;  // lanes per filter
 
-// The model parameters (164 doubles) staged in LDS once per workgroup and read
-// through an LDS pointer laundered at every RK4 stage, so the stage's reads
-// stay next to their use.  As a by-value kernel argument the compiler kept the
-// uniforms of the whole epoch loop in SGPRs: 370 SGPR spill slots spilled on
-// to scratch (272 B/lane), reloaded inside the loop (r03, VEL_P_LDS).
-#ifndef VEL_P_LDS
-#define VEL_P_LDS 1
-#endif
-using VelSharedLds = __attribute__((address_space(3))) VelShared;
-UWVK_DEV const VelShared& lds_view(VelSharedLds* p) {
-  asm volatile("" : "+v"(p));
-  return *(const VelShared*)p;
-}
-
 __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P, VelEpochArgs ea) {
   const int g = (int)threadIdx.x & (VG - 1);
   const int64_t B = b.batch, inst = (int64_t)blockIdx.x * (64 / VG) + (int)threadIdx.x / VG;
   const bool live = inst < B;
   const int64_t i = live ? inst : B - 1;  // dead groups compute on a copy and store nothing
   const bool pt = g < 9, side = g == 9;
-#if VEL_P_LDS
-  __shared__ VelShared Ps_;
-  {
-    const double* src = reinterpret_cast<const double*>(&P);
-    double* dst = reinterpret_cast<double*>(&Ps_);
-    constexpr int ND = (int)(sizeof(VelShared) / 8);
-    for (int k = (int)threadIdx.x; k < ND; k += 64) dst[k] = src[k];
-    __syncthreads();
-  }
-  VelSharedLds* const Pl = (VelSharedLds*)&Ps_;
-#endif
   double mu[4], S[16], m[13], w[3], tau[6];
   v_load(b, i, mu, S);
 #pragma unroll
@@ -659,11 +634,7 @@ __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P, VelE
 #pragma unroll
       for (int k = 0; k < 3; k++) s13[7 + k] = x[k];
     }
-#if VEL_P_LDS
-    v_rk4(lds_view(Pl), tau, ea.dt, s13, n13);
-#else
     v_rk4(P, tau, ea.dt, s13, n13);
-#endif
     {  // processMotionModel tail (VelocityUKF.cpp:22-32)
       double t[3], r[3];
 #pragma unroll
