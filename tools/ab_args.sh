@@ -12,6 +12,6 @@ for r in $(seq 1 $ROUNDS); do
     n=${spec%%:*}; args=${spec#*:}
     f="$OUT/$n-r$r"
     timeout -k 10 200 python3 bench.py --no-cpu-baseline $args > "$f.json" 2> "$f.err" || { echo "$n failed"; tail -5 "$f.err"; exit 1; }
-    python3 -c "import json; d=json.loads(open('$f.json').read().strip().splitlines()[-1]); t=d['timing']; print('$n', 'r$r', '%.2fM' % (d['value']/1e6), 'kernel %.3f ms' % t['kernel_ms'])"
+    python3 -c "import json; d=json.loads(open('$f.json').read().strip().splitlines()[-1]); t=d.get('timing') or {}; print('$n', 'r$r', '%.2fM' % (d['value']/1e6), 'kernel %s ms' % t.get('kernel_ms'), 'ms_per_step %.5f' % d['ms_per_step'])"
   done
 done
