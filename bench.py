@@ -103,6 +103,9 @@ def parse():
     ap.add_argument("--dense", action="store_true", help="literal kernels (all 2n+1 sigma points)")
     ap.add_argument("--tail-chunks", type=int, default=0,
                     help="UWVK_OPT_TAIL_CHUNKS (diagnostic A/B): force this many chunks per tail instance, 0 = planner")
+    ap.add_argument("--persist", type=int, default=-1,
+                    help="UWVK_OPT_PERSIST: 1 persistent workgroups taking work units from a ticket counter, "
+                         "0 one workgroup per instance, -1 the engine default")
     ap.add_argument("--tail-slots", type=int, default=0,
                     help="UWVK_OPT_TAIL_SLOTS: 0 runtime occupancy, > 0 blocks per XCD, < 0 no tail spreading")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core available to this process")
@@ -362,6 +365,8 @@ def main():
     log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, log_mode, a.dof, first_instance=rank * B, c4_cycle=cyc)
     f = engine.PoseUKFBatch(B, a.dof, device=local)
     f.set_tail_slots(a.tail_slots)
+    if a.persist >= 0:
+        f.set_persist(a.persist)
     if a.tail_chunks:
         f.set_tail_chunks(a.tail_chunks)
     if a.dense:

@@ -418,6 +418,18 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   apply_delta.  1 selects the literal kernels (the PSP kernels are
  *   left-only).  The oracle's or_set_so3_right is the same switch. */
 #define UWVK_OPT_SO3_RIGHT 5
+/* UWVK_OPT_PERSIST: scheduling of the PSP run_log launch.  0 (default): one
+ *   workgroup per instance (plus UWVK_OPT_TAIL_SLOTS spreading, which needs the
+ *   round-robin XCD placement of uwvk_xcd_round_robin; without it the launch
+ *   falls back to the persistent form).  1: persistent workgroups, as many as
+ *   are resident, run their own unit first and then take work units (whole
+ *   instances, then the epoch chunks of the last chunks x resident-slots
+ *   instances) from a ticket counter: faster XCDs and CUs take more units, no
+ *   workgroup dispatch between units, and a chunk's hand-off waits only on a
+ *   unit a running workgroup holds (no placement assumption).  Results are
+ *   bitwise those of 0.  (MI355X, C3 batch 65,536: 0.2-0.5% faster over 200
+ *   epochs, 0.5-0.9% slower over 20) */
+#define UWVK_OPT_PERSIST 6
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
 /* Host-only query (no device work): the chunks per tail instance the
  * UWVK_OPT_TAIL_SLOTS planner picks for one XCD's instances over its resident

@@ -61,6 +61,11 @@ struct uwvk_pose {
   double* d_tail_carry = nullptr;   // per tail instance: 64 x (ds, ids)
   int64_t tail_inst_cap = 0;
   uint32_t tail_tag = 0;
+  // persistent epoch kernel (UWVK_OPT_PERSIST): ticket counter and the value
+  // it holds when the next launch starts (every launch takes units + grid)
+  int persist = 0;
+  uint32_t* d_ticket = nullptr;
+  uint32_t ticket_next = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   aug::VisStage vis;  // visual-landmark update staging
 };
@@ -213,6 +218,7 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
             hipMalloc(&h->d_accepted, B) == hipSuccess && hipMalloc(&h->d_scratch, (B * 3 + 256 + ((B + 63) / 64) * kStatsMaxOut) * 8) == hipSuccess &&
             hipMalloc(&h->d_shared, sizeof(PoseShared)) == hipSuccess &&
             hipMalloc(&h->d_Qp, n * (n + 1) * 8) == hipSuccess && hipMalloc(&h->d_qband, 128 * 8) == hipSuccess &&
+            hipMalloc(&h->d_ticket, 4) == hipSuccess &&
             hipEventCreate(&h->ev0) == hipSuccess && hipEventCreate(&h->ev1) == hipSuccess;
   if (!ok) {
     uwvk_pose_destroy(h);
@@ -221,6 +227,7 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
   (void)hipMemsetAsync(h->d_status, 0, B * 4, h->stream);
   (void)hipMemsetAsync(h->d_rot, 0, B * 3 * 8, h->stream);
   (void)hipMemsetAsync(h->d_Q, 0, n * n * 8, h->stream);
+  (void)hipMemsetAsync(h->d_ticket, 0, 4, h->stream);
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     uwvk_pose_destroy(h);
     return UWVK_EDEVICE;
@@ -236,7 +243,7 @@ void uwvk_pose_destroy(uwvk_pose* h) {
   for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_Q, (void*)h->d_rot, (void*)h->d_off,
                   (void*)h->d_model, (void*)h->d_uwv, (void*)h->d_status, (void*)h->d_meas, (void*)h->d_mask,
                   (void*)h->d_accepted, (void*)h->d_scratch, (void*)h->d_shared, (void*)h->d_Qp, (void*)h->d_qband,
-                  (void*)h->d_tail_flag, (void*)h->d_tail_carry})
+                  (void*)h->d_tail_flag, (void*)h->d_tail_carry, (void*)h->d_ticket})
     if (p) (void)hipFree(p);
   h->vis.release();
   if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -560,26 +567,10 @@ uwvk_status uwvk_pose_get_status(uwvk_pose* h, uint32_t* status, int clear) {
   return UWVK_OK;
 }
 
-// the tail layout of one PSP epoch launch (uwvk_psp_k.hip, plan_tail), cached
-// per (instances per XCD, slots, epochs); fills ea's tail fields and the grid
-static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
-  ea.chunks = 1;
-  grid = 0;
-  if (h->tail_slots < 0 || h->batch % 8 != 0 || !xcd_round_robin(h->device)) return hipSuccess;
-  const int64_t n = h->batch / 8;
-  const int64_t s = h->tail_slots > 0 ? h->tail_slots : psp_epoch_slots_per_xcd(h->dof, h->device);
-  const std::array<int64_t, 3> key{n, s, ea.count};
-  auto it = h->tail_chunks.find(key);
-  if (it == h->tail_chunks.end()) {
-    if (h->tail_chunks.size() >= 64) h->tail_chunks.clear();
-    it = h->tail_chunks.emplace(key, plan_tail(n, s, ea.count)).first;
-  }
-  int c = it->second;
-  if (h->tail_force >= 2)  // forced (tests): every chunk count, where the shape allows it
-    c = (s > 0 && h->tail_force <= 8 && h->tail_force * s <= n && h->tail_force <= ea.count) ? h->tail_force : 1;
-  if (c <= 1) return hipSuccess;
-  const int64_t r = c * s;
-  if (8 * r > h->tail_inst_cap) {  // sized once for the largest plan (8 chunks) of these slots
+// flags and carries for `need` tail instances (sized once for the largest
+// plan: 8 chunks of these slots), and this launch's flag tag
+static hipError_t tail_buffers(uwvk_pose* h, int64_t need, int64_t cap) {
+  if (need > h->tail_inst_cap) {
     // the previous buffers may still be read by a queued launch
     hipError_t e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return e;
@@ -588,7 +579,7 @@ static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
     h->d_tail_flag = nullptr;
     h->d_tail_carry = nullptr;
     h->tail_inst_cap = 0;
-    const int64_t cap = 8 * std::max<int64_t>(r, 8 * s);
+    cap = std::max(cap, need);
     e = hipMalloc(&h->d_tail_flag, (size_t)cap * 4);
     if (e == hipSuccess) e = hipMalloc(&h->d_tail_carry, (size_t)cap * 128 * 8);
     if (e == hipSuccess) e = hipMemsetAsync(h->d_tail_flag, 0, (size_t)cap * 4, h->stream);
@@ -601,6 +592,80 @@ static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
     if (e != hipSuccess) return e;
     h->tail_tag = 1;
   }
+  return hipSuccess;
+}
+
+// chunk count of a launch: the planner's (cached per shape), or the forced one
+static int tail_plan(uwvk_pose* h, int64_t n, int64_t s, int64_t count) {
+  const std::array<int64_t, 3> key{n, s, count};
+  auto it = h->tail_chunks.find(key);
+  if (it == h->tail_chunks.end()) {
+    if (h->tail_chunks.size() >= 64) h->tail_chunks.clear();
+    it = h->tail_chunks.emplace(key, plan_tail(n, s, count)).first;
+  }
+  int c = it->second;
+  if (h->tail_force >= 2)  // forced (tests): every chunk count, where the shape allows it
+    c = (s > 0 && h->tail_force <= 8 && h->tail_force * s <= n && h->tail_force <= count) ? h->tail_force : 1;
+  return c;
+}
+
+// Persistent launch (UWVK_OPT_PERSIST): grid = resident blocks (or fewer
+// units); the last r = chunks x slots instances run as epoch chunks, claimed
+// in chunk order (uwvk_psp_k.hip, k_psp_epoch_p).  UWVK_OPT_TAIL_SLOTS < 0
+// turns the chunks off, > 0 plans for that many slots per XCD.
+static hipError_t prepare_persist(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
+  const int64_t B = h->batch;
+  const int64_t s = h->tail_slots > 0 ? 8 * h->tail_slots : psp_epoch_slots(h->dof, h->device, true);
+  const int64_t slots = psp_epoch_slots(h->dof, h->device, true);
+  if (slots <= 0) return hipErrorInvalidValue;
+  ea.chunks = 1;
+  ea.tail0 = B;
+  ea.r_x = 0;
+  int c = h->tail_slots < 0 || s <= 0 ? 1 : tail_plan(h, B, s, ea.count);
+  if (c > 1) {
+    const int64_t r = c * s;
+    hipError_t e = tail_buffers(h, r, 8 * s);
+    if (e != hipSuccess) return e;
+    ea.tail_flag = h->d_tail_flag;
+    ea.tail_carry = h->d_tail_carry;
+    ea.tail0 = B - r;
+    ea.r_x = r;
+    ea.chunks = c;
+    ea.tag = h->tail_tag;
+    // a chunk waits at most for its predecessor's unit and the unit its block
+    // held before it: ~2 of the launch's epochs per wave, see prepare_tail
+    ea.wait_bound = (uint32_t)std::min<uint64_t>(0xffffffffull, (1ull << 20) + 128ull * (uint64_t)ea.count);
+  }
+  const int64_t units = ea.tail0 + (int64_t)ea.chunks * ea.r_x;
+  grid = std::min<int64_t>(units, slots);
+  ea.units = (uint32_t)units;
+  ea.ticket = h->d_ticket;
+  ea.ticket_base = h->ticket_next;
+  // the first grid units are the blocks' own; the counter then numbers units
+  // grid .. units - 1 and one failing ticket per block: units - grid + grid
+  h->ticket_next += (uint32_t)units;
+  return hipSuccess;
+}
+
+// the tail layout of one PSP epoch launch (uwvk_psp_k.hip, plan_tail), cached
+// per (instances per XCD, slots, epochs); fills ea's tail fields and the grid
+static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
+  ea.chunks = 1;
+  ea.ticket = nullptr;
+  grid = 0;
+  if (h->persist) return prepare_persist(h, ea, grid);
+  if (h->tail_slots < 0 || h->batch % 8 != 0) return hipSuccess;
+  // placement not the round-robin the XCD-ordered tail plan needs (a
+  // partitioned device, another runtime): the ticket-ordered persistent
+  // launch spreads the tail without any placement assumption
+  if (!xcd_round_robin(h->device)) return prepare_persist(h, ea, grid);
+  const int64_t n = h->batch / 8;
+  const int64_t s = h->tail_slots > 0 ? h->tail_slots : psp_epoch_slots_per_xcd(h->dof, h->device);
+  const int c = tail_plan(h, n, s, ea.count);
+  if (c <= 1) return hipSuccess;
+  const int64_t r = c * s;
+  hipError_t e = tail_buffers(h, 8 * r, 8 * std::max<int64_t>(r, 8 * s));
+  if (e != hipSuccess) return e;
   ea.tail_flag = h->d_tail_flag;
   ea.tail_carry = h->d_tail_carry;
   ea.n_x = n;
@@ -730,6 +795,10 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
   if (option == UWVK_OPT_TAIL_CHUNKS) {
     if (value < 0 || value > 8) return UWVK_EINVAL;
     h->tail_force = value;
+    return UWVK_OK;
+  }
+  if (option == UWVK_OPT_PERSIST) {
+    h->persist = value ? 1 : 0;
     return UWVK_OK;
   }
   return UWVK_EINVAL;

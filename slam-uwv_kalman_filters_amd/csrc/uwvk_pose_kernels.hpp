@@ -48,7 +48,7 @@ struct EpochArgs {
   int efforts_only;
   // PSP epoch kernel, last-generation spreading (uwvk_psp_k.hip, plan_tail):
   // chunks <= 1 = one block per instance over [first, first + count).
-  // Otherwise block b runs on XCD x = b & 7 at position i = b >> 3: whole
+  // Otherwise (static k_psp_epoch) block b runs on XCD x = b & 7 at position i = b >> 3: whole
   // instance x n_x + i for i < tail0, else chunk k = (i - tail0) / r_x of tail
   // instance x n_x + tail0 + (i - tail0) % r_x, handed on through tail_flag /
   // tail_carry
@@ -60,6 +60,14 @@ struct EpochArgs {
   int chunks;
   uint32_t tag;         // per launch
   uint32_t wait_bound;  // tail_wait: sleeps before a hand-off counts as lost
+  // persistent PSP epoch kernel (UWVK_OPT_PERSIST, k_psp_epoch_p): block b
+  // runs unit b first, then takes units from a ticket counter, unit
+  // gridDim.x + (*ticket - ticket_base) before the atomic; units [0, tail0)
+  // whole instances, then chunk k of tail
+  // instance tail0 + t at unit tail0 + k r_x + t (r_x tail instances)
+  uint32_t* ticket;
+  uint32_t ticket_base;
+  uint32_t units;       // tail0 + chunks * r_x
 };
 
 // host-callable launchers (grid = one workgroup per instance)

@@ -12,6 +12,9 @@ hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const Po
                             int64_t grid = 0);
 // resident k_psp_epoch blocks per XCD (occupancy x CUs / 8), 0 if unknown
 int64_t psp_epoch_slots_per_xcd(int dof, int device);
+// resident blocks of the static (k_psp_epoch) or persistent (k_psp_epoch_p)
+// epoch kernel on the device (occupancy x CUs), 0 if unknown
+int64_t psp_epoch_slots(int dof, int device, bool persist);
 // chunks per tail instance for one XCD's n instances over s resident blocks in
 // a count-epoch launch (1: no tail spreading)
 int plan_tail(int64_t n, int64_t s, int64_t count);

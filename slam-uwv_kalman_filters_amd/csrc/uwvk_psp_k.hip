@@ -75,7 +75,8 @@ UWVK_DEV TailUnit tail_unit(const EpochArgs& ea, int64_t B) {
 // predecessor; every later chunk of the instance then times out the same way.
 // (scalar arguments: with the EpochArgs reference the caller kept a copy of
 // the kernel arguments in scratch, 150 -> 173 VGPRs and 800 B/lane)
-__device__ __attribute__((noinline)) bool tail_wait(uint32_t* f, uint32_t want, uint32_t bound) {
+template <bool INL>
+UWVK_DEV bool tail_wait_t(uint32_t* f, uint32_t want, uint32_t bound) {
   uint32_t n = 0;
   if (lane_id() == 0) {
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want && ++n < bound)
@@ -85,6 +86,9 @@ __device__ __attribute__((noinline)) bool tail_wait(uint32_t* f, uint32_t want, 
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous chunk's stores, from any CU
   return n < bound;
+}
+__device__ __attribute__((noinline)) bool tail_wait(uint32_t* f, uint32_t want, uint32_t bound) {
+  return tail_wait_t<false>(f, want, bound);
 }
 __device__ __attribute__((noinline)) double2 tail_carry_in(const EpochArgs& ea, int64_t t) {
   return reinterpret_cast<const double2*>(ea.tail_carry)[t * 64 + lane_id()];
@@ -102,9 +106,8 @@ UWVK_DEV void tail_signal(const EpochArgs& ea, int64_t t, int chunk) {
 #endif
 
 template <int DOF>
-UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
+UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst, int l = lane_id()) {
   using G = PG<DOF>;
-  const int l = lane_id();
   const double* gs = b.sigma + inst * (int64_t)G::NP;  // packed in HBM as in LDS: one coalesced copy
   double v[G::NSLOT];
 #pragma unroll
@@ -151,9 +154,8 @@ UWVK_DEV void lane_proc(const PoseBufs& b, const PoseShared& sh, int64_t inst, i
 }
 
 template <int DOF>
-UWVK_DEV void store_psp(const PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst) {
+UWVK_DEV void store_psp(const PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst, int l = lane_id()) {
   using G = PG<DOF>;
-  const int l = lane_id();
   double* gs = b.sigma + inst * (int64_t)G::NP;
 #pragma unroll 4
   for (int t = 0; t < G::NSLOT; t++) {
@@ -301,17 +303,39 @@ UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
 #else
 #define PSP_EPOCH_ATTR
 #endif
-template <int DOF>
-__global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
-  __shared__ PspSmem<DOF> sm;
-  const int64_t B = b.batch;
-  TailUnit tu = tail_unit(ea, B);
-  const int64_t inst = tu.inst, e_begin = tu.e0, e_end = tu.e1;
-  if (tu.chunk > 0 && !tail_wait(ea.tail_flag + tu.tslot, ea.tag * 16u + (uint32_t)tu.chunk, ea.wait_bound)) {
-    if (lane_id() == 0)  // atomic: the late predecessor may still flag the same word
-      __hip_atomic_fetch_or(b.status + inst, UWVK_ST_SCHEDULE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
+UWVK_DEV TailUnit ticket_unit(const EpochArgs& ea, uint32_t u) {
+  TailUnit t{(int64_t)u, ea.first, ea.first + ea.count, 0, -1};
+  if (ea.chunks > 1 && (int64_t)u >= ea.tail0) {
+    const uint32_t q = u - (uint32_t)ea.tail0, m = (uint32_t)ea.r_x;
+    const uint32_t k = q / m, r = q - k * m;
+    t.inst = ea.tail0 + r;
+    t.chunk = (int)k;
+    t.tslot = r;
+    t.e0 = ea.first + ea.count * k / ea.chunks;
+    t.e1 = ea.first + ea.count * (k + 1) / ea.chunks;
   }
+  return t;
+}
+UWVK_DEV uint32_t ticket_issue(const EpochArgs& ea) {  // lane 0's atomic; the value is read by ticket_value
+  uint32_t v = 0;
+  if (lane_id() == 0) v = __hip_atomic_fetch_add(ea.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+UWVK_DEV uint32_t ticket_value(const EpochArgs& ea, uint32_t v) {
+  return __builtin_amdgcn_readfirstlane(v) - ea.ticket_base;
+}
+
+// One work unit of the epoch kernel: instance tu.inst over epochs
+// [tu.e0, tu.e1), Sigma~ loaded from HBM into LDS, every epoch run, stored
+// back (folded, or unfolded for the next chunk of a tail instance).  `again`
+// re-derives the unit at the end (from the block index or the uniform ticket),
+// so that the unit is not kept live through the epochs.  tlw: the timeline
+// key of the diagnostic build.
+template <int DOF, bool PERSIST, class Again>
+UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea, const TailUnit& tu0,
+                       const LaneQ& lq, Again again, int64_t tlw, int lp, uint32_t* next = nullptr) {
+  const int64_t B = b.batch;
+  const int64_t inst = tu0.inst, e_begin = tu0.e0, e_end = tu0.e1;
 #ifdef UWVK_STAMPS
   Stamper stamper;
   Stamper* st = &stamper;
@@ -319,26 +343,28 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
   Stamper* st = nullptr;
 #endif
 #ifdef UWVK_TIMELINE
-  tl_mark(blockIdx.x, 0);
-  if (lane_id() == 0 && blockIdx.x < 131072) {
+  tl_mark(tlw, 0);
+  if (lane_id() == 0 && tlw < 131072) {
     unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    uwvk_timeline[blockIdx.x * 8 + 4] = ((unsigned long long)xcc << 32) | (unsigned)__smid();
-    uwvk_timeline[blockIdx.x * 8 + 5] = (unsigned long long)inst;
+    uwvk_timeline[tlw * 8 + 4] = ((unsigned long long)xcc << 32) | (unsigned)__smid();
+    uwvk_timeline[tlw * 8 + 5] = (unsigned long long)inst;
   }
+#else
+  (void)tlw;
 #endif
-  load_psp<DOF>(sm, b, inst);
+  load_psp<DOF>(sm, b, inst, PERSIST ? olane() : lane_id());
 #ifdef UWVK_TIMELINE
-  tl_mark(blockIdx.x, 1);
+  tl_mark(tlw, 1);
 #endif
   UWVK_STAMP(40);
   double ds = 1.0, ids = 1.0;  // time scale of the Markov DOFs (Sigma = D Sigma~ D)
-  if (tu.chunk > 0) {  // the previous chunk's, unfolded: bitwise the one-block run
-    const double2 c = tail_carry_in(ea, tu.tslot);
+  if (tu0.chunk > 0) {  // the previous chunk's, unfolded: bitwise the one-block run
+    const double2 c = PERSIST ? reinterpret_cast<const double2*>(ea.tail_carry)[tu0.tslot * 64 + lane_id()]
+                              : tail_carry_in(ea, tu0.tslot);
     ds = c.x;
     ids = c.y;
   }
-  const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
   bool ok = true, nan = false;
   uint32_t cnt[4] = {0, 0, 0, 0};
   MeasArgs ma{};
@@ -364,7 +390,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
   pc.dt = ea.dt;
 #endif
   pc.off = nullptr;
-  lane_proc<DOF>(b, *b.shared, inst, lane_id(), pc);
+  lane_proc<DOF>(b, *b.shared, inst, lp, pc);
   // the next epoch's IMU inputs are prefetched one epoch ahead (their load
   // latency overlaps this epoch's arithmetic)
   uint32_t fl_n = 0;
@@ -386,6 +412,10 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
     }
   };
   if (e_end > e_begin) fetch(e_begin);
+  // persistent: the next unit's ticket, claimed behind the first inputs' loads
+  // (a wait for those does not wait for the atomic; it has long returned when
+  // the next epoch's loads are waited for)
+  if constexpr (PERSIST) *next = ticket_issue(ea);
 #pragma unroll 1
   for (int64_t e = e_begin; e < e_end; e++) {
 #if PSP_FLAG_VGPR
@@ -480,9 +510,9 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
       for (int k = 0; k < 4; k++) ea.accept_counts[inst * 4 + k] += cnt[k];
   }
 #ifdef UWVK_TIMELINE
-  tl_mark(blockIdx.x, 2);
+  tl_mark(tlw, 2);
 #endif
-  tu = tail_unit(ea, B);  // re-read, not kept live through the epochs
+  const TailUnit tu = again();  // re-derived, not kept live through the epochs
   const bool hand = tu.chunk >= 0 && tu.chunk + 1 < ea.chunks;
   if (hand) {  // hand on: Sigma~ and d unfolded
     double* c = ea.tail_carry + (tu.tslot * 64 + lane_id()) * 2;
@@ -492,12 +522,60 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
   } else {
     psp_fold<DOF>(sm, ds, ids);
   }
-  store_psp<DOF>(sm, b, inst);
+  store_psp<DOF>(sm, b, inst, PERSIST ? olane() : lane_id());
   if (hand) tail_signal(ea, tu.tslot, tu.chunk);
 #ifdef UWVK_TIMELINE
   __builtin_amdgcn_s_waitcnt(0);
-  tl_mark(blockIdx.x, 3);
+  tl_mark(tlw, 3);
 #endif
+}
+
+template <int DOF>
+__global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
+  __shared__ PspSmem<DOF> sm;
+  const int64_t B = b.batch;
+  const TailUnit tu = tail_unit(ea, B);
+  if (tu.chunk > 0 && !tail_wait(ea.tail_flag + tu.tslot, ea.tag * 16u + (uint32_t)tu.chunk, ea.wait_bound)) {
+    if (lane_id() == 0)  // atomic: the late predecessor may still flag the same word
+      __hip_atomic_fetch_or(b.status + tu.inst, UWVK_ST_SCHEDULE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
+  psp_unit<DOF, false>(sm, b, ea, tu, lq, [&] { return tail_unit(ea, B); }, blockIdx.x, lane_id());
+}
+
+// Persistent form (UWVK_OPT_PERSIST): as many blocks as are resident, each
+// taking work units from the launch's ticket counter until none is left.  A
+// unit is claimed only by a running block, and chunk k of a tail instance is
+// claimed after chunk k - 1 (r_x tickets earlier), so a hand-off wait is always
+// on a unit that a resident block holds or has finished: no placement or
+// dispatch-order assumption.  Faster XCDs / CUs take more units, and a slot
+// moves to its next unit without a new workgroup dispatch.  The next ticket is
+// taken while the current unit runs (its atomic latency hidden).
+template <int DOF>
+__global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, PoseShared sh0, EpochArgs ea) {
+  __shared__ PspSmem<DOF> sm;
+  const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
+  // the first unit is the block's own index (no atomic: 3,072 blocks claiming
+  // one counter at once queue for ~50 us); tickets number the units from the grid on
+  const uint32_t grid = gridDim.x;
+  uint32_t u = blockIdx.x;
+#pragma unroll 1
+  while (u < ea.units) {
+    const TailUnit tu = ticket_unit(ea, u);
+    uint32_t vn = 0;
+    if (tu.chunk > 0 && !tail_wait_t<true>(ea.tail_flag + tu.tslot, ea.tag * 16u + (uint32_t)tu.chunk, ea.wait_bound)) {
+      if (lane_id() == 0)
+        __hip_atomic_fetch_or(b.status + tu.inst, UWVK_ST_SCHEDULE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      vn = ticket_issue(ea);
+    } else {
+      // a laundered lane id: the unit's per-lane constants are recomputed per
+      // unit, not hoisted out of the unit loop (held live across it)
+      psp_unit<DOF, true>(sm, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(), &vn);
+    }
+    u = grid + ticket_value(ea, vn);
+    psync();  // the next unit's LDS writes after this unit's reads
+  }
 }
 
 }  // namespace psp
@@ -536,10 +614,16 @@ hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& 
 hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
                             int64_t grid) {
   const dim3 g((unsigned)(grid > 0 ? grid : b.batch));
-  if (dof == 53)
+  if (ea.ticket) {
+    if (dof == 53)
+      hipLaunchKernelGGL(psp::k_psp_epoch_p<53>, g, dim3(64), 0, st, b, sh, ea);
+    else
+      hipLaunchKernelGGL(psp::k_psp_epoch_p<26>, g, dim3(64), 0, st, b, sh, ea);
+  } else if (dof == 53) {
     hipLaunchKernelGGL(psp::k_psp_epoch<53>, g, dim3(64), 0, st, b, sh, ea);
-  else
+  } else {
     hipLaunchKernelGGL(psp::k_psp_epoch<26>, g, dim3(64), 0, st, b, sh, ea);
+  }
   return hipGetLastError();
 }
 
@@ -589,13 +673,16 @@ int xcd_round_robin(int device) {
   return ok;
 }
 
-int64_t psp_epoch_slots_per_xcd(int dof, int device) {
+int64_t psp_epoch_slots_per_xcd(int dof, int device) { return psp_epoch_slots(dof, device, false) / 8; }
+
+int64_t psp_epoch_slots(int dof, int device, bool persist) {
   int per_cu = 0, cus = 0;
-  const void* k = dof == 53 ? (const void*)psp::k_psp_epoch<53> : (const void*)psp::k_psp_epoch<26>;
+  const void* k = persist ? (dof == 53 ? (const void*)psp::k_psp_epoch_p<53> : (const void*)psp::k_psp_epoch_p<26>)
+                          : (dof == 53 ? (const void*)psp::k_psp_epoch<53> : (const void*)psp::k_psp_epoch<26>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return 0;
-  return (int64_t)per_cu * cus / 8;
+  return (int64_t)per_cu * cus;
 }
 
 // Last-generation spreading.  Blocks of one XCD are dispatched in order to

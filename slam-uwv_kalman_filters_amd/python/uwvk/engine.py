@@ -177,6 +177,11 @@ class PoseUKFBatch:
         """UWVK_OPT_TAIL_CHUNKS: 0 the planner's chunk count, 2..8 forced (tests)."""
         _chk(self.L.uwvk_pose_set_option(self.h, 4, int(chunks)), "set_option")
 
+    def set_persist(self, on=True):
+        """UWVK_OPT_PERSIST: run_log on resident workgroups that take work units
+        from a ticket counter (bitwise the same results as one workgroup per instance)."""
+        _chk(self.L.uwvk_pose_set_option(self.h, 6, int(bool(on))), "set_option")
+
     def set_literal_apply_delta(self, on=True):
         """ukfom's literal apply_delta re-spread instead of the exact T Sigma T^T form."""
         _chk(self.L.uwvk_pose_set_option(self.h, 1, int(bool(on))), "set_option")

@@ -24,9 +24,12 @@ def eng():
     return engine
 
 
-def _run(eng, B, dof, log, cfg, uwv, slots, pieces):
+def _run(eng, B, dof, log, cfg, uwv, slots, pieces, persist=False, force=0):
     g = eng.PoseUKFBatch(B, dof)
     g.set_tail_slots(slots)
+    g.set_persist(persist)
+    if force:
+        g.set_tail_chunks(force)
     g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
     g.set_process_noise_from_config(cfg, 1e-3)
     dlog = g.upload_log(log)
@@ -119,3 +122,48 @@ def test_every_chunk_count_at_full_batch(eng, B):
     for g, _, _ in hs:
         assert not g.get_status().any()
     np.testing.assert_array_equal(hs[1][2].read(np.uint32, (B, 4)), hs[0][2].read(np.uint32, (B, 4)))
+
+
+# Persistent scheduling (UWVK_OPT_PERSIST): resident workgroups take units from
+# a ticket counter; chunk k of a tail instance may run on any XCD after chunk
+# k - 1.  Bitwise the one-workgroup-per-instance run, with and without chunks,
+# on every chunk count the planner can be forced to.
+@pytest.mark.parametrize("dof,mode,E,slots,n,pieces", CASES)
+def test_persist_bitwise(eng, dof, mode, E, slots, n, pieces):
+    from uwvk import synth
+    B = 8 * n
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    extra = dict(dropout_on=0.1, dropout_off=0.05) if mode == "C4" else {}
+    log = synth.make_pose_log(B, E, mode, dof=dof, **extra)
+    ref = _run(eng, B, dof, log, cfg, uwv, -1, pieces)
+    names = ("state", "covariance", "accept counts", "status", "rotation rate")
+    for sl in (-1, slots):  # no chunks; the planner's chunks for `slots` per XCD
+        got = _run(eng, B, dof, log, cfg, uwv, sl, pieces, persist=True)
+        for name, a, b in zip(names, got, ref):
+            np.testing.assert_array_equal(a, b, err_msg="%s (slots %d)" % (name, sl))
+
+
+@pytest.mark.parametrize("chunks", [2, 3, 5, 8])
+def test_persist_forced_chunks(eng, chunks):
+    from uwvk import synth
+    B, E = 48, 40
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(B, E, "C3")
+    ref = _run(eng, B, 53, log, cfg, uwv, -1, [(0, 17), (17, 23)])
+    got = _run(eng, B, 53, log, cfg, uwv, 1, [(0, 17), (17, 23)], persist=True, force=chunks)
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)
+    assert not got[3].any()
+
+
+def test_persist_default_plan_repeat(eng):
+    """The runtime-occupancy plan at C5's shard size plus a partial generation,
+    two launches (the ticket base carried between them)."""
+    from uwvk import synth
+    B, E = 8 * (8192 + 64), 60
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(B, E, "C3")
+    ref = _run(eng, B, 53, log, cfg, uwv, -1, [(0, 30), (30, 30)])
+    got = _run(eng, B, 53, log, cfg, uwv, 0, [(0, 30), (30, 30)], persist=True)
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)

@@ -22,12 +22,14 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--out", default="")
     ap.add_argument("--tail-slots", type=int, default=0)
+    ap.add_argument("--persist", type=int, default=0, help="UWVK_OPT_PERSIST (records are then per work unit)")
     a = ap.parse_args()
     B, E = a.batch, a.steps
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     log = synth.make_pose_log(B, E + 5, "C3")
     f = engine.PoseUKFBatch(B)
     f.set_tail_slots(a.tail_slots)
+    f.set_persist(a.persist)
     L0 = engine.lib()
     s_x = L0.uwvk_pose_resident_slots(53, 0)
     ch = L0.uwvk_pose_tail_chunks(B // 8, a.tail_slots or s_x, E) if a.tail_slots >= 0 else 1
