@@ -331,9 +331,23 @@ UWVK_DEV uint32_t ticket_value(const EpochArgs& ea, uint32_t v) {
 // re-derives the unit at the end (from the block index or the uniform ticket),
 // so that the unit is not kept live through the epochs.  tlw: the timeline
 // key of the diagnostic build.
+// the next unit's Sigma~ and mean, loaded into registers before this unit's
+// stores (persistent kernel): gfx950's vmcnt counts loads and stores in one
+// ordered counter, so a load issued after the stores waits for them as well
+#ifndef PSP_PREFETCH
+#define PSP_PREFETCH 1
+#endif
+template <int DOF>
+struct PspPre {
+  double v[PG<DOF>::NSLOT];
+  double m;
+  bool have;
+};
+
 template <int DOF, bool PERSIST, class Again>
 UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea, const TailUnit& tu0,
-                       const LaneQ& lq, Again again, int64_t tlw, int lp, uint32_t* next = nullptr) {
+                       const LaneQ& lq, Again again, int64_t tlw, int lp, uint32_t* next = nullptr,
+                       PspPre<DOF>* pre = nullptr) {
   const int64_t B = b.batch;
   const int64_t inst = tu0.inst, e_begin = tu0.e0, e_end = tu0.e1;
 #ifdef UWVK_STAMPS
@@ -353,7 +367,19 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
 #else
   (void)tlw;
 #endif
-  load_psp<DOF>(sm, b, inst, PERSIST ? olane() : lane_id());
+  if (PERSIST && PSP_PREFETCH && pre->have) {
+    using G = PG<DOF>;
+    const int l = olane();
+#pragma unroll
+    for (int t = 0; t < G::NSLOT; t++) {
+      const int e = l + 64 * t;
+      if (e < G::NP) sm.S[e] = pre->v[t];
+    }
+    if (l < Lay<DOF>::store) sm.mu[l] = pre->m;
+    psync();
+  } else {
+    load_psp<DOF>(sm, b, inst, PERSIST ? olane() : lane_id());
+  }
 #ifdef UWVK_TIMELINE
   tl_mark(tlw, 1);
 #endif
@@ -499,6 +525,26 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     }
 #endif
   }
+  if constexpr (PERSIST) {
+    // the next unit (its ticket has long returned); a whole instance or a
+    // first chunk has no predecessor to wait for, so its Sigma~ and mean are
+    // loaded now, ahead of this unit's stores
+    const uint32_t un = gridDim.x + ticket_value(ea, *next);
+    *next = un;
+    const TailUnit tn = ticket_unit(ea, un < ea.units ? un : 0u);
+    pre->have = PSP_PREFETCH && un < ea.units && tn.chunk <= 0;
+    // every path defines the registers here (zeros when nothing is
+    // prefetched), so they are dead through the next unit's epochs
+    using G = PG<DOF>;
+    const int l = olane();
+    const double* gs = b.sigma + (pre->have ? tn.inst : 0) * (int64_t)G::NP;
+#pragma unroll
+    for (int t = 0; t < G::NSLOT; t++) {
+      const int e = l + 64 * t;
+      pre->v[t] = (pre->have && e < G::NP) ? gs[e] : 0.0;
+    }
+    pre->m = (pre->have && l < Lay<DOF>::store) ? b.mu[(pre->have ? tn.inst : 0) * Lay<DOF>::store + l] : 0.0;
+  }
   if (lane_id() == 0) {
     // atomic: a later chunk that timed out flags the same word
     const uint32_t bits = (ok ? 0u : UWVK_ST_NOTPD) | (nan ? UWVK_ST_NAN : 0u);
@@ -560,6 +606,11 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, P
   // one counter at once queue for ~50 us); tickets number the units from the grid on
   const uint32_t grid = gridDim.x;
   uint32_t u = blockIdx.x;
+  PspPre<DOF> pre;
+  pre.have = false;
+#pragma unroll
+  for (int t = 0; t < PG<DOF>::NSLOT; t++) pre.v[t] = 0.0;
+  pre.m = 0.0;
 #pragma unroll 1
   while (u < ea.units) {
     const TailUnit tu = ticket_unit(ea, u);
@@ -567,13 +618,17 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, P
     if (tu.chunk > 0 && !tail_wait_t<true>(ea.tail_flag + tu.tslot, ea.tag * 16u + (uint32_t)tu.chunk, ea.wait_bound)) {
       if (lane_id() == 0)
         __hip_atomic_fetch_or(b.status + tu.inst, UWVK_ST_SCHEDULE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      vn = ticket_issue(ea);
+      u = grid + ticket_value(ea, ticket_issue(ea));
+      pre.have = false;
+#pragma unroll
+      for (int t = 0; t < PG<DOF>::NSLOT; t++) pre.v[t] = 0.0;
+      pre.m = 0.0;
     } else {
       // a laundered lane id: the unit's per-lane constants are recomputed per
       // unit, not hoisted out of the unit loop (held live across it)
-      psp_unit<DOF, true>(sm, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(), &vn);
+      psp_unit<DOF, true>(sm, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(), &vn, &pre);
+      u = vn;  // resolved by psp_unit
     }
-    u = grid + ticket_value(ea, vn);
     psync();  // the next unit's LDS writes after this unit's reads
   }
 }
