@@ -439,6 +439,11 @@ int uwvk_pose_tail_chunks(int64_t instances_per_xcd, int64_t slots_per_xcd, int6
  * device (occupancy x CUs / 8; what UWVK_OPT_TAIL_SLOTS = 0 plans for), 0 if
  * unknown. */
 int64_t uwvk_pose_resident_slots(int dof, int device);
+/* Host-only query: the process-noise shape the PSP epoch kernel is
+ * instantiated for on this handle's current Q: 1 = the lane-resident simple
+ * shape (no coupling of the rewritten rows < 9, band <= 2; the default
+ * configuration's), 2 = general (psp_predict QM). */
+int uwvk_pose_epoch_qshape(const uwvk_pose* h);
 /* 1 when a probe grid on device showed round-robin workgroup placement over 8
  * XCCs (block b on the XCC of block b % 8, read from the hardware XCC_ID
  * register): the placement tail spreading's hand-off order relies on.  0 on a

@@ -819,6 +819,8 @@ int64_t uwvk_pose_resident_slots(int dof, int device) {
 
 int uwvk_xcd_round_robin(int device) { return xcd_round_robin(device); }
 
+int uwvk_pose_epoch_qshape(const uwvk_pose* h) { return h ? (h->sh.q_simple ? 1 : 2) : 0; }
+
 int uwvk_pose_tail_chunks(int64_t instances_per_xcd, int64_t slots_per_xcd, int64_t epochs) {
   return plan_tail(instances_per_xcd, slots_per_xcd, epochs);
 }

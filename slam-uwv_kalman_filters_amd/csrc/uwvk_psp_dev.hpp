@@ -631,7 +631,11 @@ UWVK_DEV LaneQ lane_q(const double* fq, int l) {
 
 // Q: process_noise_cov (DOF x DOF); fq: per packed entry {., dt^2 Q_ij} (host-made per dt)
 // ds, ids: this lane's time scale d_l and 1/d_l (updated: d' = A_ll d)
-template <int DOF>
+// QM: the process-noise shape, 0 read from sh at run time, 1 known simple
+// (sh.q_simple: lane-resident band <= 2), 2 known general.  The epoch kernel is
+// instantiated for 1 and 2 and the host picks one: with both branches in one
+// kernel the epoch loop ran 0.7-0.8% slower (profiles/r03/qm/).
+template <int DOF, int QM = 0>
 UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q,
                           const double* fq, double& ds, double& ids, const LaneQ& lq,
                           Stamper* st = nullptr) {
@@ -860,7 +864,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   PSP_PHASE(24);
   // rewrite rows/cols < 9 (stored as Sigma / d'_l): A-coupled rows (pos, vel),
   // orientation rows (cross terms), ori x ori
-  const bool qs = sh.q_simple != 0;
+  const bool qs = QM == 1 ? true : (QM == 2 ? false : sh.q_simple != 0);
   // the lane-resident Q (qs, a uniform branch) needs no global load: the
   // dt^2 Q table is read only for a general Q (a load under a per-lane select
   // was issued anyway and waited for on the critical path)
@@ -996,7 +1000,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       }
     }
 #endif
-    for (int k = 3; k <= (PSP_DIAG_HOT ? 0 : bw); k++) {  // uniform bound: wide Q bands only
+    for (int k = 3; k <= ((PSP_DIAG_HOT || QM == 1) ? 0 : bw); k++) {  // uniform bound: wide Q bands only
       const double idj = shfl_d(ids, l - k >= 0 ? l - k : 0);
       const int j = l - k;
       if (l >= R0 && l < DOF && j >= R0) {

@@ -344,7 +344,7 @@ struct PspPre {
   bool have;
 };
 
-template <int DOF, bool PERSIST, class Again>
+template <int DOF, bool PERSIST, int QM, class Again>
 UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea, const TailUnit& tu0,
                        const LaneQ& lq, Again again, int64_t tlw, int lp, uint32_t* next = nullptr,
                        PspPre<DOF>* pre = nullptr) {
@@ -480,7 +480,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     }
 #endif
     if (!PSP_DIAG_HOT && ((e - ea.first) & 1023) == 1023) psp_fold<DOF>(sm, ds, ids);  // keep d in range
-    bool sok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, st);
+    bool sok = psp_predict<DOF, QM>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, st);
     ok = ok && sok;
 #if PSP_FETCH_LATE  // the next epoch's inputs issued after the predict: a shorter live range
     if (e + 1 < e_end) fetch(e + 1);
@@ -576,7 +576,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
 #endif
 }
 
-template <int DOF>
+template <int DOF, int QM>
 __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const int64_t B = b.batch;
@@ -587,7 +587,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
     return;
   }
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
-  psp_unit<DOF, false>(sm, b, ea, tu, lq, [&] { return tail_unit(ea, B); }, blockIdx.x, lane_id());
+  psp_unit<DOF, false, QM>(sm, b, ea, tu, lq, [&] { return tail_unit(ea, B); }, blockIdx.x, lane_id());
 }
 
 // Persistent form (UWVK_OPT_PERSIST): as many blocks as are resident, each
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
 // dispatch-order assumption.  Faster XCDs / CUs take more units, and a slot
 // moves to its next unit without a new workgroup dispatch.  The next ticket is
 // taken while the current unit runs (its atomic latency hidden).
-template <int DOF>
+template <int DOF, int QM>
 __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
@@ -626,7 +626,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, P
     } else {
       // a laundered lane id: the unit's per-lane constants are recomputed per
       // unit, not hoisted out of the unit loop (held live across it)
-      psp_unit<DOF, true>(sm, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(), &vn, &pre);
+      psp_unit<DOF, true, QM>(sm, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(), &vn, &pre);
       u = vn;  // resolved by psp_unit
     }
     psync();  // the next unit's LDS writes after this unit's reads
@@ -666,18 +666,32 @@ hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& 
   return dof == 53 ? psp_update_dof<53>(kind, st, b, sh, ma, m) : psp_update_dof<26>(kind, st, b, sh, ma, m);
 }
 
+template <int DOF, int QM>
+static void launch_epoch_q(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea, dim3 g) {
+  if (ea.ticket)
+    hipLaunchKernelGGL((psp::k_psp_epoch_p<DOF, QM>), g, dim3(64), 0, st, b, sh, ea);
+  else
+    hipLaunchKernelGGL((psp::k_psp_epoch<DOF, QM>), g, dim3(64), 0, st, b, sh, ea);
+}
+
 hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
                             int64_t grid) {
   const dim3 g((unsigned)(grid > 0 ? grid : b.batch));
-  if (ea.ticket) {
-    if (dof == 53)
-      hipLaunchKernelGGL(psp::k_psp_epoch_p<53>, g, dim3(64), 0, st, b, sh, ea);
-    else
-      hipLaunchKernelGGL(psp::k_psp_epoch_p<26>, g, dim3(64), 0, st, b, sh, ea);
-  } else if (dof == 53) {
-    hipLaunchKernelGGL(psp::k_psp_epoch<53>, g, dim3(64), 0, st, b, sh, ea);
+  // the kernel instantiated for the handle's process-noise shape (psp_predict QM)
+#ifndef PSP_QM_SPLIT
+#define PSP_QM_SPLIT 1
+#endif
+#if !PSP_QM_SPLIT  // A/B: one kernel for both shapes (the r03k build)
+  if (dof == 53) launch_epoch_q<53, 0>(st, b, sh, ea, g);
+  else launch_epoch_q<26, 0>(st, b, sh, ea, g);
+  return hipGetLastError();
+#endif
+  if (dof == 53) {
+    if (sh.q_simple) launch_epoch_q<53, 1>(st, b, sh, ea, g);
+    else launch_epoch_q<53, 2>(st, b, sh, ea, g);
   } else {
-    hipLaunchKernelGGL(psp::k_psp_epoch<26>, g, dim3(64), 0, st, b, sh, ea);
+    if (sh.q_simple) launch_epoch_q<26, 1>(st, b, sh, ea, g);
+    else launch_epoch_q<26, 2>(st, b, sh, ea, g);
   }
   return hipGetLastError();
 }
@@ -732,8 +746,9 @@ int64_t psp_epoch_slots_per_xcd(int dof, int device) { return psp_epoch_slots(do
 
 int64_t psp_epoch_slots(int dof, int device, bool persist) {
   int per_cu = 0, cus = 0;
-  const void* k = persist ? (dof == 53 ? (const void*)psp::k_psp_epoch_p<53> : (const void*)psp::k_psp_epoch_p<26>)
-                          : (dof == 53 ? (const void*)psp::k_psp_epoch<53> : (const void*)psp::k_psp_epoch<26>);
+  // (the QM = 2 instantiations have the same LDS and no more registers)
+  const void* k = persist ? (dof == 53 ? (const void*)psp::k_psp_epoch_p<53, 1> : (const void*)psp::k_psp_epoch_p<26, 1>)
+                          : (dof == 53 ? (const void*)psp::k_psp_epoch<53, 1> : (const void*)psp::k_psp_epoch<26, 1>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return 0;

@@ -43,7 +43,7 @@ SYMBOLS = [
     "uwvk_ipose_create", "uwvk_ipose_destroy", "uwvk_ipose_stream", "uwvk_ipose_init",
     "uwvk_ipose_set_pose_reference", "uwvk_ipose_predict", "uwvk_ipose_update_visual",
     "uwvk_ipose_get_corrected_pose", "uwvk_ipose_get_state", "uwvk_ipose_get_status",
-    "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots", "uwvk_pose_timer_mark", "uwvk_pose_timer_elapsed",
+    "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots", "uwvk_pose_epoch_qshape", "uwvk_pose_timer_mark", "uwvk_pose_timer_elapsed",
     "uwvk_xcd_round_robin", "uwvk_synth_normal",
 ]
 
@@ -78,6 +78,8 @@ def lib(path=None):
         L.uwvk_comm_destroy.argtypes = [VP]
         L.uwvk_device_free.argtypes = [VP]
         L.uwvk_pose_tail_chunks.argtypes = [C.c_int64, C.c_int64, C.c_int64]
+        L.uwvk_pose_epoch_qshape.argtypes = [C.c_void_p]
+        L.uwvk_pose_epoch_qshape.restype = C.c_int
         L.uwvk_pose_resident_slots.argtypes = [C.c_int, C.c_int]
         L.uwvk_pose_resident_slots.restype = C.c_int64
         L.uwvk_memcpy_h2d.argtypes = [VP, VP, C.c_size_t]
@@ -176,6 +178,10 @@ class PoseUKFBatch:
     def set_tail_chunks(self, chunks):
         """UWVK_OPT_TAIL_CHUNKS: 0 the planner's chunk count, 2..8 forced (tests)."""
         _chk(self.L.uwvk_pose_set_option(self.h, 4, int(chunks)), "set_option")
+
+    def epoch_qshape(self):
+        """The process-noise shape the PSP epoch kernel runs for: 1 simple, 2 general."""
+        return int(self.L.uwvk_pose_epoch_qshape(self.h))
 
     def set_persist(self, on=True):
         """UWVK_OPT_PERSIST: run_log on resident workgroups that take work units

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
 epochs = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 base = os.path.join(ROOT, "gpurun_out", tag)
-KERNEL = "k_psp_epoch<53>"
+KERNEL = "k_psp_epoch<53"  # k_psp_epoch<53, QM> (r03: instantiated per process-noise shape)
 
 
 def longest(pass_name):
