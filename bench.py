@@ -466,7 +466,10 @@ def main():
                        else (F_STEP_PSP * a.steps + F_UPD3_PSP * n_dvl))
     eff_tf = flops_ref / (kernel_ms * 1e-3) / 1e12
     model_tf = flops_model / (kernel_ms * 1e-3) / 1e12
-    kname = ("k_pose_epoch<%d>" % a.dof) if a.dense else ("k_psp_epoch<%d, %d>" % (a.dof, f.epoch_qshape()))
+    # the PSP instantiation run (uwvk_psp_k.hip launch_epoch_dof): Q shape, and
+    # 1 when the window holds no pressure / ADCP epoch (0x4 | 0x8)
+    evs = 0 if (f.epoch_qshape() != 1 or bool(((window & 0xC) != 0).any())) else 1
+    kname = ("k_pose_epoch<%d>" % a.dof) if a.dense else ("k_psp_epoch<%d, %d, %d>" % (a.dof, f.epoch_qshape(), evs))
     workload = "%s-dof%d-b%d%s" % (log_mode, a.dof, B, "-dense" if a.dense else "")
     pmc = pmc_entry(workload, a.steps)
     cr = None if a.dense or launches != 1 else counter_roofline(pmc, B, a.steps, kernel_ms)

@@ -742,8 +742,10 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     ea.count = last - e;
     ea.efforts_only = 0;
     int64_t grid = 0;
+    uint32_t ev_any = 0;  // the event kinds of this launch's epochs (kernel choice)
+    for (int64_t k = e; k < last; k++) ev_any |= hf[k - first];
     HIPCHK(prepare_tail(h, ea, grid));
-    HIPCHK(launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid));
+    HIPCHK(launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid, ev_any));
     if (r < first + count) {
       ea.first = r;
       ea.count = 1;

@@ -8,8 +8,10 @@ hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& 
                              const MeasArgs& ma, int m);
 #include <vector>
 // grid 0: one block per instance; otherwise 8 (n_x + (chunks - 1) r_x)
+// ev_any: the OR of the launch's epoch flags (selects the kernel instantiation;
+// all bits set is always correct)
 hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                            int64_t grid = 0);
+                            int64_t grid = 0, uint32_t ev_any = 0xffffffffu);
 // resident k_psp_epoch blocks per XCD (occupancy x CUs / 8), 0 if unknown
 int64_t psp_epoch_slots_per_xcd(int dof, int device);
 // resident blocks of the static (k_psp_epoch) or persistent (k_psp_epoch_p)

@@ -344,7 +344,7 @@ struct PspPre {
   bool have;
 };
 
-template <int DOF, bool PERSIST, int QM, class Again>
+template <int DOF, bool PERSIST, int QM, int EVS, class Again>
 UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea, const TailUnit& tu0,
                        const LaneQ& lq, Again again, int64_t tlw, int lp, uint32_t* next = nullptr,
                        PspPre<DOF>* pre = nullptr) {
@@ -503,6 +503,10 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
         nan = true;
       }
     }
+    // EVS 1: the launch's epochs hold no pressure / ADCP event (host-checked),
+    // so those updates are not compiled in (half the SGPR spills, 1% faster:
+    // profiles/r03/evs/)
+    if constexpr (EVS == 0) {
     if (fl & UWVK_EV_PRESSURE) {
       const double* z = ea.pressure + (int64_t)ea.p_index[e] * B + inst;
       if (all_finite(z, 1)) {
@@ -522,6 +526,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
         cnt[2] += psp_update<DOF>(sm, zz, R, 1, h, &sok, ds, ids);
         ok = ok && sok;
       }
+    }
     }
 #endif
   }
@@ -576,7 +581,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
 #endif
 }
 
-template <int DOF, int QM>
+template <int DOF, int QM, int EVS>
 __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const int64_t B = b.batch;
@@ -587,7 +592,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
     return;
   }
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
-  psp_unit<DOF, false, QM>(sm, b, ea, tu, lq, [&] { return tail_unit(ea, B); }, blockIdx.x, lane_id());
+  psp_unit<DOF, false, QM, EVS>(sm, b, ea, tu, lq, [&] { return tail_unit(ea, B); }, blockIdx.x, lane_id());
 }
 
 // Persistent form (UWVK_OPT_PERSIST): as many blocks as are resident, each
@@ -598,7 +603,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
 // dispatch-order assumption.  Faster XCDs / CUs take more units, and a slot
 // moves to its next unit without a new workgroup dispatch.  The next ticket is
 // taken while the current unit runs (its atomic latency hidden).
-template <int DOF, int QM>
+template <int DOF, int QM, int EVS>
 __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
@@ -626,7 +631,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, P
     } else {
       // a laundered lane id: the unit's per-lane constants are recomputed per
       // unit, not hoisted out of the unit loop (held live across it)
-      psp_unit<DOF, true, QM>(sm, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(), &vn, &pre);
+      psp_unit<DOF, true, QM, EVS>(sm, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(), &vn, &pre);
       u = vn;  // resolved by psp_unit
     }
     psync();  // the next unit's LDS writes after this unit's reads
@@ -666,33 +671,41 @@ hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& 
   return dof == 53 ? psp_update_dof<53>(kind, st, b, sh, ma, m) : psp_update_dof<26>(kind, st, b, sh, ma, m);
 }
 
-template <int DOF, int QM>
+template <int DOF, int QM, int EVS>
 static void launch_epoch_q(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea, dim3 g) {
   if (ea.ticket)
-    hipLaunchKernelGGL((psp::k_psp_epoch_p<DOF, QM>), g, dim3(64), 0, st, b, sh, ea);
+    hipLaunchKernelGGL((psp::k_psp_epoch_p<DOF, QM, EVS>), g, dim3(64), 0, st, b, sh, ea);
   else
-    hipLaunchKernelGGL((psp::k_psp_epoch<DOF, QM>), g, dim3(64), 0, st, b, sh, ea);
+    hipLaunchKernelGGL((psp::k_psp_epoch<DOF, QM, EVS>), g, dim3(64), 0, st, b, sh, ea);
 }
 
-hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                            int64_t grid) {
-  const dim3 g((unsigned)(grid > 0 ? grid : b.batch));
-  // the kernel instantiated for the handle's process-noise shape (psp_predict QM)
+template <int DOF>
+static void launch_epoch_dof(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea, dim3 g,
+                             uint32_t ev_any) {
+  // the kernel instantiated for the handle's process-noise shape (psp_predict
+  // QM) and the launch's event kinds (EVS 1: no pressure / ADCP epoch in the
+  // range, the C3 workload); a general Q runs the one kernel with everything
+  const bool pa = (ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP)) != 0;
 #ifndef PSP_QM_SPLIT
 #define PSP_QM_SPLIT 1
 #endif
-#if !PSP_QM_SPLIT  // A/B: one kernel for both shapes (the r03k build)
-  if (dof == 53) launch_epoch_q<53, 0>(st, b, sh, ea, g);
-  else launch_epoch_q<26, 0>(st, b, sh, ea, g);
-  return hipGetLastError();
+#if !PSP_QM_SPLIT  // A/B: one kernel for every shape and event set (the r03k build)
+  launch_epoch_q<DOF, 0, 0>(st, b, sh, ea, g);
+  (void)pa;
+#else
+  if (!sh.q_simple) launch_epoch_q<DOF, 2, 0>(st, b, sh, ea, g);
+  else if (pa) launch_epoch_q<DOF, 1, 0>(st, b, sh, ea, g);
+  else launch_epoch_q<DOF, 1, 1>(st, b, sh, ea, g);
 #endif
-  if (dof == 53) {
-    if (sh.q_simple) launch_epoch_q<53, 1>(st, b, sh, ea, g);
-    else launch_epoch_q<53, 2>(st, b, sh, ea, g);
-  } else {
-    if (sh.q_simple) launch_epoch_q<26, 1>(st, b, sh, ea, g);
-    else launch_epoch_q<26, 2>(st, b, sh, ea, g);
-  }
+}
+
+hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
+                            int64_t grid, uint32_t ev_any) {
+  const dim3 g((unsigned)(grid > 0 ? grid : b.batch));
+  if (dof == 53)
+    launch_epoch_dof<53>(st, b, sh, ea, g, ev_any);
+  else
+    launch_epoch_dof<26>(st, b, sh, ea, g, ev_any);
   return hipGetLastError();
 }
 
@@ -746,9 +759,9 @@ int64_t psp_epoch_slots_per_xcd(int dof, int device) { return psp_epoch_slots(do
 
 int64_t psp_epoch_slots(int dof, int device, bool persist) {
   int per_cu = 0, cus = 0;
-  // (the QM = 2 instantiations have the same LDS and no more registers)
-  const void* k = persist ? (dof == 53 ? (const void*)psp::k_psp_epoch_p<53, 1> : (const void*)psp::k_psp_epoch_p<26, 1>)
-                          : (dof == 53 ? (const void*)psp::k_psp_epoch<53, 1> : (const void*)psp::k_psp_epoch<26, 1>);
+  // (the other instantiations have the same LDS and no more registers)
+  const void* k = persist ? (dof == 53 ? (const void*)psp::k_psp_epoch_p<53, 1, 0> : (const void*)psp::k_psp_epoch_p<26, 1, 0>)
+                          : (dof == 53 ? (const void*)psp::k_psp_epoch<53, 1, 0> : (const void*)psp::k_psp_epoch<26, 1, 0>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return 0;
