@@ -345,7 +345,9 @@ typedef struct uwvk_pose_log {
   const double* efforts;     /* [n_efforts][batch][6] */
   double efforts_cov[36];
   /* HOST copy of flags (nullable): lets run_log plan its launches without a
-   * device->host read of `flags`. */
+   * device->host read of `flags`.  It must equal `flags`: run_log also picks
+   * each launch's kernel from it (a launch whose host flags hold no pressure or
+   * ADCP event runs a kernel without those updates). */
   const uint32_t* host_flags;
 } uwvk_pose_log;
 
