@@ -113,6 +113,21 @@ static void set_shared(uwvk_pose* h, const uwvk_pose_parameter& p, const uwvk_lo
 }
 
 // PSP kernels read the batch-shared parameters and dt^2 Q (packed) from device memory
+// lane-resident Q (psp::LaneQ): no coupling of the rewritten rows (< 9) with
+// anything but their own diagonal / the orientation block, and a band of at
+// most 2 below the diagonal in rows >= 9 (the epoch kernel's QM = 1)
+static bool q_is_simple(const uwvk_pose* h) {
+  const int n = h->dof;
+  auto Qij = [&](int i, int j) { return h->Qh.empty() ? 0.0 : h->Qh[(size_t)i * n + j]; };
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < i; j++) {
+      if (Qij(i, j) == 0.0) continue;
+      const bool ori = i >= 3 && i < 6 && j >= 3 && j < 6;
+      if ((i < 9 || j < 9) ? !ori : (i - j > 2)) return false;
+    }
+  return true;
+}
+
 static hipError_t upload_shared(uwvk_pose* h, double dt) {
   hipError_t e = hipSuccess;
   if (dt != h->qp_dt) {
@@ -163,15 +178,7 @@ static hipError_t upload_shared(uwvk_pose* h, double dt) {
     int bw = 0;
     for (int i = 9; i < n; i++) bw = std::max(bw, i - h->sh.qlo[i]);
     h->sh.q_bw = bw;
-    // lane-resident Q (psp::LaneQ): no coupling of the rewritten rows (< 9) with
-    // anything but their own diagonal / the orientation block, band <= 2 below
-    bool simple = bw <= 2;
-    for (int i = 0; i < n && simple; i++)
-      for (int j = 0; j < i && simple; j++) {
-        const bool ori = i >= 3 && i < 6 && j >= 3 && j < 6;
-        if ((i < 9 || j < 9) && !ori && Qij(i, j) != 0.0) simple = false;
-      }
-    h->sh.q_simple = simple ? 1 : 0;
+    h->sh.q_simple = q_is_simple(h) ? 1 : 0;
     e = hipMemcpyAsync(h->d_Qp, qp.data(), qp.size() * 8, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h->d_qband, band.data(), 128 * 8, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);  // qp, band are locals
@@ -821,7 +828,7 @@ int64_t uwvk_pose_resident_slots(int dof, int device) {
 
 int uwvk_xcd_round_robin(int device) { return xcd_round_robin(device); }
 
-int uwvk_pose_epoch_qshape(const uwvk_pose* h) { return h ? (h->sh.q_simple ? 1 : 2) : 0; }
+int uwvk_pose_epoch_qshape(const uwvk_pose* h) { return h ? (q_is_simple(h) ? 1 : 2) : 0; }
 
 int uwvk_pose_tail_chunks(int64_t instances_per_xcd, int64_t slots_per_xcd, int64_t epochs) {
   return plan_tail(instances_per_xcd, slots_per_xcd, epochs);

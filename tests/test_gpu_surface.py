@@ -240,6 +240,7 @@ def test_general_process_noise(eng, orc, dof, path, variant):
     init_both(o, g, cfg, uwv, log)
     for f in (o, g):
         f.set_process_noise(Q)
+    assert g.epoch_qshape() == 2  # run_log takes the general-Q instantiation of the epoch kernel
     for e in range(3):
         for f in (o, g):
             f.set_rotation_rate(log["gyro"][e])
@@ -265,6 +266,7 @@ def test_process_noise_imu_in_body_single_predict(eng, orc, path):
         f.set_rotation_rate(log["gyro"][0])
         f.predict(1e-3)
     _check(o, g, 53, TOL_STEP)
+    assert g.epoch_qshape() == 1  # the config's Q (rotated bias blocks): the simple-Q instantiation
 
 
 # ---- measurementEfforts -> constrainVelocity side effect ---------------------------
