@@ -756,7 +756,8 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     if (r < first + count) {
       ea.first = r;
       ea.count = 1;
-      HIPCHK(launch_pose_efforts_epoch(h->dof, h->stream, b, sh, ea));
+      HIPCHK(launch_pose_efforts_epoch(h->dof, h->stream, b, sh, ea,
+                                       (hf[r - first] & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0));
     }
     e = last;
   }

@@ -247,6 +247,9 @@ UWVK_DEV void chol2_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, d
 #ifndef UWVK_CHOL_GROUP
 #define UWVK_CHOL_GROUP 3
 #endif
+#ifndef UWVK_CHOL_CYCLIC
+#define UWVK_CHOL_CYCLIC 0
+#endif
 template <int DOF, int J, int GS>
 constexpr int chol_group() {  // columns J .. J+g-1 with one owner (the halves of the two waves)
   constexpr int H = (DOF + 1) / 2;
@@ -301,6 +304,88 @@ UWVK_DEV void chol2g_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, 
   }
 }
 
+// Cyclic form (UWVK_CHOL_CYCLIC): column blocks [tG, tG + G) alternate between
+// the two waves (block t to wave t & 1) instead of one half per wave, so that
+// both waves keep later columns to update until the end of the factorisation
+// (with halves, wave 0 only waits at the barriers of the second half while wave
+// 1 runs every column chain and every update alone).  Per entry the same fused
+// multiply-adds in the same order: the factor is bitwise chol2g_step's for
+// G = UWVK_CHOL_GROUP (its groups are the blocks, 27 being a multiple of 3).
+template <int DOF, int W, int G>
+struct CholCyc {
+  __host__ __device__ static constexpr bool own(int c) { return ((c / G) & 1) == W; }
+  __host__ __device__ static constexpr int lc(int c) { return (c / (2 * G)) * G + c % G; }  // local slot of an own column
+  __host__ __device__ static constexpr int n() {
+    int k = 0;
+    for (int c = 0; c < DOF; c++) k += own(c) ? 1 : 0;
+    return k;
+  }
+};
+template <int DOF, int W, int G, int J, int S, int NC>
+UWVK_DEV void chol2c_step(double (&a)[NC], Smem<DOF>& sm, int r, bool& ok, double piv) {
+  if constexpr (J < DOF) {
+    using CC = CholCyc<DOF, W, G>;
+    constexpr bool own = CC::own(J);
+    constexpr int g = (DOF - J) < G ? (DOF - J) : G;
+    constexpr int JN = J + g;
+    constexpr int b0 = (S & 1) * G;
+    static_assert(Geo<DOF>::LPSZ >= 2 * G * 64, "column buffers in the factor region");
+    double* buf = sm.Lp + b0 * 64;
+    if constexpr (own) {
+#pragma unroll
+      for (int k = 0; k < g; k++) {
+        const double p = k == 0 ? piv : readlane_d(a[CC::lc(J + k)], J + k);
+        ok = ok && (p > 0.0);
+        const double inv = rsqrt_f64(p);
+        const double d = p * inv;
+        a[CC::lc(J + k)] = (r == J + k) ? d : a[CC::lc(J + k)] * inv;
+        buf[k * 64 + r] = a[CC::lc(J + k)];
+#pragma unroll
+        for (int m = k + 1; m < g; m++) {
+          const double lmk = readlane_d(a[CC::lc(J + k)], J + m);  // L[J+m][J+k]
+          a[CC::lc(J + m)] -= a[CC::lc(J + k)] * lmk;
+          asm volatile("" : "+v"(a[CC::lc(J + m)]));
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < g; k++) {
+      const double lk = own ? a[CC::lc(own ? J + k : 0)] : buf[k * 64 + r];
+#pragma unroll
+      for (int c = JN; c < DOF; c++)
+        if (CC::own(c)) a[CC::lc(c)] -= lk * buf[k * 64 + c];
+    }
+#pragma unroll
+    for (int c = JN; c < DOF; c++)
+      if (CC::own(c)) asm volatile("" : "+v"(a[CC::lc(c)]));
+    double pnext = 0.0;
+    if constexpr (JN < DOF && CC::own(JN)) pnext = readlane_d(a[CC::lc(JN)], JN);
+    chol2c_step<DOF, W, G, JN, S + 1, NC>(a, sm, r, ok, pnext);
+  }
+}
+template <int DOF, int W>
+UWVK_DEV void chol2c_wave(Smem<DOF>& sm) {
+  constexpr int G = UWVK_CHOL_GROUP;
+  using CC = CholCyc<DOF, W, G>;
+  const int r = lane_id();
+  const int rr = r < DOF ? r : DOF - 1;  // lanes >= DOF shadow the last row (discarded)
+  constexpr int NC = CC::n();
+  double a[NC];
+#pragma unroll
+  for (int c = 0; c < DOF; c++)
+    if (CC::own(c)) a[CC::lc(c)] = sm.S[rr * DOF + c];
+  bool ok = true;
+  chol2c_step<DOF, W, G, 0, 0, NC>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
+  if (r < DOF) {
+    const int base = r * (r + 1) / 2;
+#pragma unroll
+    for (int c = 0; c < DOF; c++)
+      if (CC::own(c) && c <= r) sm.Lp[base + c] = a[CC::lc(c)];
+  }
+  if (r == 0) sm.vec[62 + W] = ok ? 1.0 : 0.0;
+}
+
 template <int DOF, int W, int C0, int C1>
 UWVK_DEV void chol2_wave(Smem<DOF>& sm) {
   const int r = lane_id();
@@ -326,11 +411,18 @@ UWVK_DEV void chol2_wave(Smem<DOF>& sm) {
 template <int DOF>
 UWVK_DEV bool chol_lds(Smem<DOF>& sm) {
   if constexpr (Geo<DOF>::NW == 2) {
+#if UWVK_CHOL_CYCLIC
+    if (wid() == 0)
+      chol2c_wave<DOF, 0>(sm);
+    else
+      chol2c_wave<DOF, 1>(sm);
+#else
     constexpr int H = (DOF + 1) / 2;
     if (wid() == 0)
       chol2_wave<DOF, 0, 0, H>(sm);
     else
       chol2_wave<DOF, 1, H, DOF>(sm);
+#endif
     __syncthreads();
     const bool ok = sm.vec[62] != 0.0 && sm.vec[63] != 0.0;
     __syncthreads();
@@ -887,7 +979,10 @@ struct HJmax {
   static constexpr int value = DOF;
 };
 
-template <int DOF, int M, class H>
+// LAD: -1 the apply_delta form from `literal` at run time; 0 / 1 fixed at compile
+// time (the exact rotation identity / the literal re-spread), so a kernel built
+// for one form carries only its registers
+template <int DOF, int M, class H, int LAD = -1>
 UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)[M * M], int zmode, int gate, H h,
                           bool* ok, Stamper* st, bool literal, int right) {
   using L = Lay<DOF>;
@@ -1063,7 +1158,7 @@ UWVK_DEV bool pose_update(Smem<DOF>& sm, const double (&z)[M], const double (&R)
   }
   __syncthreads();
   UWVK_STAMP(7);
-  const bool aok = apply_delta<DOF>(sm, literal, right, st);
+  const bool aok = apply_delta<DOF>(sm, LAD < 0 ? literal : LAD != 0, right, st);
   *ok = cok && aok;
   return true;
 }

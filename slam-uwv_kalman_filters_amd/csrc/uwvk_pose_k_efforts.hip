@@ -7,11 +7,17 @@
 namespace uwvk {
 
 hipError_t launch_pose_efforts_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
-                                     const EpochArgs& ea) {
-  if (dof == 53)
-    hipLaunchKernelGGL(k_pose_efforts_epoch<53>, dim3((unsigned)b.batch), dim3(Geo<53>::T), 0, st, b, sh, ea);
-  else
-    hipLaunchKernelGGL(k_pose_efforts_epoch<26>, dim3((unsigned)b.batch), dim3(Geo<26>::T), 0, st, b, sh, ea);
+                                     const EpochArgs& ea, int vo) {
+  const dim3 g((unsigned)b.batch);
+  if (dof == 53) {
+    if (sh.literal_apply_delta) hipLaunchKernelGGL((k_pose_efforts_epoch<53, -1, -1>), g, dim3(Geo<53>::T), 0, st, b, sh, ea);
+    else if (vo) hipLaunchKernelGGL((k_pose_efforts_epoch<53, 1, 0>), g, dim3(Geo<53>::T), 0, st, b, sh, ea);
+    else hipLaunchKernelGGL((k_pose_efforts_epoch<53, 0, 0>), g, dim3(Geo<53>::T), 0, st, b, sh, ea);
+  } else {
+    if (sh.literal_apply_delta) hipLaunchKernelGGL((k_pose_efforts_epoch<26, -1, -1>), g, dim3(Geo<26>::T), 0, st, b, sh, ea);
+    else if (vo) hipLaunchKernelGGL((k_pose_efforts_epoch<26, 1, 0>), g, dim3(Geo<26>::T), 0, st, b, sh, ea);
+    else hipLaunchKernelGGL((k_pose_efforts_epoch<26, 0, 0>), g, dim3(Geo<26>::T), 0, st, b, sh, ea);
+  }
   return hipGetLastError();
 }
 

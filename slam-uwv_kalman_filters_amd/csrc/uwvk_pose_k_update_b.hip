@@ -12,9 +12,16 @@ hipError_t launch_pose_update_b(int dof, int kind, hipStream_t st, const PoseBuf
       if (dof == 53) hipLaunchKernelGGL((k_pose_update<53, MK_WATER>), g, dim3(Geo<53>::T), 0, st, b, sh, ma, m);
       else hipLaunchKernelGGL((k_pose_update<26, MK_WATER>), g, dim3(Geo<26>::T), 0, st, b, sh, ma, m);
       return hipGetLastError();
-    case MK_EFFORTS:
-      if (dof == 53) hipLaunchKernelGGL((k_pose_update<53, MK_EFFORTS>), g, dim3(Geo<53>::T), 0, st, b, sh, ma, m);
-      else hipLaunchKernelGGL((k_pose_update<26, MK_EFFORTS>), g, dim3(Geo<26>::T), 0, st, b, sh, ma, m);
+    case MK_EFFORTS:  // one instantiation per model (efforts / velocity-only) with the exact apply_delta
+      if (dof == 53) {
+        if (sh.literal_apply_delta) hipLaunchKernelGGL((k_pose_update<53, MK_EFFORTS>), g, dim3(Geo<53>::T), 0, st, b, sh, ma, m);
+        else if (ma.only_vel) hipLaunchKernelGGL((k_pose_update<53, MK_EFFORTS, 1, 0>), g, dim3(Geo<53>::T), 0, st, b, sh, ma, m);
+        else hipLaunchKernelGGL((k_pose_update<53, MK_EFFORTS, 0, 0>), g, dim3(Geo<53>::T), 0, st, b, sh, ma, m);
+      } else {
+        if (sh.literal_apply_delta) hipLaunchKernelGGL((k_pose_update<26, MK_EFFORTS>), g, dim3(Geo<26>::T), 0, st, b, sh, ma, m);
+        else if (ma.only_vel) hipLaunchKernelGGL((k_pose_update<26, MK_EFFORTS, 1, 0>), g, dim3(Geo<26>::T), 0, st, b, sh, ma, m);
+        else hipLaunchKernelGGL((k_pose_update<26, MK_EFFORTS, 0, 0>), g, dim3(Geo<26>::T), 0, st, b, sh, ma, m);
+      }
       return hipGetLastError();
   }
   return hipErrorInvalidValue;

@@ -75,8 +75,10 @@ hipError_t launch_pose_predict(int dof, hipStream_t st, const PoseBufs& b, const
 hipError_t launch_pose_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                               const MeasArgs& ma, int m);
 hipError_t launch_pose_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea);
+// vo: the epoch's flag word has UWVK_EV_EFFORTS_VELOCITY_ONLY (constrainVelocity);
+// the apply_delta form is sh.literal_apply_delta
 hipError_t launch_pose_efforts_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
-                                     const EpochArgs& ea);
+                                     const EpochArgs& ea, int vo);
 hipError_t launch_pose_rotation_rate(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double* out);
 // the truth store-vector of the ensemble statistics, passed by value (kernarg)
 struct StatTruth {
@@ -132,6 +134,60 @@ UWVK_DEV bool all_finite(const double* a, int n) {
   return f;
 }
 
+// The BodyEfforts update (VO = 0, measurementEfforts, PoseUKF.cpp:581-602) or its
+// velocity-only form (VO = 1, constrainVelocity, PoseUKF.cpp:585-591); LAD as in
+// pose_update.  k_pose_efforts_epoch instantiates each (VO, LAD = 0) pair alone:
+// with both models and the literal re-spread in one kernel the register peak was
+// the re-spread's (512 B/lane of scratch; 24 B/lane without it).
+template <int DOF, int VO, int LAD = -1>
+UWVK_DEV bool do_update_efforts(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, int64_t i, const double* zin,
+                                const double* Rin, const MeasArgs& ma, double wrot[3], bool* ok, Stamper* st) {
+  using L = Lay<DOF>;
+  double z[6], R[36];
+  for (int k = 0; k < 6; k++) z[k] = zin[k];
+  for (int k = 0; k < 36; k++) R[k] = Rin[k];
+  Efforts6 ef;
+  ef.base = b.uwv;
+  ef.weight = sh.uwv_weight;
+  ef.buoyancy = sh.uwv_buoyancy;
+  for (int k = 0; k < 3; k++) { ef.cog[k] = sh.cog[k]; ef.cob[k] = sh.cob[k]; }
+  double wb[3];
+  rotation_rate_body<DOF>(sm, sh, wrot, wb);
+  double* model = b.model + i * 27;
+  if constexpr (VO) {
+    HConstrain<DOF> h;
+    h.ef = ef;
+    h.blk.has = true;
+    h.blk.v = model;
+    for (int k = 0; k < 3; k++) { h.wb[k] = wb[k]; h.imu[k] = sh.p.imu_in_body[k]; }
+    h.w3[0] = sm.mu[L::s_wv]; h.w3[1] = sm.mu[L::s_wv + 1]; h.w3[2] = 0.0;
+    for (int k = 0; k < 4; k++) h.q[k] = sm.mu[L::s_quat + k];
+    double ra[3], cr[3], cc[3];
+    qrot_inv(h.q, sm.mu + L::s_acc, ra);
+    cross3(wb, h.imu, cr);
+    cross3(wb, cr, cc);
+    for (int k = 0; k < 3; k++) h.ab[k] = ra[k] - cc[k];
+    return pose_update<DOF, 6, HConstrain<DOF>, LAD>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0,
+                                                     sh.so3_right);
+  } else {
+    HEfforts<DOF> h;
+    h.ef = ef;
+    for (int k = 0; k < 3; k++) { h.wb[k] = wb[k]; h.imu[k] = sh.p.imu_in_body[k]; }
+    // side effect of PoseUKF.cpp:173: the shared model ends with the last sigma
+    // point's blocks, X_2n = mu [+] -L_{:,n-1}, i.e. the pre-update mean's.
+    if constexpr (L::has_params) {
+      const int l = tid();
+      if (l < 9) {
+        model[l] = sm.mu[L::s_inertia + l];
+        model[9 + l] = sm.mu[L::s_lin + l];
+        model[18 + l] = sm.mu[L::s_quad + l];
+      }
+    }
+    return pose_update<DOF, 6, HEfforts<DOF>, LAD>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0,
+                                                   sh.so3_right);
+  }
+}
+
 // one measurement update of kind K on instance i (Sigma in LDS)
 template <int DOF, int K>
 UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, int64_t i, const double* zin,
@@ -179,46 +235,8 @@ UWVK_DEV bool do_update(Smem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, 
     double z[1] = {zin[0]}, R[1] = {Rin[0]};
     return pose_update<DOF, 1>(sm, z, R, 0, 0, HZ<DOF>{}, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
   } else {  // MK_EFFORTS, PoseUKF.cpp:581-602
-    double z[6], R[36];
-    for (int k = 0; k < 6; k++) z[k] = zin[k];
-    for (int k = 0; k < 36; k++) R[k] = Rin[k];
-    Efforts6 ef;
-    ef.base = b.uwv;
-    ef.weight = sh.uwv_weight;
-    ef.buoyancy = sh.uwv_buoyancy;
-    for (int k = 0; k < 3; k++) { ef.cog[k] = sh.cog[k]; ef.cob[k] = sh.cob[k]; }
-    double wb[3];
-    rotation_rate_body<DOF>(sm, sh, wrot, wb);
-    double* model = b.model + i * 27;
-    if (ma.only_vel) {
-      HConstrain<DOF> h;
-      h.ef = ef;
-      h.blk.has = true;
-      h.blk.v = model;
-      for (int k = 0; k < 3; k++) { h.wb[k] = wb[k]; h.imu[k] = sh.p.imu_in_body[k]; }
-      h.w3[0] = sm.mu[L::s_wv]; h.w3[1] = sm.mu[L::s_wv + 1]; h.w3[2] = 0.0;
-      for (int k = 0; k < 4; k++) h.q[k] = sm.mu[L::s_quat + k];
-      double ra[3], cr[3], cc[3];
-      qrot_inv(h.q, sm.mu + L::s_acc, ra);
-      cross3(wb, h.imu, cr);
-      cross3(wb, cr, cc);
-      for (int k = 0; k < 3; k++) h.ab[k] = ra[k] - cc[k];
-      return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
-    }
-    HEfforts<DOF> h;
-    h.ef = ef;
-    for (int k = 0; k < 3; k++) { h.wb[k] = wb[k]; h.imu[k] = sh.p.imu_in_body[k]; }
-    // side effect of PoseUKF.cpp:173: the shared model ends with the last sigma
-    // point's blocks, X_2n = mu [+] -L_{:,n-1}, i.e. the pre-update mean's.
-    if constexpr (L::has_params) {
-      const int l = tid();
-      if (l < 9) {
-        model[l] = sm.mu[L::s_inertia + l];
-        model[9 + l] = sm.mu[L::s_lin + l];
-        model[18 + l] = sm.mu[L::s_quad + l];
-      }
-    }
-    return pose_update<DOF, 6>(sm, z, R, 0, 0, h, ok, st, sh.literal_apply_delta != 0, sh.so3_right);
+    return ma.only_vel ? do_update_efforts<DOF, 1>(sm, sh, b, i, zin, Rin, ma, wrot, ok, st)
+                       : do_update_efforts<DOF, 0>(sm, sh, b, i, zin, Rin, ma, wrot, ok, st);
   }
 }
 
@@ -241,7 +259,9 @@ __global__ __launch_bounds__(Geo<DOF>::T) void k_pose_predict(PoseBufs b, PoseSh
 #ifndef UWVK_UPD_ATTR
 #define UWVK_UPD_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
-template <int DOF, int K>
+// VO / LAD (MK_EFFORTS only): >= 0 the efforts / velocity-only model and the
+// apply_delta form fixed at compile time (do_update_efforts), picked by the host
+template <int DOF, int K, int VO = -1, int LAD = -1>
 __global__ __launch_bounds__(Geo<DOF>::T) UWVK_UPD_ATTR void k_pose_update(PoseBufs b, PoseShared sh, MeasArgs ma, int m) {
   __shared__ Smem<DOF> sm;
   const int64_t i = xcd_instance(b.batch);
@@ -261,7 +281,11 @@ __global__ __launch_bounds__(Geo<DOF>::T) UWVK_UPD_ATTR void k_pose_update(PoseB
   load_instance<DOF>(sm, b, i);
   double w[3] = {b.rot[i * 3], b.rot[i * 3 + 1], b.rot[i * 3 + 2]};
   bool ok = true;
-  const bool acc = do_update<DOF, K>(sm, sh, b, i, z, R, ma, w, &ok);
+  bool acc;
+  if constexpr (K == MK_EFFORTS && VO >= 0)
+    acc = do_update_efforts<DOF, VO, LAD>(sm, sh, b, i, z, R, ma, w, &ok, nullptr);
+  else
+    acc = do_update<DOF, K>(sm, sh, b, i, z, R, ma, w, &ok);
   if (tid() == 0) {
     if (!ok) b.status[i] |= UWVK_ST_NOTPD;
     if (ma.accepted) ma.accepted[i] = acc ? 1 : 0;
@@ -279,7 +303,10 @@ __global__ __launch_bounds__(Geo<DOF>::T) UWVK_UPD_ATTR void k_pose_update(PoseB
 #ifndef UWVK_EFF_ATTR
 #define UWVK_EFF_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
-template <int DOF>
+// VO: 0 / 1 the efforts / velocity-only instantiation picked by the host from the
+// epoch's flag word, LAD 0 (the default exact apply_delta); VO = -1 with LAD = -1
+// decides both at run time (the UWVK_OPT_LITERAL_APPLY_DELTA option)
+template <int DOF, int VO, int LAD>
 __global__ __launch_bounds__(Geo<DOF>::T) UWVK_EFF_ATTR void k_pose_efforts_epoch(PoseBufs b, PoseShared sh, EpochArgs ea) {
   __shared__ Smem<DOF> sm;
   const int64_t B = b.batch, i = xcd_instance(B), e = ea.first;
@@ -294,13 +321,15 @@ __global__ __launch_bounds__(Geo<DOF>::T) UWVK_EFF_ATTR void k_pose_efforts_epoc
   load_instance<DOF>(sm, b, i);
   UWVK_STAMP(11);
   MeasArgs me{};
-  me.only_vel = (fl & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0;
+  me.only_vel = VO >= 0 ? VO : ((fl & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0);
   me.v3[0] = ea.p_sens[0]; me.v3[1] = ea.p_sens[1]; me.v3[2] = ea.p_sens[2];
   double w[3] = {b.rot[i * 3], b.rot[i * 3 + 1], b.rot[i * 3 + 2]};
   const double* z = ea.efforts + ((int64_t)ea.e_index[e] * B + i) * 6;
   bool sok = true, nan = false;
   uint32_t acc = 0;
-  if (all_finite(z, 6)) acc = do_update<DOF, MK_EFFORTS>(sm, sh, b, i, z, ea.e_cov, me, w, &sok, st) ? 1u : 0u;
+  if (all_finite(z, 6)) acc = (VO > 0 || (VO < 0 && me.only_vel) ? do_update_efforts<DOF, 1, LAD>(sm, sh, b, i, z, ea.e_cov, me, w, &sok, st)
+                                                    : do_update_efforts<DOF, 0, LAD>(sm, sh, b, i, z, ea.e_cov, me, w, &sok, st))
+              ? 1u : 0u;
   else nan = true;
   UWVK_STAMP(12);
   if (tid() == 0) {
