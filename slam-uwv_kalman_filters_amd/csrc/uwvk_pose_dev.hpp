@@ -408,9 +408,12 @@ UWVK_DEV void chol2_wave(Smem<DOF>& sm) {
   if (r == 0) sm.vec[62 + W] = ok ? 1.0 : 0.0;
 }
 
+#ifndef UWVK_CHOL_ONEWAVE  // A/B: the 53-DOF factor on wave 0 alone (chol_step, no workgroup barrier per column)
+#define UWVK_CHOL_ONEWAVE 0
+#endif
 template <int DOF>
 UWVK_DEV bool chol_lds(Smem<DOF>& sm) {
-  if constexpr (Geo<DOF>::NW == 2) {
+  if constexpr (Geo<DOF>::NW == 2 && !UWVK_CHOL_ONEWAVE) {
 #if UWVK_CHOL_CYCLIC
     if (wid() == 0)
       chol2c_wave<DOF, 0>(sm);

@@ -265,23 +265,24 @@ def test_ensemble_stats_excludes_non_pd_instances():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
-def test_bench_self_launches_two_ranks():
-    """`bench.py --gpus 2` with no launcher starts its two rank processes itself
-    (one-GPU rehearsal: UWVK_BENCH_SAME_DEVICE puts both on device 0, where
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_bench_self_launches_ranks(ranks):
+    """`bench.py --gpus N` with no launcher starts its N rank processes itself
+    (one-GPU rehearsal: UWVK_BENCH_SAME_DEVICE puts all on device 0, where
     RCCL refuses a second rank, so the statistics sum goes over gloo) and
-    reports the whole job: n_gpus 2, the global batch of both shards."""
+    reports the whole job: n_gpus N, the global batch of all shards."""
     import json
     import subprocess
     env = dict(os.environ, UWVK_BENCH_SAME_DEVICE="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup",
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(ranks), "--steps", "20", "--warmup",
                         "2", "--batch-per-gpu", "16384", "--no-cpu-baseline"], capture_output=True, text=True,
                        timeout=500, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * 16384
+    assert d["n_gpus"] == ranks and d["config"]["global_batch"] == ranks * 16384
     assert d["config"]["workload"].startswith("C5") and d["collective_check"] is True
     assert d["value"] > 0 and d["config"]["stats_allreduces_in_window"] == 1
