@@ -345,6 +345,38 @@ def init_dist(world):
     return dist
 
 
+def make_rccl(dist, engine, world, rank, local):
+    """The engine's RCCL communicator (rank 0's id broadcast over gloo), or
+    (None, reason) on every rank when any rank failed to make it: the ranks
+    agree through a gloo MIN, so a failure everywhere (an RCCL that cannot run
+    on the node) falls back to the gloo sum and says so in the line, instead of
+    ending the run."""
+    import torch
+    err = None
+    uid = [None]
+    if rank == 0:
+        try:
+            uid[0] = engine.RcclComm.unique_id()
+        except Exception as e:  # noqa: BLE001 (reported in the line)
+            err = "unique_id: %s" % e
+    dist.broadcast_object_list(uid, src=0)
+    comm = None
+    if uid[0] is not None:
+        try:
+            comm = engine.RcclComm(world, uid[0], rank, local)
+        except Exception as e:  # noqa: BLE001
+            err = "comm_init on rank %d: %s" % (rank, e)
+    ok = torch.tensor([0 if comm is None else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok[0]) == 1:
+        return comm, None
+    if comm is not None:
+        comm.close()
+    err = err or "another rank could not make it"
+    print("warning: RCCL communicator unavailable (%s); the statistics are summed over gloo" % err, file=sys.stderr)
+    return None, err
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -391,11 +423,9 @@ def main():
     # GPU, so the one-GPU rehearsal (UWVK_BENCH_SAME_DEVICE) sums over gloo;
     # UWVK_BENCH_COLL=host does the same on purpose (A/B).
     coll = "host" if (same_dev or os.environ.get("UWVK_BENCH_COLL") == "host") else "rccl"
-    comm = None
+    comm, comm_err = None, None
     if dist is not None and world > 1 and coll == "rccl":
-        uid = [engine.RcclComm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = engine.RcclComm(world, uid[0], rank, local)
+        comm, comm_err = make_rccl(dist, engine, world, rank, local)
 
     def reduce_stats(truth):
         st = f.ensemble_stats(truth, comm)
@@ -510,6 +540,8 @@ def main():
         coll_desc = None
     elif comm is not None:
         coll_desc = "RCCL all_reduce of the ensemble statistics on the handle's stream (uwvk_pose_ensemble_allreduce)"
+    elif comm_err is not None:
+        coll_desc = "gloo all_reduce of the ensemble statistics (host): the RCCL communicator failed (%s)" % comm_err
     else:
         coll_desc = "gloo all_reduce of the ensemble statistics (host)%s" % (
             ": RCCL refuses two ranks on one GPU (UWVK_BENCH_SAME_DEVICE rehearsal)" if same_dev else "")

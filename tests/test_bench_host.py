@@ -133,3 +133,40 @@ def test_gloo_control_plane_two_ranks(tmp_path):
         "dist.barrier()\n"
         "sys.exit(0 if (uid[0] == b'id' and float(w[0]) == 1.0) else 5)\n" % ROOT)
     assert bench.spawn_ranks([], 2, timeout=120, script=str(script)) == 0
+
+
+@pytest.mark.parametrize("fail", ["none", "rank1", "uid"])
+def test_make_rccl_agrees_on_a_fallback(tmp_path, fail):
+    """make_rccl over the gloo control plane with a stand-in engine: every rank
+    gets the communicator, or every rank gets (None, reason) when one rank
+    (or rank 0's id) failed, so the bench falls back to the gloo sum together."""
+    script = tmp_path / "rank.py"
+    script.write_text(
+        "import os, sys\n"
+        "sys.path.insert(0, %r)\n"
+        "import bench, torch\n"
+        "FAIL = %r\n"
+        "class Comm:\n"
+        "    closed = False\n"
+        "    def __init__(self, world, uid, rank, local):\n"
+        "        if FAIL == 'rank1' and rank == 1:\n"
+        "            raise RuntimeError('no device')\n"
+        "        assert uid == b'uid'\n"
+        "    def close(self):\n"
+        "        Comm.closed = True\n"
+        "    @staticmethod\n"
+        "    def unique_id():\n"
+        "        if FAIL == 'uid':\n"
+        "            raise RuntimeError('no rccl')\n"
+        "        return b'uid'\n"
+        "class Eng:\n"
+        "    RcclComm = Comm\n"
+        "world = int(os.environ['WORLD_SIZE'])\n"
+        "dist = bench.init_dist(world)\n"
+        "comm, err = bench.make_rccl(dist, Eng, world, dist.get_rank(), 0)\n"
+        "ok = (comm is not None and err is None) if FAIL == 'none' else (comm is None and err is not None)\n"
+        "if FAIL == 'rank1' and dist.get_rank() == 0:\n"
+        "    ok = ok and Comm.closed\n"
+        "dist.barrier()\n"
+        "sys.exit(0 if ok else 5)\n" % (ROOT, fail))
+    assert bench.spawn_ranks([], 2, timeout=120, script=str(script)) == 0
