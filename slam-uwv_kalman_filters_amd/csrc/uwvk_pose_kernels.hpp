@@ -298,8 +298,9 @@ __global__ __launch_bounds__(Geo<DOF>::T) UWVK_UPD_ATTR void k_pose_update(PoseB
 // k_pose_epoch with efforts_only, but only this update is instantiated, so the
 // kernel has the single-update register footprint instead of the fused
 // kernel's (576 B/lane scratch, VGPR spills).
-// 2 waves/SIMD (4 instances per CU, LDS-bound) at the price of 688 B/lane of
-// scratch spills: 6.41 -> 4.10 ms per update at batch 65,536 (C4 134.4 -> 136.6M)
+// 2 waves/SIMD (4 instances per CU, LDS-bound): 6.41 -> 4.10 ms per update at
+// batch 65,536 when introduced (688 B/lane of scratch then; 24 B/lane since the
+// per-model / per-apply_delta instantiation, 2.44 ms per update)
 #ifndef UWVK_EFF_ATTR
 #define UWVK_EFF_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
