@@ -101,6 +101,9 @@ def parse():
     ap.add_argument("--vel-groups", type=int, default=-1, help="C2: -1 auto, 0 lane per filter, 1 16-lane rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true", help="literal kernels (all 2n+1 sigma points)")
+    ap.add_argument("--so3-right", action="store_true",
+                    help="UWVK_OPT_SO3_RIGHT: the body-frame SO3 boxplus q exp(d) (classic MTK) instead of the "
+                         "nav-frame exp(d) q; the PSP kernels' SR = 1 instantiations (DESIGN.md 4.3)")
     ap.add_argument("--tail-chunks", type=int, default=0,
                     help="UWVK_OPT_TAIL_CHUNKS (diagnostic A/B): force this many chunks per tail instance, 0 = planner")
     ap.add_argument("--persist", type=int, default=-1,
@@ -191,13 +194,16 @@ def initialise(f, log, cfg, uwv, init, first_instance=0):
     del x, P
 
 
-def cpu_baseline(synth, cfg, uwv, mode, dof, threads, init="mc"):
+def cpu_baseline(synth, cfg, uwv, mode, dof, threads, init="mc", right=False):
     """The fp64 C oracle's timing build (oracle/liboracle_fast.so: -O3,
     x86-64-v4, one instance per task, pthreads) on a bounded sample of the same
     workload, on every core this process may use; plus one instance on one
     core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as O
+    if right:  # the oracle's switch is process-wide: the whole sample on the right side
+        with O.so3_right():
+            return cpu_baseline(synth, cfg, uwv, mode, dof, threads, init, right=False)
     epochs = 2000
     # single core first: it sizes the multi-core sample to ~15 s of wall time
     log1 = synth.make_pose_log(1, epochs, mode=mode, dof=dof)
@@ -377,6 +383,19 @@ def make_rccl(dist, engine, world, rank, local):
     return None, err
 
 
+def collective_desc(dist, world, comm, comm_err, same_dev):
+    """config.collective of the bench line: which all-reduce summed the
+    ensemble statistics (None for a single-process run)."""
+    if dist is None or world == 1:
+        return None
+    if comm is not None:
+        return "RCCL all_reduce of the ensemble statistics on the handle's stream (uwvk_pose_ensemble_allreduce)"
+    if comm_err is not None:
+        return "gloo all_reduce of the ensemble statistics (host): the RCCL communicator failed (%s)" % comm_err
+    return "gloo all_reduce of the ensemble statistics (host)%s" % (
+        ": RCCL refuses two ranks on one GPU (UWVK_BENCH_SAME_DEVICE rehearsal)" if same_dev else "")
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -403,6 +422,8 @@ def main():
         f.set_tail_chunks(a.tail_chunks)
     if a.dense:
         f.set_dense_sigma(True)
+    if a.so3_right:
+        f.set_so3_right(True)
     initialise(f, log, cfg, uwv, a.init, first_instance=rank * B)
     f.set_process_noise_from_config(cfg, log["dt"])
     dlog = f.upload_log(log)
@@ -499,8 +520,9 @@ def main():
     # the PSP instantiation run (uwvk_psp_k.hip launch_epoch_dof): Q shape, and
     # 1 when the window holds no pressure / ADCP epoch (0x4 | 0x8)
     evs = 0 if (f.epoch_qshape() != 1 or bool(((window & 0xC) != 0).any())) else 1
-    kname = ("k_pose_epoch<%d>" % a.dof) if a.dense else ("k_psp_epoch<%d, %d, %d>" % (a.dof, f.epoch_qshape(), evs))
-    workload = "%s-dof%d-b%d%s" % (log_mode, a.dof, B, "-dense" if a.dense else "")
+    sr = 1 if a.so3_right else 0
+    kname = ("k_pose_epoch<%d>" % a.dof) if a.dense else ("k_psp_epoch<%d, %d, %d, %d>" % (a.dof, f.epoch_qshape(), evs, sr))
+    workload = "%s-dof%d-b%d%s%s" % (log_mode, a.dof, B, "-dense" if a.dense else "", "-right" if sr else "")
     pmc = pmc_entry(workload, a.steps)
     cr = None if a.dense or launches != 1 else counter_roofline(pmc, B, a.steps, kernel_ms)
     traffic = pmc.get("bytes_per_launch") if pmc.get("epochs_per_launch") == a.steps and launches == 1 else None
@@ -536,15 +558,7 @@ def main():
     else:
         desc = "%s: PoseUKF %d-DOF, batch %d per GPU, 1 kHz IMU + 5 Hz DVL%s" % (
             mode, a.dof, B, " + ADCP x4 + DVL drop-out/efforts + pressure" if mode == "C4" else "")
-    if dist is None or world == 1:
-        coll_desc = None
-    elif comm is not None:
-        coll_desc = "RCCL all_reduce of the ensemble statistics on the handle's stream (uwvk_pose_ensemble_allreduce)"
-    elif comm_err is not None:
-        coll_desc = "gloo all_reduce of the ensemble statistics (host): the RCCL communicator failed (%s)" % comm_err
-    else:
-        coll_desc = "gloo all_reduce of the ensemble statistics (host)%s" % (
-            ": RCCL refuses two ranks on one GPU (UWVK_BENCH_SAME_DEVICE rehearsal)" if same_dev else "")
+    coll_desc = collective_desc(dist, world, comm, comm_err, same_dev)
     out = {
         "metric": METRIC, "value": value, "unit": "steps/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak",
@@ -563,6 +577,7 @@ def main():
                             "sd %g m/s), second constructor" % (list(synth.MC_ROT_SD), synth.MC_VEL_SD))
                            if a.init == "mc" else "first constructor (prior from the config)",
                    "path": "dense (all 2n+1 sigma points)" if a.dense else "PSP (partitioned sigma points)",
+                   "so3_boxplus": "right (body frame, q exp(d))" if a.so3_right else "left (nav frame, exp(d) q)",
                    "kernel": kname},
         "collective_check": coll_check,
         "roofline": roof,
@@ -572,7 +587,7 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(synth, cfg, uwv, log_mode, a.dof, a.cpu_threads or available_cores(),
-                                           a.init)
+                                           a.init, right=a.so3_right)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

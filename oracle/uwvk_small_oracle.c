@@ -24,7 +24,9 @@
 #define SM_NPTS (2 * SM_MAXN + 1)
 #define SM_MAXSEG 8
 
-enum { SEG_V = 0, SEG_SO3 = 1, SEG_S2 = 2 };
+/* SEG_SO3R: an SO3 segment with the body-frame (right) [+]/[-], q exp(d) and
+ * log(b^-1 a): the PoseUKF visual update's segments under or_set_so3_right(1) */
+enum { SEG_V = 0, SEG_SO3 = 1, SEG_S2 = 2, SEG_SO3R = 3 };
 
 typedef struct sm_manifold {
   int nseg, dof, store;
@@ -33,9 +35,9 @@ typedef struct sm_manifold {
 
 static void sm_add(sm_manifold* M, int kind, int dim) {
   M->kind[M->nseg] = kind;
-  M->dim[M->nseg] = kind == SEG_V ? dim : (kind == SEG_SO3 ? 3 : 2);
+  M->dim[M->nseg] = kind == SEG_V ? dim : (kind == SEG_S2 ? 2 : 3);
   M->dof += M->dim[M->nseg];
-  M->store += kind == SEG_V ? dim : (kind == SEG_SO3 ? 4 : 3);
+  M->store += kind == SEG_V ? dim : (kind == SEG_S2 ? 3 : 4);
   M->nseg++;
 }
 
@@ -83,10 +85,11 @@ static void sm_boxplus(const sm_manifold* M, const double* x, const double* d, d
     if (M->kind[g] == SEG_V) {
       for (int k = 0; k < M->dim[g]; k++) tmp[si + k] = x[si + k] + s * d[di + k];
       si += M->dim[g];
-    } else if (M->kind[g] == SEG_SO3) {
+    } else if (M->kind[g] == SEG_SO3 || M->kind[g] == SEG_SO3R) {
       double v[3] = {s * d[di], s * d[di + 1], s * d[di + 2]}, e[4];
       or_so3_exp(v, e);
-      or_quat_mul(e, x + si, tmp + si);
+      if (M->kind[g] == SEG_SO3R) or_quat_mul(x + si, e, tmp + si);
+      else or_quat_mul(e, x + si, tmp + si);
       si += 4;
     } else {
       or_s2_boxplus(x + si, d + di, s, tmp + si);
@@ -103,9 +106,10 @@ static void sm_boxminus(const sm_manifold* M, const double* a, const double* b, 
     if (M->kind[g] == SEG_V) {
       for (int k = 0; k < M->dim[g]; k++) o[di + k] = a[si + k] - b[si + k];
       si += M->dim[g];
-    } else if (M->kind[g] == SEG_SO3) {
+    } else if (M->kind[g] == SEG_SO3 || M->kind[g] == SEG_SO3R) {
       double bc[4] = {b[si], -b[si + 1], -b[si + 2], -b[si + 3]}, r[4];
-      or_quat_mul(a + si, bc, r);
+      if (M->kind[g] == SEG_SO3R) or_quat_mul(bc, a + si, r);
+      else or_quat_mul(a + si, bc, r);
       or_so3_log(r, o + di);
       si += 4;
     } else {
@@ -530,11 +534,14 @@ int or_pose_update_visual(or_pose* f, int nf, const double* features, const doub
   if (!check_features(nf, features, feature_cov)) return UWVK_ENAN;
   int n = f->L.dof, s = f->L.store, na = n + 6;
   sm_manifold A = {0};
+  /* both SO3 segments take the PoseUKF side (or_set_so3_right): MTK has one
+   * SO3::boxplus, so the marker orientation follows the filter's */
+  const int so3 = or_get_so3_right() ? SEG_SO3R : SEG_SO3;
   sm_add(&A, SEG_V, 3);     /* position */
-  sm_add(&A, SEG_SO3, 3);   /* orientation */
+  sm_add(&A, so3, 3);       /* orientation */
   sm_add(&A, SEG_V, n - 6); /* velocity ... water_density */
   sm_add(&A, SEG_V, 3);     /* marker_position */
-  sm_add(&A, SEG_SO3, 3);   /* marker_orientation */
+  sm_add(&A, so3, 3);       /* marker_orientation */
   static __thread double amu[SM_MAXS], asig[SM_MAXN * SM_MAXN];
   memcpy(amu, f->mu, sizeof(double) * s);
   memcpy(amu + s, marker_pose, sizeof(double) * 7);

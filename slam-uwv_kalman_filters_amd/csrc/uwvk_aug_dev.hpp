@@ -22,13 +22,15 @@
 namespace uwvk {
 namespace aug {
 
-enum { SEG_V = 0, SEG_SO3 = 1, SEG_S2 = 2 };
+// SEG_SO3R: SO3 with the body-frame (right) [+] / [-], q exp(d) and log(b^-1 a)
+// (the PoseUKF visual update under UWVK_OPT_SO3_RIGHT); SEG_SO3 the nav-frame one
+enum { SEG_V = 0, SEG_SO3 = 1, SEG_S2 = 2, SEG_SO3R = 3 };
 
 template <int K, int D = 0>
 struct Seg {
   static constexpr int kind = K;
-  static constexpr int dof = K == SEG_V ? D : (K == SEG_SO3 ? 3 : 2);
-  static constexpr int store = K == SEG_V ? D : (K == SEG_SO3 ? 4 : 3);
+  static constexpr int dof = K == SEG_V ? D : (K == SEG_S2 ? 2 : 3);
+  static constexpr int store = K == SEG_V ? D : (K == SEG_S2 ? 3 : 4);
 };
 
 // ---- S2 [EXT MTK S2], DESIGN.md §3 item 11 ---------------------------------
@@ -77,10 +79,11 @@ UWVK_DEV void bplus(const double* x, const double* d, double s, double* o) {
   if constexpr (S0::kind == SEG_V) {
 #pragma unroll
     for (int k = 0; k < S0::dof; k++) o[SI + k] = x[SI + k] + s * d[DI + k];
-  } else if constexpr (S0::kind == SEG_SO3) {
+  } else if constexpr (S0::kind == SEG_SO3 || S0::kind == SEG_SO3R) {
     double v[3] = {s * d[DI], s * d[DI + 1], s * d[DI + 2]}, e[4], r[4];
     so3_exp(v, e);
-    qmul(e, x + SI, r);
+    if constexpr (S0::kind == SEG_SO3R) qmul(x + SI, e, r);
+    else qmul(e, x + SI, r);
 #pragma unroll
     for (int k = 0; k < 4; k++) o[SI + k] = r[k];
   } else {
@@ -101,6 +104,10 @@ UWVK_DEV void bminus(const double* a, const double* b, double* o) {
     for (int k = 0; k < S0::dof; k++) o[DI + k] = a[SI + k] - b[SI + k];
   } else if constexpr (S0::kind == SEG_SO3) {
     qboxminus(a + SI, b + SI, o + DI);
+  } else if constexpr (S0::kind == SEG_SO3R) {
+    double bc[4] = {b[SI], -b[SI + 1], -b[SI + 2], -b[SI + 3]}, r[4];
+    qmul(bc, a + SI, r);
+    so3_log(r, o + DI);
   } else {
     s2_boxminus(a + SI, b + SI, o + DI);
   }

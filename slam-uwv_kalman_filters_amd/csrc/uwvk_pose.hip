@@ -15,7 +15,7 @@
 #include "uwvk_aug_dev.hpp"
 
 namespace uwvk {
-hipError_t launch_pose_visual(int dof, hipStream_t st, const PoseBufs& b, const aug::VisArgs& va);
+hipError_t launch_pose_visual(int dof, int right, hipStream_t st, const PoseBufs& b, const aug::VisArgs& va);
 }
 
 #include <algorithm>
@@ -74,7 +74,9 @@ struct uwvk_pose {
 
 // literal (all 2n+1 sigma points) kernels requested?
 // (and the body-frame SO3 side, which only the literal kernels implement)
-static bool use_dense(const uwvk_pose* h) { return h->dense || h->sh.literal_apply_delta || h->sh.so3_right; }
+// the literal kernels: on request, or for ukfom's literal apply_delta re-spread
+// (the PSP kernels run both SO3 sides, sh.so3_right, since r04)
+static bool use_dense(const uwvk_pose* h) { return h->dense || h->sh.literal_apply_delta; }
 
 static PoseBufs bufs(const uwvk_pose* h) {
   PoseBufs b;
@@ -513,7 +515,7 @@ uwvk_status uwvk_pose_update_visual_landmark(uwvk_pose* h, int32_t n_features, c
     (void)hipStreamSynchronize(h->stream);
     return (uwvk_status)st;
   }
-  const hipError_t e = launch_pose_visual(h->dof, h->stream, bufs(h), va);
+  const hipError_t e = launch_pose_visual(h->dof, h->sh.so3_right, h->stream, bufs(h), va);
   if (hipStreamSynchronize(h->stream) != hipSuccess || e != hipSuccess) return UWVK_EDEVICE;
   return UWVK_OK;
 }
@@ -778,6 +780,7 @@ uwvk_status uwvk_pose_ensemble_allreduce(uwvk_pose* h, const double* truth, doub
   StatTruth t{};  // by value in the kernel arguments: no upload in front of the kernel
   if (truth) std::memcpy(t.v, truth, s * 8);
   else t.v[3] = 1.0;
+  t.right = h->sh.so3_right;
   // ensemble partials after the rotation-rate area: d_scratch + 256 + 3 batch
   double* d_part = h->d_scratch + 256 + 3 * h->batch;
   PoseBufs b = bufs(h);

@@ -83,6 +83,7 @@ hipError_t launch_pose_rotation_rate(int dof, hipStream_t st, const PoseBufs& b,
 // the truth store-vector of the ensemble statistics, passed by value (kernarg)
 struct StatTruth {
   double v[54];
+  int right;  // the handle's SO3 side (UWVK_OPT_SO3_RIGHT): orientation error log(t^-1 q), else log(q t^-1)
 };
 // part: ceil(batch / 64) x (3 store + 2) doubles of device scratch
 hipError_t launch_pose_stats(int dof, hipStream_t st, const PoseBufs& b, const StatTruth& truth, double* out,
@@ -481,7 +482,7 @@ __global__ __launch_bounds__(64) void k_pose_stats(PoseBufs b, StatTruth truth, 
     const double* x = xs + l * S;
     const double* P = b.sigma + (i0 + l) * (int64_t)tri_n<DOF>();
     double r[3];
-    qboxminus(x + 3, tv + 3, r);
+    qboxminus_side(x + 3, tv + 3, r, truth.right);  // the error in the covariance's frame
     // NEES over (position, orientation, velocity): e^T P_sub^-1 e via a 9x9 Cholesky solve
     double err[9];
     for (int k = 0; k < 3; k++) { err[k] = x[k] - tv[k]; err[3 + k] = r[k]; err[6 + k] = x[7 + k] - tv[7 + k]; }

@@ -15,13 +15,16 @@ namespace uwvk {
 
 namespace {
 
-template <int DOF>
-using PoseMarkerM = aug::Manifold<aug::Seg<aug::SEG_V, 3>, aug::Seg<aug::SEG_SO3>, aug::Seg<aug::SEG_V, DOF - 6>,
-                                  aug::Seg<aug::SEG_V, 3>, aug::Seg<aug::SEG_SO3>>;
+// SR: the handle's SO3 side (UWVK_OPT_SO3_RIGHT); both SO3 segments follow it
+// (MTK has one SO3::boxplus, so the marker orientation takes the filter's side)
+template <int DOF, int SR>
+using PoseMarkerM = aug::Manifold<aug::Seg<aug::SEG_V, 3>, aug::Seg<SR ? aug::SEG_SO3R : aug::SEG_SO3>,
+                                  aug::Seg<aug::SEG_V, DOF - 6>, aug::Seg<aug::SEG_V, 3>,
+                                  aug::Seg<SR ? aug::SEG_SO3R : aug::SEG_SO3>>;
 
-template <int DOF>
-__global__ __launch_bounds__(aug::Engine<PoseMarkerM<DOF>>::BLOCK) void k_pose_visual(PoseBufs b, aug::VisArgs va) {
-  using E = aug::Engine<PoseMarkerM<DOF>>;
+template <int DOF, int SR>
+__global__ __launch_bounds__((aug::Engine<PoseMarkerM<DOF, SR>>::BLOCK)) void k_pose_visual(PoseBufs b, aug::VisArgs va) {
+  using E = aug::Engine<PoseMarkerM<DOF, SR>>;
   static_assert(E::IPB == 1, "one instance per workgroup");
   constexpr int n = DOF, na = E::n, S = Lay<DOF>::store;
   __shared__ double smem[E::words];
@@ -58,12 +61,18 @@ __global__ __launch_bounds__(aug::Engine<PoseMarkerM<DOF>>::BLOCK) void k_pose_v
 
 }  // namespace
 
-hipError_t launch_pose_visual(int dof, hipStream_t st, const PoseBufs& b, const aug::VisArgs& va) {
+template <int SR>
+static void launch_pose_visual_sr(int dof, hipStream_t st, const PoseBufs& b, const aug::VisArgs& va) {
   const dim3 g((unsigned)b.batch);
   if (dof == 53)
-    hipLaunchKernelGGL(k_pose_visual<53>, g, dim3(aug::Engine<PoseMarkerM<53>>::BLOCK), 0, st, b, va);
+    hipLaunchKernelGGL((k_pose_visual<53, SR>), g, dim3(aug::Engine<PoseMarkerM<53, SR>>::BLOCK), 0, st, b, va);
   else
-    hipLaunchKernelGGL(k_pose_visual<26>, g, dim3(aug::Engine<PoseMarkerM<26>>::BLOCK), 0, st, b, va);
+    hipLaunchKernelGGL((k_pose_visual<26, SR>), g, dim3(aug::Engine<PoseMarkerM<26, SR>>::BLOCK), 0, st, b, va);
+}
+
+hipError_t launch_pose_visual(int dof, int right, hipStream_t st, const PoseBufs& b, const aug::VisArgs& va) {
+  if (right) launch_pose_visual_sr<1>(dof, st, b, va);
+  else launch_pose_visual_sr<0>(dof, st, b, va);
   return hipGetLastError();
 }
 

@@ -3,6 +3,27 @@
 #include "uwvk_pose_kernels.hpp"
 
 namespace uwvk {
+// Per-side launchers (SR = 0 nav-frame / left, 1 body-frame / right SO3 [+]),
+// each instantiated in one object: uwvk_psp_k.hip (0) and uwvk_psp_k_r.hip (1).
+template <int SR>
+hipError_t launch_psp_predict_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt);
+template <int SR>
+hipError_t launch_psp_update_sr(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                                const MeasArgs& ma, int m);
+template <int SR>
+hipError_t launch_psp_epoch_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
+                               int64_t grid, uint32_t ev_any);
+extern template hipError_t launch_psp_predict_sr<0>(int, hipStream_t, const PoseBufs&, const PoseShared&, double);
+extern template hipError_t launch_psp_predict_sr<1>(int, hipStream_t, const PoseBufs&, const PoseShared&, double);
+extern template hipError_t launch_psp_update_sr<0>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
+                                                   const MeasArgs&, int);
+extern template hipError_t launch_psp_update_sr<1>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
+                                                   const MeasArgs&, int);
+extern template hipError_t launch_psp_epoch_sr<0>(int, hipStream_t, const PoseBufs&, const PoseShared&,
+                                                  const EpochArgs&, int64_t, uint32_t);
+extern template hipError_t launch_psp_epoch_sr<1>(int, hipStream_t, const PoseBufs&, const PoseShared&,
+                                                  const EpochArgs&, int64_t, uint32_t);
+// the handle's side (sh.so3_right) picks the launcher
 hipError_t launch_psp_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt);
 hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                              const MeasArgs& ma, int m);

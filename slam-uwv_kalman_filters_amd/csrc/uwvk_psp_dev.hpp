@@ -22,6 +22,16 @@
 // literal spread to rounding (parity tests run both paths against the oracle).
 // The literal path (uwvk_pose_dev.hpp) stays selectable: UWVK_OPT_DENSE_SIGMA.
 //
+// Both SO3 sides (template parameter SR, UWVK_OPT_SO3_RIGHT).  Nothing above
+// depends on which side the orientation [+] multiplies: a point with a zero
+// orientation component is mu on that block under q exp(0) and exp(0) q alike,
+// so the points j >= k still agree with mu on every non-affine DOF, and the
+// models' affine Jacobians do not involve the orientation.  The side enters
+// only where a quaternion is combined: the 2k points' orientation, the process
+// model's orientation step, the manifold mean and the deviations (qplus_psp /
+// qboxminus_psp), and apply_delta's T (R(exp d) on the left, R(exp d)^T on the
+// right; see psp_update).
+//
 // Execution: one wavefront (64 lanes) per filter instance, Sigma packed
 // (lower triangle, row i at i(i+1)/2) in LDS for the whole multi-epoch run.
 #pragma once
@@ -214,9 +224,20 @@ UWVK_DEV void so3_log_psp(const double q[4], double o[3]) {
     else so3_log(q, o);
   }
 }
+// SO3 [+] / [-] of side SR (a template parameter of every PSP kernel, DESIGN.md
+// section 4.3): SR = 0 nav-frame (left), q [+] v = exp(v) q, a [-] b = log(a b^-1);
+// SR = 1 body-frame (right, classic MTK SO3::boxplus), q [+] v = q exp(v),
+// a [-] b = log(b^-1 a).  e = exp(v) is passed in.  The oracle's or_set_so3_right.
+template <int SR>
+UWVK_DEV void qplus_psp(const double e[4], const double q[4], double o[4]) {
+  if constexpr (SR) qmul(q, e, o);
+  else qmul(e, q, o);
+}
+template <int SR>
 UWVK_DEV void qboxminus_psp(const double a[4], const double b[4], double o[3]) {
   double bc[4] = {b[0], -b[1], -b[2], -b[3]}, r[4];
-  qmul(a, bc, r);
+  if constexpr (SR) qmul(bc, a, r);
+  else qmul(a, bc, r);
   so3_log_psp(r, o);
 }
 
@@ -452,7 +473,7 @@ UWVK_DEV constexpr bool has_rot() {
     if (RL::rows[q] >= 3 && RL::rows[q] < 6) return true;
   return false;
 }
-template <class RL, int DOF, int K>
+template <class RL, int DOF, int K, int SR>
 UWVK_DEV void gen_rows(const double* mu, const double* stg, int p, double x[Lay<DOF>::store]) {
   using L = Lay<DOF>;
 #pragma unroll
@@ -466,7 +487,7 @@ UWVK_DEV void gen_rows(const double* mu, const double* stg, int p, double x[Lay<
     if constexpr (has_rot<RL>()) {
       double e[4];
       so3_exp_psp(v, e);
-      qmul(e, mu + L::s_quat, x + L::s_quat);
+      qplus_psp<SR>(e, mu + L::s_quat, x + L::s_quat);
     }
   }
 }
@@ -475,7 +496,7 @@ UWVK_DEV void gen_rows(const double* mu, const double* stg, int p, double x[Lay<
 // Process model pieces (PoseUKF.cpp:12-84), bitwise the same expressions as
 // process_point() in uwvk_pose_dev.hpp.
 // ---------------------------------------------------------------------------
-template <int DOF>
+template <int DOF, int SR>
 UWVK_DEV void proc_orientation(const double x[Lay<DOF>::store], const PoseShared& sh, const ProcCtx& c, double o[4]) {
   using L = Lay<DOF>;
   // sin / cos of lat = lat0 + x / R_M by angle addition from lat0 (Taylor in
@@ -501,7 +522,7 @@ UWVK_DEV void proc_orientation(const double x[Lay<DOF>::store], const PoseShared
   for (int i = 0; i < 3; i++) wn[i] = (wn[i] - er[i]) * c.dt;
   double e[4];
   so3_exp_psp(wn, e);
-  qmul(e, x + L::s_quat, o);
+  qplus_psp<SR>(e, x + L::s_quat, o);  // new_state.orientation.boxplus (PoseUKF.cpp:32)
 }
 
 // storage component s (not orientation) of f(mu)
@@ -635,7 +656,7 @@ UWVK_DEV LaneQ lane_q(const double* fq, int l) {
 // (sh.q_simple: lane-resident band <= 2), 2 known general.  The epoch kernel is
 // instantiated for 1 and 2 and the host picks one: with both branches in one
 // kernel the epoch loop ran 0.7-0.8% slower (profiles/r03/qm/).
-template <int DOF, int QM = 0>
+template <int DOF, int QM = 0, int SR = 0>
 UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q,
                           const double* fq, double& ds, double& ids, const LaneQ& lq,
                           Stamper* st = nullptr) {
@@ -682,11 +703,11 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   double o[4];
   {
     double x[L::store];
-    gen_rows<PredRows, DOF, K>(sm.mu, sm.stg + STG_ROWS, l, x);
+    gen_rows<PredRows, DOF, K, SR>(sm.mu, sm.stg + STG_ROWS, l, x);
 #if PSP_ABL & 16
     for (int i = 0; i < 4; i++) o[i] = x[3 + i];
 #else
-    proc_orientation<DOF>(x, sh, pc, o);
+    proc_orientation<DOF, SR>(x, sh, pc, o);
 #endif
   }
   PSP_PHASE(21);
@@ -700,7 +721,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     double nrm;
     do {
       double d[3];
-      qboxminus_psp(o, mq, d);
+      qboxminus_psp<SR>(o, mq, d);
       const double w = pt ? 1.0 : (ctr ? wc : 0.0);
       nrm = 0.0;
 #pragma unroll
@@ -714,7 +735,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       }
       double e[4], q[4];
       so3_exp_psp(d, e);
-      qmul(e, mq, q);
+      qplus_psp<SR>(e, mq, q);
 #pragma unroll
       for (int i = 0; i < 4; i++) mq[i] = q[i];
 #if PSP_FAST & 2
@@ -727,7 +748,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   PSP_PHASE(22);
   // deviations; ori x ori block; Delta_j = d_{j+} - d_{j-}
   double d[3];
-  qboxminus_psp(o, mq, d);
+  qboxminus_psp<SR>(o, mq, d);
   double oo[6];
   {
     const double w = pt ? 1.0 : (ctr ? wc : 0.0);
@@ -1503,7 +1524,7 @@ UWVK_DEV double hfma(double h, double x, double acc) {
 // ukf::update [EXT], PSP form.  gate: 0 accept any, 1 d2p95.  Returns the gate
 // decision; *ok = false on a non-positive pivot of the partial Cholesky.
 // ---------------------------------------------------------------------------
-template <int DOF, class HM>
+template <int DOF, int SR, class HM>
 UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const double (&Rm)[HM::M * HM::M], int gate,
                          const HM& hm, bool* ok, double ds, double ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
@@ -1524,7 +1545,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double zp[M];
   {
     double x[L::store];
-    gen_rows<HM, DOF, K>(sm.mu, sm.stg + STG_ROWS, l, x);
+    gen_rows<HM, DOF, K, SR>(sm.mu, sm.stg + STG_ROWS, l, x);
     hm.eval(x, zp);
   }
   double zc[M], zb[M], e[M];
@@ -1849,13 +1870,22 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
 #endif
   psync();
   PSP_PHASE(34);
-  // apply_delta, exact nav-frame form: mu <- mu [+] delta, Sigma <- T Sigma T^T
+  // apply_delta, exact form: mu <- mu [+] delta, Sigma <- T Sigma T^T with T
+  // the identity except on the orientation block.  ukfom re-spreads X_p =
+  // mu [+] +-L_j, shifts every point by delta and takes the deviations from
+  // mu [+] delta; on the orientation block that deviation is, for the left
+  // side, log(exp(d) exp(l) q q^-1 exp(-d)) = R(exp d) l, and for the right
+  // side log(exp(-d) q^-1 q exp(l) exp(d)) = R(exp d)^T l (conjugation), so
+  // T = R(exp d) (SR = 0) or R(exp d)^T = R(exp(d)^-1) (SR = 1); the vector
+  // deviations are L_j unchanged.  The weights (1/2 over the 2n points) give
+  // T L L^T T^T exactly.
   {
     const double dv[3] = {readlane_d(dl, 3), readlane_d(dl, 4), readlane_d(dl, 5)};
     double R[9];
     {
       double eq[4];
       so3_exp_psp(dv, eq);
+      if constexpr (SR) eq[1] = -eq[1], eq[2] = -eq[2], eq[3] = -eq[3];
       qmatrix(eq, R);
     }
     // rows 3..5 of every column j outside the block
@@ -1893,7 +1923,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     {
       double eq[4];
       so3_exp_psp(dv, eq);
-      qmul(eq, sm.mu + L::s_quat, qn);
+      qplus_psp<SR>(eq, sm.mu + L::s_quat, qn);
     }
     psync();
     if (l < 9 && (l / 3) >= (l % 3)) sm.S[pidx(3 + l / 3, 3 + l % 3)] = nb;

@@ -11,7 +11,20 @@
 // spreading (EpochArgs::chunks > 1, plan_tail below) the last instances of
 // each XCD run as a few epoch chunks, one block each, handed on in order.
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <vector>
+
+// PSP_SIDE: the SO3 side this translation unit instantiates the kernels for
+// (0 here; uwvk_psp_k_r.hip includes this file with 1).  The two sides are
+// separate objects so the build parallelises; the host dispatchers, the
+// placement probe and the occupancy helpers live in the side-0 object.
+#ifndef PSP_SIDE
+#define PSP_SIDE 0
+#endif
+#if PSP_SIDE != 0
+#undef UWVK_TIMELINE  // the per-wave timeline buffer is the side-0 object's
+#endif
 
 #define UWVK_POSE_KERNEL_BODIES
 #include "uwvk_pose_kernels.hpp"
@@ -173,32 +186,32 @@ UWVK_DEV void copy_zr(const double* zin, const double* Rin, double (&z)[M], doub
   for (int k = 0; k < M * M; k++) R[k] = Rin[k];
 }
 
-// one measurement update of kind KIND on instance inst (PSP form)
-template <int DOF, int KIND>
+// one measurement update of kind KIND on instance inst (PSP form, SO3 side SR)
+template <int DOF, int KIND, int SR>
 UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, const double* zin, const double* Rin,
                         const MeasArgs& ma, bool* ok, double ds, double ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   if constexpr (KIND == MK_ACC) {
     double z[3], R[9];
     copy_zr<3>(zin, Rin, z, R);
-    return psp_update<DOF>(sm, z, R, 0, PAcc<DOF>{}, ok, ds, ids, st);
+    return psp_update<DOF, SR>(sm, z, R, 0, PAcc<DOF>{}, ok, ds, ids, st);
   } else if constexpr (KIND == MK_VEL) {
     double z[3], R[9];
     copy_zr<3>(zin, Rin, z, R);
-    return psp_update<DOF>(sm, z, R, 0, PVel<DOF>{}, ok, ds, ids, st);
+    return psp_update<DOF, SR>(sm, z, R, 0, PVel<DOF>{}, ok, ds, ids, st);
   } else if constexpr (KIND == MK_PRESSURE) {
     double z[1], R[1];
     copy_zr<1>(zin, Rin, z, R);
     PPressure<DOF> h;
     h.h.s[0] = ma.v3[0]; h.h.s[1] = ma.v3[1]; h.h.s[2] = ma.v3[2];
     h.h.patm = sh.p.atmospheric_pressure;
-    return psp_update<DOF>(sm, z, R, 0, h, ok, ds, ids, st);
+    return psp_update<DOF, SR>(sm, z, R, 0, h, ok, ds, ids, st);
   } else if constexpr (KIND == MK_WATER) {
     double z[2], R[4];
     copy_zr<2>(zin, Rin, z, R);
     PWater<DOF> h;
     h.cw = ma.extra ? ma.extra[inst] : 0.0;
-    return psp_update<DOF>(sm, z, R, 1, h, ok, ds, ids, st);
+    return psp_update<DOF, SR>(sm, z, R, 1, h, ok, ds, ids, st);
   } else if constexpr (KIND == MK_XY || KIND == MK_GEO || KIND == MK_DELAYED) {
     double z[2], R[4];
     copy_zr<2>(zin, Rin, z, R);
@@ -216,16 +229,16 @@ UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, co
       z[0] = zin[0] + (sm.mu[L::s_pos] - ma.extra[2 * inst]);
       z[1] = zin[1] + (sm.mu[L::s_pos + 1] - ma.extra[2 * inst + 1]);
     }
-    return psp_update<DOF>(sm, z, R, gate, PXY<DOF>{}, ok, ds, ids, st);
+    return psp_update<DOF, SR>(sm, z, R, gate, PXY<DOF>{}, ok, ds, ids, st);
   } else {
     static_assert(KIND == MK_Z, "PSP update kind");
     double z[1], R[1];
     copy_zr<1>(zin, Rin, z, R);
-    return psp_update<DOF>(sm, z, R, 0, PZ<DOF>{}, ok, ds, ids, st);
+    return psp_update<DOF, SR>(sm, z, R, 0, PZ<DOF>{}, ok, ds, ids, st);
   }
 }
 
-template <int DOF>
+template <int DOF, int SR>
 __global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, double dt) {
   __shared__ PspSmem<DOF> sm;
   const int64_t inst = xcd_instance(b.batch);
@@ -237,13 +250,13 @@ __global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, d
   lane_proc<DOF>(b, sh, inst, lane_id(), pc);
   double ds = 1.0, ids = 1.0;
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
-  const bool ok = psp_predict<DOF>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq);
+  const bool ok = psp_predict<DOF, 0, SR>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq);
   if (!ok && lane_id() == 0) b.status[inst] |= UWVK_ST_NOTPD;
   psp_fold<DOF>(sm, ds, ids);
   store_psp<DOF>(sm, b, inst);
 }
 
-template <int DOF, int KIND>
+template <int DOF, int KIND, int SR>
 __global__ __launch_bounds__(64) void k_psp_update(PoseBufs b, PoseShared sh, MeasArgs ma, int m) {
   __shared__ PspSmem<DOF> sm;
   const int64_t inst = xcd_instance(b.batch);
@@ -262,7 +275,7 @@ __global__ __launch_bounds__(64) void k_psp_update(PoseBufs b, PoseShared sh, Me
   }
   load_psp<DOF>(sm, b, inst);
   bool ok = true;
-  const bool acc = do_update<DOF, KIND>(sm, sh, inst, z, R, ma, &ok, 1.0, 1.0);
+  const bool acc = do_update<DOF, KIND, SR>(sm, sh, inst, z, R, ma, &ok, 1.0, 1.0);
   if (lane_id() == 0) {
     if (!ok) b.status[inst] |= UWVK_ST_NOTPD;
     if (ma.accepted) ma.accepted[inst] = acc ? 1 : 0;
@@ -344,7 +357,7 @@ struct PspPre {
   bool have;
 };
 
-template <int DOF, bool PERSIST, int QM, int EVS, class Again>
+template <int DOF, bool PERSIST, int QM, int EVS, int SR, class Again>
 UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea, const TailUnit& tu0,
                        const LaneQ& lq, Again again, int64_t tlw, int lp, uint32_t* next = nullptr,
                        PspPre<DOF>* pre = nullptr) {
@@ -480,14 +493,14 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     }
 #endif
     if (!PSP_DIAG_HOT && ((e - ea.first) & 1023) == 1023) psp_fold<DOF>(sm, ds, ids);  // keep d in range
-    bool sok = psp_predict<DOF, QM>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, st);
+    bool sok = psp_predict<DOF, QM, SR>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, st);
     ok = ok && sok;
 #if PSP_FETCH_LATE  // the next epoch's inputs issued after the predict: a shorter live range
     if (e + 1 < e_end) fetch(e + 1);
 #endif
     if (fl & UWVK_EV_ACC) {
       if (all_finite(za, 3)) {
-        do_update<DOF, MK_ACC>(sm, sh, inst, za, sh.log_acc_cov, ma, &sok, ds, ids, st);
+        do_update<DOF, MK_ACC, SR>(sm, sh, inst, za, sh.log_acc_cov, ma, &sok, ds, ids, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -497,7 +510,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + inst) * 3;
       if (all_finite(z, 3)) {
-        cnt[0] += do_update<DOF, MK_VEL>(sm, sh, inst, z, sh.log_dvl_cov, ma, &sok, ds, ids, st);
+        cnt[0] += do_update<DOF, MK_VEL, SR>(sm, sh, inst, z, sh.log_dvl_cov, ma, &sok, ds, ids, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -510,7 +523,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     if (fl & UWVK_EV_PRESSURE) {
       const double* z = ea.pressure + (int64_t)ea.p_index[e] * B + inst;
       if (all_finite(z, 1)) {
-        cnt[1] += do_update<DOF, MK_PRESSURE>(sm, sh, inst, z, &ea.p_cov, ma, &sok, ds, ids);
+        cnt[1] += do_update<DOF, MK_PRESSURE, SR>(sm, sh, inst, z, &ea.p_cov, ma, &sok, ds, ids);
         ok = ok && sok;
       } else {
         nan = true;
@@ -523,7 +536,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
         double zz[2] = {z[0], z[1]}, R[4] = {ea.adcp_cov[0], ea.adcp_cov[1], ea.adcp_cov[2], ea.adcp_cov[3]};
         PWater<DOF> h;
         h.cw = ea.cw[c];
-        cnt[2] += psp_update<DOF>(sm, zz, R, 1, h, &sok, ds, ids);
+        cnt[2] += psp_update<DOF, SR>(sm, zz, R, 1, h, &sok, ds, ids);
         ok = ok && sok;
       }
     }
@@ -581,7 +594,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
 #endif
 }
 
-template <int DOF, int QM, int EVS>
+template <int DOF, int QM, int EVS, int SR>
 __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const int64_t B = b.batch;
@@ -592,7 +605,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
     return;
   }
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
-  psp_unit<DOF, false, QM, EVS>(sm, b, ea, tu, lq, [&] { return tail_unit(ea, B); }, blockIdx.x, lane_id());
+  psp_unit<DOF, false, QM, EVS, SR>(sm, b, ea, tu, lq, [&] { return tail_unit(ea, B); }, blockIdx.x, lane_id());
 }
 
 // Persistent form (UWVK_OPT_PERSIST): as many blocks as are resident, each
@@ -603,7 +616,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
 // dispatch-order assumption.  Faster XCDs / CUs take more units, and a slot
 // moves to its next unit without a new workgroup dispatch.  The next ticket is
 // taken while the current unit runs (its atomic latency hidden).
-template <int DOF, int QM, int EVS>
+template <int DOF, int QM, int EVS, int SR>
 __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
@@ -631,7 +644,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, P
     } else {
       // a laundered lane id: the unit's per-lane constants are recomputed per
       // unit, not hoisted out of the unit loop (held live across it)
-      psp_unit<DOF, true, QM, EVS>(sm, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(), &vn, &pre);
+      psp_unit<DOF, true, QM, EVS, SR>(sm, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(), &vn, &pre);
       u = vn;  // resolved by psp_unit
     }
     psync();  // the next unit's LDS writes after this unit's reads
@@ -640,46 +653,48 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, P
 
 }  // namespace psp
 
-template <int DOF>
+template <int DOF, int SR>
 static hipError_t psp_update_dof(int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                                  const MeasArgs& ma, int m) {
   const dim3 g((unsigned)b.batch), t(64);
   switch (kind) {
-    case MK_ACC: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_ACC>), g, t, 0, st, b, sh, ma, m); break;
-    case MK_VEL: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_VEL>), g, t, 0, st, b, sh, ma, m); break;
-    case MK_PRESSURE: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_PRESSURE>), g, t, 0, st, b, sh, ma, m); break;
-    case MK_WATER: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_WATER>), g, t, 0, st, b, sh, ma, m); break;
-    case MK_XY: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_XY>), g, t, 0, st, b, sh, ma, m); break;
-    case MK_Z: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_Z>), g, t, 0, st, b, sh, ma, m); break;
-    case MK_GEO: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_GEO>), g, t, 0, st, b, sh, ma, m); break;
-    case MK_DELAYED: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_DELAYED>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_ACC: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_ACC, SR>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_VEL: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_VEL, SR>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_PRESSURE: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_PRESSURE, SR>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_WATER: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_WATER, SR>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_XY: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_XY, SR>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_Z: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_Z, SR>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_GEO: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_GEO, SR>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_DELAYED: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_DELAYED, SR>), g, t, 0, st, b, sh, ma, m); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t launch_psp_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt) {
+template <int SR>
+hipError_t launch_psp_predict_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt) {
   if (dof == 53)
-    hipLaunchKernelGGL(psp::k_psp_predict<53>, dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, dt);
+    hipLaunchKernelGGL((psp::k_psp_predict<53, SR>), dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, dt);
   else
-    hipLaunchKernelGGL(psp::k_psp_predict<26>, dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, dt);
+    hipLaunchKernelGGL((psp::k_psp_predict<26, SR>), dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, dt);
   return hipGetLastError();
 }
 
-hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
-                             const MeasArgs& ma, int m) {
-  return dof == 53 ? psp_update_dof<53>(kind, st, b, sh, ma, m) : psp_update_dof<26>(kind, st, b, sh, ma, m);
+template <int SR>
+hipError_t launch_psp_update_sr(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                                const MeasArgs& ma, int m) {
+  return dof == 53 ? psp_update_dof<53, SR>(kind, st, b, sh, ma, m) : psp_update_dof<26, SR>(kind, st, b, sh, ma, m);
 }
 
-template <int DOF, int QM, int EVS>
+template <int DOF, int QM, int EVS, int SR>
 static void launch_epoch_q(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea, dim3 g) {
   if (ea.ticket)
-    hipLaunchKernelGGL((psp::k_psp_epoch_p<DOF, QM, EVS>), g, dim3(64), 0, st, b, sh, ea);
+    hipLaunchKernelGGL((psp::k_psp_epoch_p<DOF, QM, EVS, SR>), g, dim3(64), 0, st, b, sh, ea);
   else
-    hipLaunchKernelGGL((psp::k_psp_epoch<DOF, QM, EVS>), g, dim3(64), 0, st, b, sh, ea);
+    hipLaunchKernelGGL((psp::k_psp_epoch<DOF, QM, EVS, SR>), g, dim3(64), 0, st, b, sh, ea);
 }
 
-template <int DOF>
+template <int DOF, int SR>
 static void launch_epoch_dof(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea, dim3 g,
                              uint32_t ev_any) {
   // the kernel instantiated for the handle's process-noise shape (psp_predict
@@ -690,23 +705,50 @@ static void launch_epoch_dof(hipStream_t st, const PoseBufs& b, const PoseShared
 #define PSP_QM_SPLIT 1
 #endif
 #if !PSP_QM_SPLIT  // A/B: one kernel for every shape and event set (the r03k build)
-  launch_epoch_q<DOF, 0, 0>(st, b, sh, ea, g);
+  launch_epoch_q<DOF, 0, 0, SR>(st, b, sh, ea, g);
   (void)pa;
 #else
-  if (!sh.q_simple) launch_epoch_q<DOF, 2, 0>(st, b, sh, ea, g);
-  else if (pa) launch_epoch_q<DOF, 1, 0>(st, b, sh, ea, g);
-  else launch_epoch_q<DOF, 1, 1>(st, b, sh, ea, g);
+  if (!sh.q_simple) launch_epoch_q<DOF, 2, 0, SR>(st, b, sh, ea, g);
+  else if (pa) launch_epoch_q<DOF, 1, 0, SR>(st, b, sh, ea, g);
+  else launch_epoch_q<DOF, 1, 1, SR>(st, b, sh, ea, g);
 #endif
+}
+
+template <int SR>
+hipError_t launch_psp_epoch_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
+                               int64_t grid, uint32_t ev_any) {
+  const dim3 g((unsigned)(grid > 0 ? grid : b.batch));
+  if (dof == 53)
+    launch_epoch_dof<53, SR>(st, b, sh, ea, g, ev_any);
+  else
+    launch_epoch_dof<26, SR>(st, b, sh, ea, g, ev_any);
+  return hipGetLastError();
+}
+
+// this translation unit's side (uwvk_psp_k.hip: 0, uwvk_psp_k_r.hip: 1)
+template hipError_t launch_psp_predict_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&, double);
+template hipError_t launch_psp_update_sr<PSP_SIDE>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
+                                                   const MeasArgs&, int);
+template hipError_t launch_psp_epoch_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&,
+                                                  const EpochArgs&, int64_t, uint32_t);
+
+#if PSP_SIDE == 0
+// the handle's side picks the instantiation set (a template parameter of every
+// PSP kernel, not a run-time branch in the epoch loop)
+hipError_t launch_psp_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt) {
+  return sh.so3_right ? launch_psp_predict_sr<1>(dof, st, b, sh, dt) : launch_psp_predict_sr<0>(dof, st, b, sh, dt);
+}
+
+hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                             const MeasArgs& ma, int m) {
+  return sh.so3_right ? launch_psp_update_sr<1>(dof, kind, st, b, sh, ma, m)
+                      : launch_psp_update_sr<0>(dof, kind, st, b, sh, ma, m);
 }
 
 hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
                             int64_t grid, uint32_t ev_any) {
-  const dim3 g((unsigned)(grid > 0 ? grid : b.batch));
-  if (dof == 53)
-    launch_epoch_dof<53>(st, b, sh, ea, g, ev_any);
-  else
-    launch_epoch_dof<26>(st, b, sh, ea, g, ev_any);
-  return hipGetLastError();
+  return sh.so3_right ? launch_psp_epoch_sr<1>(dof, st, b, sh, ea, grid, ev_any)
+                      : launch_psp_epoch_sr<0>(dof, st, b, sh, ea, grid, ev_any);
 }
 
 // XCC placement probe: block b writes the XCC it runs on (hardware XCC_ID).
@@ -722,14 +764,17 @@ __global__ __launch_bounds__(64) void k_xcc_probe(uint32_t* out) {
 // XCCs (block b on the XCC of block b % 8: the placement of a single-partition MI355X, which the tail
 // plan and xcd_instance assume), else 0.  Measured once per device.
 int xcd_round_robin(int device) {
-  static int cache[64];
-  static bool init = false;
-  if (!init) {
-    for (int& c : cache) c = -1;
-    init = true;
-  }
+  // per-device result, -1 until measured; atomic so that host threads driving
+  // handles on several GPUs may probe concurrently (two first callers of one
+  // device both probe and store the same answer)
+  static std::atomic<int> cache[64] = {};
+  static std::once_flag init;
+  std::call_once(init, [] {
+    for (auto& c : cache) c.store(-1, std::memory_order_relaxed);
+  });
   if (device < 0 || device >= 64) return 0;
-  if (cache[device] >= 0) return cache[device];
+  const int known = cache[device].load(std::memory_order_acquire);
+  if (known >= 0) return known;
   DeviceGuard g(device);
   constexpr int kBlocks = 8 * 1024;
   uint32_t* d = nullptr;
@@ -751,7 +796,7 @@ int xcd_round_robin(int device) {
     }
     (void)hipFree(d);
   }
-  cache[device] = ok;
+  cache[device].store(ok, std::memory_order_release);
   return ok;
 }
 
@@ -760,8 +805,10 @@ int64_t psp_epoch_slots_per_xcd(int dof, int device) { return psp_epoch_slots(do
 int64_t psp_epoch_slots(int dof, int device, bool persist) {
   int per_cu = 0, cus = 0;
   // (the other instantiations have the same LDS and no more registers)
-  const void* k = persist ? (dof == 53 ? (const void*)psp::k_psp_epoch_p<53, 1, 0> : (const void*)psp::k_psp_epoch_p<26, 1, 0>)
-                          : (dof == 53 ? (const void*)psp::k_psp_epoch<53, 1, 0> : (const void*)psp::k_psp_epoch<26, 1, 0>);
+  // (every instantiation, both SO3 sides, is held to the same budget by
+  // tests/test_kernel_resources.py: <= 168 registers, no scratch, 3 waves/SIMD)
+  const void* k = persist ? (dof == 53 ? (const void*)psp::k_psp_epoch_p<53, 1, 0, 0> : (const void*)psp::k_psp_epoch_p<26, 1, 0, 0>)
+                          : (dof == 53 ? (const void*)psp::k_psp_epoch<53, 1, 0, 0> : (const void*)psp::k_psp_epoch<26, 1, 0, 0>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return 0;
@@ -802,16 +849,19 @@ int plan_tail(int64_t n, int64_t s, int64_t count) {
   return chunks;
 }
 
+#endif  // PSP_SIDE == 0
+
 }  // namespace uwvk
 
-#ifdef UWVK_TIMELINE
+#if defined(UWVK_TIMELINE) && PSP_SIDE == 0
 extern "C" int uwvk_debug_read_timeline(unsigned long long* out, long long n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(uwvk::psp::uwvk_timeline), (size_t)n * 8) != hipSuccess;
 }
 #endif
 
-#ifdef UWVK_STAMPS
-// diagnostic build only: per-phase cycle sums of the PSP epoch kernel
+#if defined(UWVK_STAMPS) && PSP_SIDE == 0
+// diagnostic build only: per-phase cycle sums of the PSP epoch kernel (the
+// left-side kernels; the right side's translation unit keeps its own sums)
 extern "C" int uwvk_debug_read_stamps_psp(unsigned long long* sum, unsigned long long* cnt, int reset) {
   if (hipMemcpyFromSymbol(sum, HIP_SYMBOL(uwvk::uwvk_stamp_sum), 64 * 8) != hipSuccess) return 1;
   if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(uwvk::uwvk_stamp_cnt), 64 * 8) != hipSuccess) return 1;

@@ -172,7 +172,7 @@ class PoseUKFBatch:
         _chk(self.L.uwvk_pose_set_option(self.h, 3, int(slots)), "set_option")
 
     def set_so3_right(self, on=True):
-        """UWVK_OPT_SO3_RIGHT: body-frame SO3 boxplus (literal kernels), like the oracle's or_set_so3_right."""
+        """UWVK_OPT_SO3_RIGHT: body-frame SO3 boxplus q exp(d) on every path (PSP, dense, literal), like the oracle's or_set_so3_right."""
         _chk(self.L.uwvk_pose_set_option(self.h, 5, int(bool(on))), "set_option")
 
     def set_tail_chunks(self, chunks):

@@ -16,10 +16,15 @@ def shard_range(rank, world, global_batch):
     return lo, hi
 
 
-def _qlog_delta(q, t):
-    """log(q * conj(t)) for arrays of unit quaternions (w, x, y, z)."""
+def _qlog_delta(q, t, right=False):
+    """log(q * conj(t)) (nav frame, the left SO3 side) or, right=True,
+    log(conj(t) * q) (body frame, UWVK_OPT_SO3_RIGHT) for arrays of unit
+    quaternions (w, x, y, z): the orientation error in the frame the filter's
+    covariance is expressed in.  The two products differ only in the sign of
+    the cross term."""
     w = q[..., 0] * t[0] + np.sum(q[..., 1:] * t[1:], -1)
-    v = t[0] * q[..., 1:] - q[..., :1] * t[1:] - np.cross(q[..., 1:], t[1:])
+    cr = np.cross(q[..., 1:], t[1:])
+    v = t[0] * q[..., 1:] - q[..., :1] * t[1:] + (cr if right else -cr)
     sgn = np.where(w < 0, -1.0, 1.0)
     w, v = w * sgn, v * sgn[..., None]
     nv = np.linalg.norm(v, axis=-1)
@@ -27,15 +32,16 @@ def _qlog_delta(q, t):
     return k[..., None] * v
 
 
-def ensemble_stats_host(x, P, truth):
-    """Host reference of uwvk_pose_ensemble_stats (same layout of `out`)."""
+def ensemble_stats_host(x, P, truth, right=False):
+    """Host reference of uwvk_pose_ensemble_stats (same layout of `out`);
+    right: the handle's SO3 side (the orientation error log(t^-1 q))."""
     store = x.shape[1]
     out = np.zeros(3 * store + 2)
     out[:store] = x.sum(0)
     out[store:2 * store] = (x * x).sum(0)
     e = x - truth
     e[:, 3:7] = 0.0
-    r = _qlog_delta(x[:, 3:7], truth[3:7])
+    r = _qlog_delta(x[:, 3:7], truth[3:7], right)
     sq = (e * e).sum(0)
     sq[3:6] += (r * r).sum(0)
     out[2 * store:3 * store] = sq

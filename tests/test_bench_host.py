@@ -170,3 +170,47 @@ def test_make_rccl_agrees_on_a_fallback(tmp_path, fail):
         "dist.barrier()\n"
         "sys.exit(0 if ok else 5)\n" % (ROOT, fail))
     assert bench.spawn_ranks([], 2, timeout=120, script=str(script)) == 0
+
+
+@pytest.mark.parametrize("fail", ["none", "rank5"])
+def test_eight_rank_spawn_and_collective_text(tmp_path, fail):
+    """C5's launch shape on CPU: bench.spawn_ranks starts 8 stand-in ranks,
+    they form the gloo control plane, make_rccl agrees on the engine's
+    communicator (stand-in) or, when rank 5 cannot make it, on the gloo
+    fallback on every rank; each rank reports config.collective as bench.py
+    would and the job's exit code is 0 either way.  (RCCL with N > 1 itself
+    runs only in the driver's 8-GPU bench: DESIGN.md section 8.)"""
+    script = tmp_path / "rank.py"
+    out = tmp_path / "out"
+    out.mkdir()
+    script.write_text(
+        "import os, sys\n"
+        "sys.path.insert(0, %r)\n"
+        "import bench\n"
+        "FAIL = %r\n"
+        "class Comm:\n"
+        "    def __init__(self, world, uid, rank, local):\n"
+        "        if FAIL == 'rank5' and rank == 5:\n"
+        "            raise RuntimeError('ncclCommInitRank failed')\n"
+        "    def close(self):\n"
+        "        pass\n"
+        "    @staticmethod\n"
+        "    def unique_id():\n"
+        "        return b'uid'\n"
+        "class Eng:\n"
+        "    RcclComm = Comm\n"
+        "world = int(os.environ['WORLD_SIZE'])\n"
+        "dist = bench.init_dist(world)\n"
+        "rank = dist.get_rank()\n"
+        "comm, err = bench.make_rccl(dist, Eng, world, rank, rank)\n"
+        "open(os.path.join(sys.argv[1], str(rank)), 'w').write(bench.collective_desc(dist, world, comm, err, False))\n"
+        "dist.barrier()\n"
+        "dist.destroy_process_group()\n" % (ROOT, fail))
+    assert bench.spawn_ranks([str(out)], 8, timeout=240, script=str(script)) == 0
+    texts = [(out / str(r)).read_text() for r in range(8)]
+    # every rank agrees on the collective (the reason names the failing rank or "another rank")
+    assert len(set(t.split(" failed (")[0] for t in texts)) == 1
+    if fail == "none":
+        assert all(t.startswith("RCCL all_reduce") for t in texts)
+    else:
+        assert all(t.startswith("gloo all_reduce") and "RCCL communicator failed" in t for t in texts)

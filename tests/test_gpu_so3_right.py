@@ -1,10 +1,12 @@
 """GPU parity with the body-frame (right) SO3 boxplus, the largest unpinned
-semantic (PoseUKF.cpp:31-32, :451): the engine's literal
-kernels under UWVK_OPT_SO3_RIGHT against the oracle under or_set_so3_right(1),
-for the predict, every update kind (both apply_delta forms) and multi-epoch
-logs.  Whichever side the real MTK uses, a GPU path reproduces it.  The PSP
-kernels are left-only; the option selects the literal
-kernels.  Tolerances as in test_gpu_parity.py."""
+semantic (PoseUKF.cpp:31-32, :451): the engine under
+UWVK_OPT_SO3_RIGHT against the oracle under or_set_so3_right(1), for the
+predict, every update kind and multi-epoch logs, on all three engine paths:
+psp (the default: the SR = 1 instantiations of the PSP kernels, with
+apply_delta's T = R(exp d)^T), dense (the literal kernels)
+and literal (the literal kernels with ukfom's literal apply_delta re-spread).
+Whichever side the real MTK uses, the fast path reproduces it.  Tolerances as
+in test_gpu_parity.py."""
 import numpy as np
 import pytest
 
@@ -41,12 +43,17 @@ class RightOracle:
         return call
 
 
-def _pair(eng, batch, dof, mode="C3", epochs=10, literal=False):
+PATHS = ["psp", "dense", "literal"]
+
+
+def _pair(eng, batch, dof, mode="C3", epochs=10, path="psp"):
     cfg, uwv, log = pose_setup(batch, dof, mode, epochs)
     o = RightOracle(batch, dof)
     g = eng.PoseUKFBatch(batch, dof)
     g.set_so3_right(True)
-    if literal:
+    if path == "dense":
+        g.set_dense_sigma(True)
+    elif path == "literal":
         g.set_literal_apply_delta(True)
     for f in (o, g):
         f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
@@ -61,9 +68,10 @@ def _check(o, g, dof, tol):
     assert se < tol and ce < tol, (se, ce)
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("dof", [53, 26])
-def test_predict_right(eng, dof):
-    cfg, uwv, log, o, g = _pair(eng, 6, dof)
+def test_predict_right(eng, dof, path):
+    cfg, uwv, log, o, g = _pair(eng, 6, dof, path=path)
     for k in range(3):
         for f in (o, g):
             f.set_rotation_rate(log["gyro"][k])
@@ -71,12 +79,12 @@ def test_predict_right(eng, dof):
     _check(o, g, dof, TOL_STEP)
 
 
-@pytest.mark.parametrize("literal", [False, True])
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("kind", ["acceleration", "velocity", "pressure", "water_velocity", "xy", "z", "efforts",
                                   "efforts_vel", "geographic", "delayed_xy"])
-def test_single_update_right(eng, kind, literal):
+def test_single_update_right(eng, kind, path):
     dof, B = 53, 5
-    cfg, uwv, log, o, g = _pair(eng, B, dof, literal=literal)
+    cfg, uwv, log, o, g = _pair(eng, B, dof, path=path)
     for f in (o, g):
         f.set_rotation_rate(log["gyro"][0])
         f.predict(1e-3)
@@ -114,10 +122,12 @@ def test_single_update_right(eng, kind, literal):
     _check(o, g, dof, TOL_STEP)
 
 
-@pytest.mark.parametrize("dof,mode,epochs,literal", [(53, "C3", 400, False), (26, "C3", 400, False),
-                                                     (53, "C4", 1000, False), (53, "C3", 400, True)])
-def test_run_log_right(eng, dof, mode, epochs, literal):
-    cfg, uwv, log, o, g = _pair(eng, 4, dof, mode, epochs, literal=literal)
+@pytest.mark.parametrize("dof,mode,epochs,path", [(53, "C3", 400, "psp"), (26, "C3", 400, "psp"),
+                                                  (53, "C4", 1000, "psp"), (26, "C4", 1000, "psp"),
+                                                  (53, "C3", 400, "dense"), (26, "C3", 400, "dense"),
+                                                  (53, "C4", 1000, "dense"), (53, "C3", 400, "literal")])
+def test_run_log_right(eng, dof, mode, epochs, path):
+    cfg, uwv, log, o, g = _pair(eng, 4, dof, mode, epochs, path=path)
     counts_o = o.run_log(log)
     acc = eng.DeviceBuffer(np.zeros((4, 4), np.uint32))
     g.run_log(g.upload_log(log), accept_counts=acc)
@@ -126,17 +136,56 @@ def test_run_log_right(eng, dof, mode, epochs, literal):
     _check(o, g, dof, TOL_LOG)
 
 
-def test_right_differs_from_left(eng):
+@pytest.mark.parametrize("dense", [False, True])
+def test_right_differs_from_left(eng, dense):
     """The switch reaches the kernels: the same 400-epoch C3 log on the left
     and right engine paths differs by far more than the parity tolerance."""
     cfg, uwv, log = pose_setup(2, 53, "C3", 400)
     xs = []
     for right in (False, True):
         g = eng.PoseUKFBatch(2, 53)
-        g.set_dense_sigma(True)
+        g.set_dense_sigma(dense)
         g.set_so3_right(right)
         g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
         g.set_process_noise_from_config(cfg, 1e-3)
         g.run_log(g.upload_log(log))
         xs.append(g.get_state())
     assert state_err(xs[1][0], xs[0][0], xs[0][1], 53).max() > 0.1
+
+
+@pytest.mark.parametrize("dof", [53, 26])
+def test_visual_landmark_right(eng, dof):
+    """The marker-augmented visual update (PoseUKF.cpp:613-654) with both SO3
+    segments (filter and marker orientation) on the right side, against the
+    oracle's right side (aug SEG_SO3R / sm SEG_SO3R)."""
+    from test_small_filters import pose_scene, visual_common
+    B = 5
+    cfg, uwv, log, o, g = _pair(eng, B, dof, "C3", 60)
+    o.run_log(log)
+    g.run_log(g.upload_log(log))
+    x0 = o.get_state()[0]
+    true_t, true_q, marker, px = pose_scene(x0)
+    fcov, fpos, cm, cam, cib = visual_common(B)
+    for f in (g, o):
+        f.update_visual(px, fcov, fpos, marker, cm, cam, cib)
+    _check(o, g, dof, TOL_STEP * 10)
+    assert not g.get_status().any()
+
+
+def test_ensemble_stats_right(eng):
+    """uwvk_pose_ensemble_stats on a right-side handle measures the orientation
+    error in the body frame, log(t^-1 q), like the host reference."""
+    from uwvk import ensemble
+    B = 130  # two partial rows of 64 plus a remainder
+    cfg, uwv, log, o, g = _pair(eng, B, 53, "C3", 50)
+    g.run_log(g.upload_log(log))
+    x, P = g.get_state()
+    truth = np.array(log["truth"].state(50, 53), dtype=np.float64)
+    # a truth orientation far from the identity, where the nav- and body-frame
+    # errors differ (the synthetic heading is ~0): 1.2 rad about (0.6, -0.3, 0.74)
+    ax = np.array([0.6, -0.3, 0.74]) / np.linalg.norm([0.6, -0.3, 0.74])
+    truth[3:7] = np.r_[np.cos(0.6), np.sin(0.6) * ax]
+    got = g.ensemble_stats(truth)
+    np.testing.assert_allclose(got, ensemble.ensemble_stats_host(x, P, truth, right=True), rtol=1e-9, atol=1e-12)
+    left = ensemble.ensemble_stats_host(x, P, truth, right=False)
+    assert not np.allclose(got[2 * 54 + 3:2 * 54 + 6], left[2 * 54 + 3:2 * 54 + 6], rtol=1e-3)

@@ -194,8 +194,12 @@ def pose_scene(x, seed=21):
     return true_t, true_q, marker, px + V.pixel_noise(B, seed + 1, 0.3)
 
 
+@pytest.mark.parametrize("right", [False, True])
 @pytest.mark.parametrize("dof", [53, 26])
-def test_pose_visual_update_reduces_error(dof):
+def test_pose_visual_update_reduces_error(dof, right):
+    """right: both SO3 segments of PoseStateWithMarker on the body-frame side
+    (or_set_so3_right, sm SEG_SO3R)"""
+    import contextlib
     B = 3
     cfg, uwv, log = pose_setup(B, dof=dof, epochs=5)
     o = O.OraclePoseBatch(B, dof)
@@ -204,8 +208,15 @@ def test_pose_visual_update_reduces_error(dof):
     x0, P0 = o.get_state()
     true_t, true_q, marker, px = pose_scene(x0)
     fcov, fpos, cm, cam, cib = visual_common(B)
-    o.update_visual(px, fcov, fpos, marker, cm, cam, cib)
+    with (O.so3_right() if right else contextlib.nullcontext()):
+        o.update_visual(px, fcov, fpos, marker, cm, cam, cib)
     x1, P1 = o.get_state()
+    if right:  # the side reaches the augmented update: it differs from the left one
+        o2 = O.OraclePoseBatch(B, dof)
+        o2.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+        o2.set_process_noise_from_config(cfg, log["dt"])
+        o2.update_visual(px, fcov, fpos, marker, cm, cam, cib)
+        assert np.abs(o2.get_state()[1] - P1).max() > 1e-9
     e0 = np.linalg.norm(x0[:, :3] - true_t, axis=1)
     e1 = np.linalg.norm(x1[:, :3] - true_t, axis=1)
     assert (e1 < e0).all(), (e0, e1)

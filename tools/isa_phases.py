@@ -20,7 +20,7 @@ subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-
                 "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", "-DUWVK_STAMPS", "-DPSP_HOT_ONLY", "-DPSP_DIAG_HOT=1", *extra, "-S", "-o", out,
                 os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
 s = open(out).read().split("\n")
-name = "_ZN4uwvk3psp11k_psp_epochILi%sELi1ELi1EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % dof
+name = "_ZN4uwvk3psp11k_psp_epochILi%sELi1ELi1ELi0EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % dof
 st = [i for i, l in enumerate(s) if l.startswith(name + ":")][0]
 en = [i for i, l in enumerate(s) if i > st and l.startswith(".Lfunc_end")][0]
 INT = re.compile(r"v_(add|sub|subrev|mul_lo|mul_hi|mad|lshl|lshr|ashr|and|or|xor|bfe|bfi|max|min|cvt|mul_u32|"
