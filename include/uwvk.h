@@ -59,7 +59,14 @@ typedef enum uwvk_status {
 #define UWVK_ST_NOTPD 0x1u    /* Cholesky of Sigma failed (non-positive pivot) */
 #define UWVK_ST_NAN 0x2u      /* non-finite measurement skipped for this instance */
 #define UWVK_ST_NONFINITE 0x4u/* non-finite state after a step */
-#define UWVK_ST_SCHEDULE 0x8u /* engine fault: a tail-chunk hand-off timed out (see UWVK_OPT_TAIL_SLOTS) */
+/* UWVK_ST_SCHEDULE: engine fault, a tail-chunk hand-off timed out (see
+ * UWVK_OPT_TAIL_SLOTS; never observed outside forced tests).  The instance's
+ * state is then INVALID, not merely late: the chunks after the lost hand-off
+ * did not run, and the late predecessor may have left Sigma in the kernel's
+ * time-scaled (unfolded) form.  Re-initialise a flagged instance
+ * (uwvk_pose_init_from_state with a state of the caller's choosing) before
+ * using it again. */
+#define UWVK_ST_SCHEDULE 0x8u
 
 /* ---- PoseState layout (src/PoseState.hpp:29-45) ------------------------ */
 /* Full layout: 53 DOF, 54 stored scalars (SO3 as a quaternion).           */
@@ -417,8 +424,10 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   (PoseUKF.cpp:31-32, :451).  1: body frame (right, classic MTK
  *   SO3::boxplus), q [+] d = q exp(d), in every orientation [+] / [-]: sigma
  *   points, processModel's orientation step (PoseUKF.cpp:32), manifold mean,
- *   apply_delta.  1 selects the literal kernels (the PSP kernels are
- *   left-only).  The oracle's or_set_so3_right is the same switch. */
+ *   apply_delta, the visual update's filter and marker orientations and the
+ *   ensemble statistics' orientation error (log(t^-1 q)).  Every engine path
+ *   runs either side (the PSP kernels are instantiated per side, SR); the
+ *   oracle's or_set_so3_right is the same switch. */
 #define UWVK_OPT_SO3_RIGHT 5
 /* UWVK_OPT_PERSIST: scheduling of the PSP run_log launch.  0 (default): one
  *   workgroup per instance (plus UWVK_OPT_TAIL_SLOTS spreading, which needs the

@@ -659,8 +659,9 @@ static hipError_t prepare_persist(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
   ea.ticket = h->d_ticket;
   ea.ticket_base = h->ticket_next;
   // the first grid units are the blocks' own; the counter then numbers units
-  // grid .. units - 1 and one failing ticket per block: units - grid + grid
-  h->ticket_next += (uint32_t)units;
+  // grid .. units - 1 and one failing ticket per block: units - grid + grid.
+  // ticket_next advances only once the launch is queued (commit_persist): a
+  // launch that fails leaves the device counter where it was
   return hipSuccess;
 }
 
@@ -754,7 +755,16 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     uint32_t ev_any = 0;  // the event kinds of this launch's epochs (kernel choice)
     for (int64_t k = e; k < last; k++) ev_any |= hf[k - first];
     HIPCHK(prepare_tail(h, ea, grid));
-    HIPCHK(launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid, ev_any));
+    if (launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid, ev_any) != hipSuccess) {
+      // a persistent launch that did not run took no tickets: restart the
+      // counter from zero (stream-ordered, before any later launch)
+      if (ea.ticket) {
+        h->ticket_next = 0;
+        (void)hipMemsetAsync(h->d_ticket, 0, 4, h->stream);
+      }
+      return UWVK_EDEVICE;
+    }
+    if (ea.ticket) h->ticket_next += ea.units;  // the tickets the launch takes
     if (r < first + count) {
       ea.first = r;
       ea.count = 1;
