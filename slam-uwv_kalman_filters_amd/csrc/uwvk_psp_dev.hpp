@@ -60,7 +60,9 @@
 #endif
 // ablation knobs for timing analysis only (results are invalid when set):
 // PSP_ABL = bitmask: 1 mean 1 iteration, 2 no rank-m pass, 4 no L Delta / X,
-// 8 no predict Cholesky, 16 no predict points, 32 no update Cholesky, 64 no HG/C/S
+// 8 no predict Cholesky, 16 no predict points, 32 no update Cholesky, (r04)
+// 64 no A-coupled rows (pos / vel rows and columns), 128 no flat pass (the Q
+// band), 256 no apply_delta (tools/abl_pmc.sh: per-phase counter budgets)
 #ifndef PSP_ABL
 #define PSP_ABL 0
 #endif
@@ -327,6 +329,16 @@ UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 #ifndef PSP_STAGE_LATE  // r03: the L_a rows staged after the last column step (pchol)
 #define PSP_STAGE_LATE 1
 #endif
+// r04: broadcast reads from the staging area 16-byte aligned, so that pairs of
+// doubles are one ds_read_b128 (4 LDS-array cycles, one address) instead of a
+// ds_read2_b64 (8 cycles) with a per-pair address.  sm.stg starts 8 bytes past a
+// 16-byte boundary (PspSmem: 11,448 + 432 B), so an odd stg index is aligned.
+// The Cholesky column of step J is shifted by one slot when J + 1 is even; the
+// predict's Delta_j and the update's P / Dz rows are padded to 4 per j.
+// (LDS-array cycles per instance-epoch: 1,987 measured before, r04b lds pass.)
+#ifndef PSP_LDS_ALIGN
+#define PSP_LDS_ALIGN 1
+#endif
 #ifndef PSP_PIV_EARLY
 #define PSP_PIV_EARLY 0  // r03: fewer VALU (-56 per epoch) but 176 VGPRs (2 waves per SIMD), not kept
 #endif
@@ -375,19 +387,22 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
       // col aliases the LAST staged row's not-yet-written slots J+1 .. K-1:
       // only L[c][J] for c > J is read, and that row's own L[.][c] lands in
       // slot c at step c, after this step's reads (one wave: LDS in order)
+      // (PSP_LDS_ALIGN with PSP_STAGE_LATE: slot c + 1 when J + 1 is even, so
+      // that the reads start on a 16-byte boundary; col is odd-aligned)
+      double* const cj = col + ((PSP_LDS_ALIGN && PSP_STAGE_LATE && ((J + 1) & 1) == 0) ? 1 : 0);
 #if PSP_STAGE_LATE && PSP_COL_SEL
       // lanes outside (J, K) store to their own throw-away slot past the column
       // (the rows area is written only after the last step): no exec-masked branch
-      static_assert(K + 64 <= 115, "throw-away slots (PG::STG)");
-      col[(r > J && r < K) ? r : K + (r & 63)] = a[J];
+      static_assert(K + 65 <= 115, "throw-away slots (PG::STG)");
+      cj[(r > J && r < K) ? r : K + (r & 63)] = a[J];
 #else
-      if (r > J && r < K) col[r] = a[J];
+      if (r > J && r < K) cj[r] = a[J];
 #endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-      for (int c = J + 1; c < K; c++) a[c] -= a[J] * col[c];
+      for (int c = J + 1; c < K; c++) a[c] -= a[J] * cj[c];
 #pragma unroll
       for (int c = J + 1; c < K; c++) asm volatile("" : "+v"(a[c]));
     }
@@ -790,20 +805,24 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     // back by every lane as a broadcast, one j at a time (a compiler memory
     // barrier per j keeps at most two j's loads in flight: hoisted all at once
     // they took 90 VGPRs); 45 LDS reads instead of 90 v_readlane
+    // (PSP_LDS_ALIGN: 4 slots per j from slot 1, so each j's first pair is one
+    // aligned ds_read_b128)
+    constexpr int DS = PSP_LDS_ALIGN ? 4 : 3, D0 = PSP_LDS_ALIGN ? 1 : 0;
+    static_assert(D0 + DS * K <= PG<DOF>::STG, "Delta (PG::STG)");
     if ((l & 1) == 0 && l < 2 * K) {
 #pragma unroll
-      for (int i = 0; i < 3; i++) sm.stg[(l >> 1) * 3 + i] = dd[i];
+      for (int i = 0; i < 3; i++) sm.stg[D0 + (l >> 1) * DS + i] = dd[i];
     }
     wsync();
     double dn[3];
 #pragma unroll
-    for (int i = 0; i < 3; i++) dn[i] = sm.stg[i];
+    for (int i = 0; i < 3; i++) dn[i] = sm.stg[D0 + i];
 #pragma unroll
     for (int j = 0; j < ((PSP_ABL & 4) ? 0 : K); j++) {
       double dj[3] = {dn[0], dn[1], dn[2]};
       if (j + 1 < K) {
 #pragma unroll
-        for (int i = 0; i < 3; i++) dn[i] = sm.stg[3 * (j + 1) + i];
+        for (int i = 0; i < 3; i++) dn[i] = sm.stg[D0 + DS * (j + 1) + i];
       }
 #pragma unroll
       for (int i = 0; i < 3; i++) Y[i] += a[j] * dj[i];
@@ -857,6 +876,10 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #pragma unroll
   for (int q = 0; q < 6; q++) {
     const int r = pv[q], rc = proc_couple(r);
+    if (PSP_ABL & 64) {
+      nv[q] = 0.0;
+      continue;
+    }
     const double t0 = aj * (ds * sm.S[pidx_sel(r, jl, Tl)]) + (jc >= 0 ? dt * sm.S[pidx_sel(r, jcc, Tc)] : 0.0);
     const double t1 = aj * (ds * sm.S[pidx_sel(rc, jl, Tl)]) + (jc >= 0 ? dt * sm.S[pidx_sel(rc, jcc, Tc)] : 0.0);
     nv[q] = t0 + dt * t1;  // A_rr = 1 for pos/vel rows
@@ -918,7 +941,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       const bool jpv = jc >= 0;
       const double2* f2 = reinterpret_cast<const double2*>(fq);
 #pragma unroll
-      for (int q = 0; q < 6; q++)
+      for (int q = 0; q < ((PSP_ABL & 64) ? 0 : 6); q++)
         if (!jpv || l <= pv[q]) {
           const int e = PSP_PIDX_SEL ? pidx_sel(pv[q], l, Tl) : pidx(pv[q], l);  // l < DOF: jl == l
           double qq;
@@ -999,7 +1022,9 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
         }
       }
     };
-    if (qs || PSP_DIAG_HOT)
+    if (PSP_ABL & 128)
+      ;
+    else if (qs || PSP_DIAG_HOT)
       band(std::true_type{});
     else
       band(std::false_type{});
@@ -1688,11 +1713,14 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     // P (lane i K + j) and Dz_j (lane 2 j) staged in stg (free after the sums)
     // and read back as broadcasts one j at a time, as the predict's Delta
     // (PSP_DELTA_LDS): LDS reads instead of 4 M K v_readlane
-    static_assert(2 * M * K <= PG<DOF>::STG, "P and Dz (PG::STG)");
-    if (l < M * K) sm.stg[(l % K) * M + l / K] = Pl;  // j-major: P[i][j] at j M + i
+    // (PSP_LDS_ALIGN: M = 3 rows padded to 4 from slot 1, so each j's first
+    // pair is one aligned ds_read_b128)
+    constexpr int PS = (PSP_LDS_ALIGN && M == 3) ? 4 : M, P0 = (PSP_LDS_ALIGN && M >= 2) ? 1 : 0;
+    static_assert(P0 + 2 * PS * K <= PG<DOF>::STG, "P and Dz (PG::STG)");
+    if (l < M * K) sm.stg[P0 + (l % K) * PS + l / K] = Pl;  // j-major: P[i][j] at j PS + i
     if ((l & 1) == 0 && l < 2 * K) {
 #pragma unroll
-      for (int i = 0; i < M; i++) sm.stg[M * K + (l >> 1) * M + i] = zd[i];
+      for (int i = 0; i < M; i++) sm.stg[P0 + PS * K + (l >> 1) * PS + i] = zd[i];
     }
     wsync();
     double g[M], c[M];
@@ -1706,8 +1734,8 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       double pj[M], zj[M];
 #pragma unroll
       for (int i = 0; i < M; i++) {
-        pj[i] = sm.stg[j * M + i];
-        zj[i] = sm.stg[M * K + j * M + i];
+        pj[i] = sm.stg[P0 + j * PS + i];
+        zj[i] = sm.stg[P0 + PS * K + j * PS + i];
       }
 #pragma unroll
       for (int i = 0; i < M; i++) {
@@ -1870,6 +1898,10 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
 #endif
   psync();
   PSP_PHASE(34);
+  if (PSP_ABL & 256) {
+    asm volatile("" ::"v"(dl));
+    return true;
+  }
   // apply_delta, exact form: mu <- mu [+] delta, Sigma <- T Sigma T^T with T
   // the identity except on the orientation block.  ukfom re-spreads X_p =
   // mu [+] +-L_j, shifts every point by delta and takes the deviations from
