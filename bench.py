@@ -50,20 +50,45 @@ F_UPD3_EXEC = 155_237
 F_STEP_EXEC = F_PRED + F_UPD3_EXEC  # 855,614 (literal kernels, UWVK_OPT_DENSE_SIGMA)
 
 
+def _pchol_flops(n, k):
+    """k-column partial Cholesky of an n x n matrix: the column scales, the
+    trailing updates of the panel's columns (c > J, rows >= c) and one
+    reciprocal square root + product per pivot."""
+    return sum((n - j - 1) + sum(2 * (n - c) for c in range(j + 1, k)) for j in range(k)) + 2 * k
+
+
+def psp_flops_phases(n=53, k_pred=15, updates=((6, 3, 7),)):
+    """Useful flops of one PSP step by phase: the operation
+    count of the algorithm, whatever the lane mapping.  Per-point costs are
+    counted from the models' code (uwvk_psp_dev.hpp): a sigma point's
+    orientation through the process model 215 flop (generation 14, SO3 exp 38
+    and product 28 twice, latitude series 28, q-rotation 30, rest 13); a
+    manifold-mean term 64 (SO3 product 28, small-angle log 30, weighted sum 6);
+    an acceleration / DVL point 132 (generation 14, SO3 exp 38, product 28,
+    rotation matrix 30, R^T(a + g) 22).  updates: (k, m, ncols) per update."""
+    kp, N2 = k_pred, 2 * k_pred + 1
+    npk = n * (n + 1) // 2
+    ph = {}
+    ph["predict partial Cholesky + R Q_o R^T"] = _pchol_flops(n, kp) + 138
+    ph["predict points, mean, deviations, ori x ori, X"] = (N2 * 215 + (N2 * 64 + 70)   # points, 1 mean iteration
+                                                          + N2 * 58 + N2 * 12 + 12 + 3 * kp  # deviations, ori x ori, Delta
+                                                          + 2 * n * 3 * kp + 9 * n)          # X = 1/2 A L_a Delta
+    ph["predict covariance rows (A-coupled, Q' band, mean)"] = 6 * n * 7 + 9 * n + 9 * n + 2 * (n + 1)
+    for i, (k, m, nc) in enumerate(updates):
+        tag = "update %d (k %d, m %d)" % (i, k, m)
+        ph[tag + " partial Cholesky"] = _pchol_flops(n, k)
+        ph[tag + " points, zbar, S"] = (2 * k + 1) * (132 if m == 3 else 80) + (2 * k + 1) * (m + m * (m + 1))
+        ph[tag + " H, P, G, C, S, gain"] = (30 + 2 * m * k * nc + 2 * n * nc * m + n * m + 2 * 2 * n * k * m
+                                            + n * m + 2 * m * m * nc + 40 + 2 * n * m * m + 24 + 2 * n * m)
+        ph[tag + " Sigma -= C K^T"] = 2 * npk * m + 2 * n * m
+        ph[tag + " apply_delta"] = 38 + 30 + 15 * (n - 3) + 108 + 28 + (n + 1)
+    return ph
+
+
 def psp_flops(n=53, k_pred=15, updates=((6, 3, 7),)):
-    """Flops the PSP kernels execute per step: k-column
-    partial Cholesky, 2k+1 model evaluations, O(n^2) covariance algebra.
-    updates: (k, m, ncols) per update of the step."""
-    def pchol(k):
-        return 2 * sum((k - 1 - j) * (n - j) for j in range(k)) + 3 * k * (n - k // 2)
-    np_ = n * (n + 1) // 2
-    f = pchol(k_pred) + (2 * k_pred + 1) * (120 + 3 * 60)  # points + 3 mean iterations
-    f += 2 * n * k_pred * 3 + 6 * 2 * (2 * k_pred + 1)      # L Delta, ori x ori
-    f += 7 * 6 * n + 4 * np_                                # A-coupled rows, decays + Q'
-    for k, m, nc in updates:
-        f += pchol(k) + (2 * k + 1) * 50 + 2 * m * k * nc + 2 * n * nc * m
-        f += 2 * n * k * m + 2 * n * m * m + 2 * np_ * m + 2 * 9 * n
-    return f
+    """Flops the PSP kernels execute per step (DESIGN.md sections 4.3, 6.1): the
+    sum of psp_flops_phases."""
+    return sum(psp_flops_phases(n, k_pred, updates).values())
 
 
 F_STEP_PSP = psp_flops()

@@ -1913,12 +1913,11 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   // T L L^T T^T exactly.
   {
     const double dv[3] = {readlane_d(dl, 3), readlane_d(dl, 4), readlane_d(dl, 5)};
-    double R[9];
+    double R[9], eq[4];  // exp(delta_ori) once: T's rotation and the mean's [+]
+    so3_exp_psp(dv, eq);
     {
-      double eq[4];
-      so3_exp_psp(dv, eq);
-      if constexpr (SR) eq[1] = -eq[1], eq[2] = -eq[2], eq[3] = -eq[3];
-      qmatrix(eq, R);
+      const double tq[4] = {eq[0], SR ? -eq[1] : eq[1], SR ? -eq[2] : eq[2], SR ? -eq[3] : eq[3]};
+      qmatrix(tq, R);
     }
     // rows 3..5 of every column j outside the block
     if (l < DOF && !(l >= 3 && l < 6)) {
@@ -1952,11 +1951,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     double mnew = 0.0;
     if (l < L::store && !(l >= 3 && l < 7)) mnew = sm.mu[l] + 1.0 * (l < 3 ? dl : dsh);
     double qn[4];
-    {
-      double eq[4];
-      so3_exp_psp(dv, eq);
-      qplus_psp<SR>(eq, sm.mu + L::s_quat, qn);
-    }
+    qplus_psp<SR>(eq, sm.mu + L::s_quat, qn);
     psync();
     if (l < 9 && (l / 3) >= (l % 3)) sm.S[pidx(3 + l / 3, 3 + l % 3)] = nb;
     if (l < L::store && !(l >= 3 && l < 7)) sm.mu[l] = mnew;
