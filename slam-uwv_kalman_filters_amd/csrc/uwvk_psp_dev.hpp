@@ -323,8 +323,8 @@ UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 #ifndef PSP_ROWS_SEL  // r03 A/B: the predict's rows < 9 and Q-band stores branch-free (throw-away slots)
 #define PSP_ROWS_SEL 0
 #endif
-#ifndef PSP_COL_SEL  // r03: the Cholesky column broadcast stored branch-free (pchol_step_lds)
-#define PSP_COL_SEL 1
+#ifndef PSP_COL_SEL  // r03: the Cholesky column broadcast stored branch-free (pchol_step_lds); r04: 2 unconditional
+#define PSP_COL_SEL 2
 #endif
 #ifndef PSP_STAGE_LATE  // r03: the L_a rows staged after the last column step (pchol)
 #define PSP_STAGE_LATE 1
@@ -390,7 +390,16 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
       // (PSP_LDS_ALIGN with PSP_STAGE_LATE: slot c + 1 when J + 1 is even, so
       // that the reads start on a 16-byte boundary; col is odd-aligned)
       double* const cj = col + ((PSP_LDS_ALIGN && PSP_STAGE_LATE && ((J + 1) & 1) == 0) ? 1 : 0);
-#if PSP_STAGE_LATE && PSP_COL_SEL
+#if PSP_STAGE_LATE && PSP_COL_SEL == 2
+      // r04: every lane stores its a[J] to slot r: the slots read this step
+      // are (J, K), which only the lanes r in (J, K) write; the others land in
+      // slots that are not read now and that nothing else holds while the
+      // factor runs (the rows area is written only after the last step).  The
+      // address is one per-lane constant plus the step's immediate offset,
+      // instead of a select per step (4 VALU)
+      static_assert(64 + 1 <= 115, "column slots (PG::STG)");
+      cj[r & 63] = a[J];
+#elif PSP_STAGE_LATE && PSP_COL_SEL
       // lanes outside (J, K) store to their own throw-away slot past the column
       // (the rows area is written only after the last step): no exec-masked branch
       static_assert(K + 65 <= 115, "throw-away slots (PG::STG)");

@@ -25,6 +25,7 @@ struct VelShared {  // batch-shared model parameters (by value)
 
 struct VelBufs {
   int64_t batch;
+  const VelShared* shared;  // device copy of the handle's VelShared (k_vel_epoch_g stages it in LDS)
   double* mu;       // [batch][4]
   double* sigma;    // [batch][16]
   double* gyro;     // [batch][3]  stored GyroMeasurement
@@ -47,8 +48,23 @@ struct VelEpochArgs {
   int64_t first, count;
 };
 
+// The model parameters reach the RK4 code either by value (kernel argument:
+// SGPRs) or, in k_vel_epoch_g (VEL_LDS), from an LDS copy read through a
+// pointer laundered before every derivative, so that each derivative loads
+// the rows it uses next to their use instead of the whole set being hoisted
+// out of the epoch loop (the by-value matrices were 370 spilled SGPR slots
+// and ~1,250 v_readlane per epoch).
+using LVS = __attribute__((address_space(3))) const VelShared;
+UWVK_DEV const VelShared& vlaunder(const VelShared& p) { return p; }
+UWVK_DEV LVS& vlaunder(LVS& p) {
+  LVS* q = &p;
+  asm volatile("" : "+v"(q));
+  return *q;
+}
+
 // ---- [EXT] ModelSimulation: M nu_dot + C(nu) nu + D(nu) nu + g(q) = tau, RK4 --
-UWVK_DEV void v_coriolis(const VelShared& P, const double nu[6], double c[6]) {
+template <class PS>
+UWVK_DEV void v_coriolis(const PS& P, const double nu[6], double c[6]) {
   double a[3], b[3], t0[3], t1[3], t2[3];
 #pragma unroll
   for (int i = 0; i < 3; i++) {
@@ -67,7 +83,8 @@ UWVK_DEV void v_coriolis(const VelShared& P, const double nu[6], double c[6]) {
   for (int i = 0; i < 3; i++) { c[i] = t0[i]; c[3 + i] = t1[i] + t2[i]; }
 }
 
-UWVK_DEV void v_deriv(const VelShared& P, const double tau[6], const double s[13], double ds[13]) {
+template <class PS>
+UWVK_DEV void v_deriv(const PS& P, const double tau[6], const double s[13], double ds[13]) {
   const double q[4] = {s[3], s[4], s[5], s[6]};
   const double nu[6] = {s[7], s[8], s[9], s[10], s[11], s[12]};
   const double v[3] = {s[7], s[8], s[9]};
@@ -90,11 +107,12 @@ UWVK_DEV void v_deriv(const VelShared& P, const double tau[6], const double s[13
     d[i] = sl + sq;
   }
   const double fw[3] = {0, 0, -P.weight}, fb[3] = {0, 0, P.buoyancy};
+  const double cog[3] = {P.cog[0], P.cog[1], P.cog[2]}, cob[3] = {P.cob[0], P.cob[1], P.cob[2]};
   double fg[3], fbb[3], mg[3], mb[3];
   qrot_inv(q, fw, fg);
   qrot_inv(q, fb, fbb);
-  cross3(P.cog, fg, mg);
-  cross3(P.cob, fbb, mb);
+  cross3(cog, fg, mg);
+  cross3(cob, fbb, mb);
 #pragma unroll
   for (int i = 0; i < 3; i++) { g[i] = -(fg[i] + fbb[i]); g[3 + i] = -(mg[i] + mb[i]); }
 #pragma unroll
@@ -108,20 +126,32 @@ UWVK_DEV void v_deriv(const VelShared& P, const double tau[6], const double s[13
   }
 }
 
-UWVK_DEV void v_rk4(const VelShared& P, const double tau[6], double dt, const double s[13], double o[13]) {
-  double k1[13], k2[13], k3[13], k4[13], t[13];
-  v_deriv(P, tau, s, k1);
+// the stage sum k1 + 2 k2 + 2 k3 + k4 is accumulated as the stages finish, in
+// the same left-to-right order (one 13-vector live instead of four)
+template <class PS>
+UWVK_DEV void v_rk4(const PS& P, const double tau[6], double dt, const double s[13], double o[13]) {
+  double k[13], acc[13], t[13];
+  v_deriv(vlaunder(P), tau, s, k);
 #pragma unroll
-  for (int i = 0; i < 13; i++) t[i] = s[i] + 0.5 * dt * k1[i];
-  v_deriv(P, tau, t, k2);
+  for (int i = 0; i < 13; i++) {
+    acc[i] = k[i];
+    t[i] = s[i] + 0.5 * dt * k[i];
+  }
+  v_deriv(vlaunder(P), tau, t, k);
 #pragma unroll
-  for (int i = 0; i < 13; i++) t[i] = s[i] + 0.5 * dt * k2[i];
-  v_deriv(P, tau, t, k3);
+  for (int i = 0; i < 13; i++) {
+    acc[i] = acc[i] + 2.0 * k[i];
+    t[i] = s[i] + 0.5 * dt * k[i];
+  }
+  v_deriv(vlaunder(P), tau, t, k);
 #pragma unroll
-  for (int i = 0; i < 13; i++) t[i] = s[i] + dt * k3[i];
-  v_deriv(P, tau, t, k4);
+  for (int i = 0; i < 13; i++) {
+    acc[i] = acc[i] + 2.0 * k[i];
+    t[i] = s[i] + dt * k[i];
+  }
+  v_deriv(vlaunder(P), tau, t, k);
 #pragma unroll
-  for (int i = 0; i < 13; i++) o[i] = s[i] + (dt / 6.0) * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
+  for (int i = 0; i < 13; i++) o[i] = s[i] + (dt / 6.0) * (acc[i] + k[i]);
   const double n = sqrt(o[3] * o[3] + o[4] * o[4] + o[5] * o[5] + o[6] * o[6]);
 #pragma unroll
   for (int i = 3; i < 7; i++) o[i] /= n;
@@ -602,7 +632,24 @@ UWVK_DEV bool vg_update(double mu[4], double S[16], const double z[M], const dou
 
 constexpr int VG = 16;  // lanes per filter
 
-__global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P, VelEpochArgs ea) {
+#ifndef VEL_LDS
+#define VEL_LDS 1
+#endif
+__global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, VelEpochArgs ea) {
+#if VEL_LDS
+  // the model parameters in LDS (one copy per workgroup), read per derivative
+  __shared__ VelShared sp;
+  {
+    constexpr int NW = (int)(sizeof(VelShared) / 8);
+    const double* src = reinterpret_cast<const double*>(b.shared);
+    double* dst = reinterpret_cast<double*>(&sp);
+    for (int k = (int)threadIdx.x; k < NW; k += 64) dst[k] = src[k];
+    __syncthreads();
+  }
+  LVS& P = *(LVS*)&sp;
+#else
+  const VelShared& P = P0;
+#endif
   const int g = (int)threadIdx.x & (VG - 1);
   const int64_t B = b.batch, inst = (int64_t)blockIdx.x * (64 / VG) + (int)threadIdx.x / VG;
   const bool live = inst < B;
@@ -705,6 +752,7 @@ struct uwvk_vel {
          *d_meas = nullptr;
   uint8_t* d_mask = nullptr;
   uint32_t* d_status = nullptr;
+  VelShared* d_shared = nullptr;  // device copy of P (uploaded by every call that changes P)
   VelShared P{};
   bool has_state = false, has_model = false;
   int groups = -1;  // UWVK_VEL_OPT_LANE_GROUPS: -1 auto, 0 lane per filter, 1 16 lanes per filter
@@ -720,6 +768,7 @@ static VelBufs vbufs(const uwvk_vel* h) {
   VelBufs b;
   b.batch = h->batch; b.mu = h->d_mu; b.sigma = h->d_sigma; b.gyro = h->d_gyro; b.efforts = h->d_eff;
   b.model = h->d_model; b.status = h->d_status;
+  b.shared = h->d_shared;
   return b;
 }
 
@@ -754,7 +803,8 @@ uwvk_status uwvk_vel_create(int64_t batch, int device, uwvk_vel** out) {
   const bool ok = hipMalloc(&h->d_mu, B * 4 * 8) == hipSuccess && hipMalloc(&h->d_sigma, B * 16 * 8) == hipSuccess &&
                   hipMalloc(&h->d_gyro, B * 3 * 8) == hipSuccess && hipMalloc(&h->d_eff, B * 6 * 8) == hipSuccess &&
                   hipMalloc(&h->d_model, B * 13 * 8) == hipSuccess && hipMalloc(&h->d_meas, B * 12 * 8) == hipSuccess &&
-                  hipMalloc(&h->d_mask, B) == hipSuccess && hipMalloc(&h->d_status, B * 4) == hipSuccess;
+                  hipMalloc(&h->d_mask, B) == hipSuccess && hipMalloc(&h->d_status, B * 4) == hipSuccess &&
+                  hipMalloc(&h->d_shared, sizeof(VelShared)) == hipSuccess;
   if (!ok) {
     uwvk_vel_destroy(h);
     return UWVK_ENOMEM;
@@ -765,7 +815,8 @@ uwvk_status uwvk_vel_create(int64_t batch, int device, uwvk_vel** out) {
   (void)hipMemsetAsync(h->d_status, 0, B * 4, h->stream);
   // process_noise_cov = 0 except velocity diag 1e-4 (VelocityUKF.cpp:54-55)
   for (int k = 0; k < 3; k++) h->P.Q0[k * 4 + k] = 0.0001;
-  if (hipStreamSynchronize(h->stream) != hipSuccess) {
+  if (hipMemcpyAsync(h->d_shared, &h->P, sizeof(VelShared), hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+      hipStreamSynchronize(h->stream) != hipSuccess) {
     uwvk_vel_destroy(h);
     return UWVK_EDEVICE;
   }
@@ -778,7 +829,7 @@ void uwvk_vel_destroy(uwvk_vel* h) {
   if (!h) return;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_gyro, (void*)h->d_eff, (void*)h->d_model,
-                  (void*)h->d_meas, (void*)h->d_mask, (void*)h->d_status})
+                  (void*)h->d_meas, (void*)h->d_mask, (void*)h->d_status, (void*)h->d_shared})
     if (p) (void)hipFree(p);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -799,6 +850,10 @@ uwvk_status uwvk_vel_set_process_noise(uwvk_vel* h, const double Q[16]) {
   if (!h || !Q) return UWVK_EINVAL;
   if (!vfinite(Q, 16)) return UWVK_ENAN;
   std::memcpy(h->P.Q0, Q, sizeof(h->P.Q0));
+  // after all queued work (a running kernel may read the previous copy)
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpyAsync(h->d_shared, &h->P, sizeof(VelShared), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
   return UWVK_OK;
 }
 
@@ -852,6 +907,8 @@ uwvk_status uwvk_vel_setup_motion_model(uwvk_vel* h, const uwvk_uwv_params* u) {
     h->P.cog[k] = u->distance_body2centerofgravity[k];
     h->P.cob[k] = u->distance_body2centerofbuoyancy[k];
   }
+  HIPCHK(hipStreamSynchronize(h->stream));  // a running kernel may read the previous copy
+  HIPCHK(hipMemcpyAsync(h->d_shared, &h->P, sizeof(VelShared), hipMemcpyHostToDevice, h->stream));
   hipLaunchKernelGGL(k_vel_setup, dim3(vgrid(h->batch)), dim3(64), 0, h->stream, vbufs(h));
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(h->stream));

@@ -23,7 +23,7 @@ def mix(extra=(), dof=53):
                     os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
     s = open(out).read().split("\n")
     os.unlink(out)
-    name = "_ZN4uwvk3psp11k_psp_epochILi%dELi1ELi1EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % dof
+    name = "_ZN4uwvk3psp11k_psp_epochILi%dELi1ELi1ELi0EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % dof
     st = [i for i, l in enumerate(s) if l.startswith(name + ":")][0]
     en = [i for i, l in enumerate(s) if i > st and l.startswith(".Lfunc_end")][0]
     body = s[st:en + 1]

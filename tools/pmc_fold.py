@@ -45,7 +45,7 @@ waves = mix["SQ_WAVES"]
 instances = int(workload.rsplit("-b", 1)[1])
 we = instances * steps
 e = {
-    "kernel": "k_psp_epoch<53, 1, 1>", "epochs_per_launch": steps, "waves": waves, "instances": instances,
+    "kernel": "k_psp_epoch<53, 1, 1, 0>", "epochs_per_launch": steps, "waves": waves, "instances": instances,
     "fetch_size_kib_raw": fetch["FETCH_SIZE"], "write_size_kib_raw": write["WRITE_SIZE"],
     "fetch_bytes": fetch["FETCH_SIZE"] * 1024 * 2, "write_bytes": write["WRITE_SIZE"] * 1024,
 }

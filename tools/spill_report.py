@@ -21,7 +21,7 @@ subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-
                 os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
 s = open(out).read().split("\n")
 os.unlink(out)
-name = "_ZN4uwvk3psp11k_psp_epochILi53ELi1ELi1EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE"
+name = "_ZN4uwvk3psp11k_psp_epochILi53ELi1ELi1ELi0EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE"
 a = [i for i, l in enumerate(s) if l.startswith(name + ":")][0]
 b = [i for i, l in enumerate(s) if i > a and l.startswith(".Lfunc_end")][0]
 L = s[a:b + 1]
