@@ -633,7 +633,7 @@ UWVK_DEV bool vg_update(double mu[4], double S[16], const double z[M], const dou
 constexpr int VG = 16;  // lanes per filter
 
 #ifndef VEL_LDS
-#define VEL_LDS 1
+#define VEL_LDS 0  // r04 A/B: 474.5 against 546.8 M steps/s on C2 (profiles/r04/c2ab/), not kept
 #endif
 __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, VelEpochArgs ea) {
 #if VEL_LDS
