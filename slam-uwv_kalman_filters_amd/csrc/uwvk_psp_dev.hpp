@@ -320,6 +320,12 @@ UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 #ifndef PSP_PIDX_SEL  // r03: packed indices of the predict's rows < 12 by pidx_sel
 #define PSP_PIDX_SEL 1
 #endif
+#ifndef PSP_CPL_FMA  // r04: the predict's A-coupled rows read the coupled column unconditionally (FMA with 0 / dt)
+#define PSP_CPL_FMA 1
+#endif
+#ifndef PSP_QDIAG  // r04: the lane-resident Q's pos / vel diagonal added per lane (rows_lt9), not selected per row
+#define PSP_QDIAG 1
+#endif
 #ifndef PSP_ROWS_SEL  // r03 A/B: the predict's rows < 9 and Q-band stores branch-free (throw-away slots)
 #define PSP_ROWS_SEL 0
 #endif
@@ -882,6 +888,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   // loads need no exec branch (their products are selected away)
   const int jcc = jc >= 0 ? jc : jl;
   const int Tc = (jcc * (jcc + 1)) >> 1;
+  [[maybe_unused]] const double cf = jc >= 0 ? dt : 0.0;
 #pragma unroll
   for (int q = 0; q < 6; q++) {
     const int r = pv[q], rc = proc_couple(r);
@@ -889,8 +896,16 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       nv[q] = 0.0;
       continue;
     }
+#if PSP_CPL_FMA
+    // (r04) the coupled column's term as an FMA with cf = dt (coupled lanes) or
+    // 0: the conditional form was compiled to 12 exec-masked branches, each
+    // waiting for its own LDS load (lgkmcnt(0)); S~ is finite, so cf = 0 adds 0
+    const double t0 = fma(cf, sm.S[pidx_sel(r, jcc, Tc)], aj * (ds * sm.S[pidx_sel(r, jl, Tl)]));
+    const double t1 = fma(cf, sm.S[pidx_sel(rc, jcc, Tc)], aj * (ds * sm.S[pidx_sel(rc, jl, Tl)]));
+#else
     const double t0 = aj * (ds * sm.S[pidx_sel(r, jl, Tl)]) + (jc >= 0 ? dt * sm.S[pidx_sel(r, jcc, Tc)] : 0.0);
     const double t1 = aj * (ds * sm.S[pidx_sel(rc, jl, Tl)]) + (jc >= 0 ? dt * sm.S[pidx_sel(rc, jcc, Tc)] : 0.0);
+#endif
     nv[q] = t0 + dt * t1;  // A_rr = 1 for pos/vel rows
   }
 #else
@@ -954,10 +969,17 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
         if (!jpv || l <= pv[q]) {
           const int e = PSP_PIDX_SEL ? pidx_sel(pv[q], l, Tl) : pidx(pv[q], l);  // l < DOF: jl == l
           double qq;
-          if constexpr (kQS) qq = (l == pv[q]) ? lq.q0 : 0.0;
+          if constexpr (kQS) qq = (PSP_QDIAG || l != pv[q]) ? 0.0 : lq.q0;
           else qq = f2[e].y;
           sm.S[e] = (nv[q] + qq) * ids;
         }
+#if PSP_QDIAG
+      // (r04) the lane-resident Q's diagonal on the pos / vel rows added by
+      // their own lane afterwards, instead of a select per row: lane l in
+      // {0, 1, 2, 6, 7, 8} (jpv) stored (l, l) above; d_l = 1 there (ids == 1),
+      // so nv + q0 is bitwise the (nv + q0) * ids of the select form
+      if (kQS && jpv && !(PSP_ABL & 64)) sm.S[Tl + l] += lq.q0;
+#endif
 #pragma unroll
       for (int i = 0; i < 3; i++) {
         const int e = PSP_PIDX_SEL ? pidx_sel(3 + i, l, Tl) : pidx(3 + i, l);
@@ -1360,15 +1382,25 @@ UWVK_DEV void rankm_mfma(double* S, double* stg, const double (&Ct)[M], const do
 }
 
 // one row block I of rankm_mfma_o (tiles (I, J), J <= I), then block I + 1
+#ifndef PSP_TQ_BASE  // r04: tile row offsets as T(x + q) = T(x) + q x + T(q) (x compile-time): one multiply-add
+#define PSP_TQ_BASE 1
+#endif
 template <int DOF, int I, int NT>
-UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop)[NT], int q, int c) {
+UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop)[NT], int q, int c, int tq) {
   if constexpr (I < NT) {
     constexpr int O = DOF - 16 * NT;
     int base[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
+#if PSP_TQ_BASE
+      // row R = x + q, x = O + 16 I + 4 i: packed offset T(x) + q x + T(q) + O + c
+      // (tq = T(q) + O + c, once per phase) instead of R (R + 1) / 2 per row
+      const int x = O + 16 * I + 4 * i;  // a constant after unrolling
+      base[i] = q * x + (x * (x + 1) / 2) + tq;
+#else
       const unsigned R = O + 16 * I + q + 4 * i;
       base[i] = (int)((R * (R + 1)) >> 1) + O + c;
+#endif
     }
     d4_t acc[I + 1];
 #pragma unroll
@@ -1388,7 +1420,7 @@ UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop
 #pragma unroll
       for (int i = 0; i < 4; i++)
         if (J < I || c <= q + 4 * i) S[base[i] + 16 * J] = acc[J][i];
-    rankm_block<DOF, I + 1, NT>(S, Aop, Bop, q, c);
+    rankm_block<DOF, I + 1, NT>(S, Aop, Bop, q, c, tq);
   }
 }
 
@@ -1457,7 +1489,7 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
       }
     }
   }
-  rankm_block<DOF, 0, NT>(S, Aop, Bop, q, c);
+  rankm_block<DOF, 0, NT>(S, Aop, Bop, q, c, ((q * (q + 1)) >> 1) + O + c);
 }
 
 // rankm_mfma_o with every tile in flight at once (PSP_RANKM_MFMA == 3): all
