@@ -320,6 +320,12 @@ UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 #ifndef PSP_PIDX_SEL  // r03: packed indices of the predict's rows < 12 by pidx_sel
 #define PSP_PIDX_SEL 1
 #endif
+#ifndef PSP_CHOL_RL1  // r04 A/B: the partial Cholesky's next-column entry by readlane instead of LDS
+#define PSP_CHOL_RL1 0
+#endif
+#ifndef PSP_BAND_PRE  // r04: the Q band's three entries loaded before the masked stores (no waits in branches)
+#define PSP_BAND_PRE 1
+#endif
 #ifndef PSP_CPL_FMA  // r04: the predict's A-coupled rows read the coupled column unconditionally (FMA with 0 / dt)
 #define PSP_CPL_FMA 1
 #endif
@@ -395,7 +401,10 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
       // slot c at step c, after this step's reads (one wave: LDS in order)
       // (PSP_LDS_ALIGN with PSP_STAGE_LATE: slot c + 1 when J + 1 is even, so
       // that the reads start on a 16-byte boundary; col is odd-aligned)
-      double* const cj = col + ((PSP_LDS_ALIGN && PSP_STAGE_LATE && ((J + 1) & 1) == 0) ? 1 : 0);
+      // (PSP_CHOL_RL1: the next column's entry L[J+1][J] by readlane, the
+      // LDS reads start at J + 2 and are aligned from there)
+      constexpr int C0 = PSP_CHOL_RL1 ? J + 2 : J + 1;
+      double* const cj = col + ((PSP_LDS_ALIGN && PSP_STAGE_LATE && (C0 & 1) == 0) ? 1 : 0);
 #if PSP_STAGE_LATE && PSP_COL_SEL == 2
       // r04: every lane stores its a[J] to slot r: the slots read this step
       // are (J, K), which only the lanes r in (J, K) write; the others land in
@@ -413,11 +422,18 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
 #else
       if (r > J && r < K) cj[r] = a[J];
 #endif
+#if PSP_CHOL_RL1
+      // (r04) L[J+1][J], the one entry the next step's scale waits for, as a
+      // readlane of lane J + 1 (two SGPR reads, no LDS round trip on the
+      // step-to-step chain); the rest of the column through LDS as before
+      const double cn = readlane_d(a[J], J + 1);
+      a[J + 1] -= a[J] * cn;
+#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-      for (int c = J + 1; c < K; c++) a[c] -= a[J] * cj[c];
+      for (int c = C0; c < K; c++) a[c] -= a[J] * cj[c];
 #pragma unroll
       for (int c = J + 1; c < K; c++) asm volatile("" : "+v"(a[c]));
     }
@@ -1014,6 +1030,39 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     for (int i = 0; i < 4; i++) asm volatile("" : "+s"(qw4[i]));
     auto band = [&](auto QS) {
       constexpr bool kQS = decltype(QS)::value;
+#if PSP_BAND_PRE
+      if constexpr (kQS) {
+        // (r04) the three entries (l, l - k) loaded unconditionally (clamped
+        // into the triangle), then stored under the lane's mask: the masked
+        // read-modify-write per k waited for its own load (lgkmcnt(0)) inside
+        // an exec branch, three times in a row
+        const int lc = l < DOF ? l : DOF - 1;
+        const int T = (lc * (lc + 1)) >> 1;
+        double v[3], f[3];
+        int e[3];
+        bool w[3];
+        double idk = ids;  // 1 / d'_{l-k}
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          if (k > 0) idk = dpp_d<0x138, 0xf, 0xf>(idk);  // wave_shr:1 -> lane l - k
+          const int j = l - k;
+          e[k] = T + (j >= 0 ? (j <= lc ? j : lc) : 0);
+          v[k] = sm.S[e[k]];
+          double q = k == 0 ? lq.q0 : (k == 1 ? lq.q1 : lq.q2);
+          if (k == 0 && l >= L::d_wv && l < L::d_wv + 4) {
+            const int iw = l - L::d_wv;
+            const double qw = iw == 0 ? qw4[0] : (iw == 1 ? qw4[1] : (iw == 2 ? qw4[2] : qw4[3]));
+            q = dt2 * (qw + wv_add);
+          }
+          w[k] = l >= R0 && l < DOF && j >= R0 && k <= bw && q != 0.0;
+          f[k] = q * (ids * idk);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+          if (w[k]) sm.S[e[k]] = v[k] + f[k];
+        return;
+      }
+#endif
       double idk = ids;  // 1 / d'_{l-k}
 #pragma unroll
       for (int k = 0; k < 3; k++) {
@@ -1089,8 +1138,16 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   }
   PSP_PHASE(25);
   // new mean: vect parts f(mu), orientation the manifold mean
+#if PSP_BAND_PRE
+  // every lane evaluates (reads past mu land in the staging area, never
+  // stored): the loads need no exec branch and wait
+  static_assert(Lay<DOF>::store + PG<DOF>::STG >= 64, "mu reads of lanes >= store stay in PspSmem");
+  double mv = proc_vect_lane(l & 63, sm.mu, pc);
+  asm volatile("" : "+v"(mv));
+#else
   double mv = 0.0;
   if (l < L::store && !(l >= 3 && l < 7)) mv = proc_vect_lane(l, sm.mu, pc);
+#endif
   psync();
   if (l < L::store && !(l >= 3 && l < 7)) sm.mu[l] = mv;
   if (l < 4) sm.mu[3 + l] = mq[l];
@@ -1475,6 +1532,29 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
     for (int j = 0; j < O; j++)
 #pragma unroll
       for (int k = 0; k < M; k++) kc[j][k] = kStripLds ? stg[32 * M + j * M + k] : readlane_d(Kt[k], j);
+#if PSP_BAND_PRE
+    {
+      // (r04) every lane loads its row (clamped to the last one) outside any
+      // branch; only the stores are masked to the rows of the triangle
+      const int lc = l < DOF ? l : DOF - 1;
+      const int b0 = (lc * (lc + 1)) >> 1;
+      double sv[O];
+#pragma unroll
+      for (int j = 0; j < O; j++) sv[j] = S[b0 + (j <= lc ? j : lc)];
+      double nv[O];
+#pragma unroll
+      for (int j = O - 1; j >= 0; j--) {
+        double s2 = sv[j];
+#pragma unroll
+        for (int k = 0; k < M; k++) s2 = fma(-Ct[k], kc[j][k], s2);
+        nv[j] = s2;
+      }
+      if (l < DOF) {
+#pragma unroll
+        for (int j = O - 1; j >= 0; j--) S[b0 + (j <= lc ? j : lc)] = nv[j];
+      }
+    }
+#else
     if (l < DOF) {
       const int b0 = (l * (l + 1)) >> 1;
       double sv[O];
@@ -1488,6 +1568,7 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
         S[b0 + (j <= l ? j : l)] = s2;
       }
     }
+#endif
   }
   rankm_block<DOF, 0, NT>(S, Aop, Bop, q, c, ((q * (q + 1)) >> 1) + O + c);
 }
@@ -1960,6 +2041,44 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       const double tq[4] = {eq[0], SR ? -eq[1] : eq[1], SR ? -eq[2] : eq[2], SR ? -eq[3] : eq[3]};
       qmatrix(tq, R);
     }
+#if PSP_BAND_PRE
+    // (r04) rows 3..5 of every column j outside the block, and the ori x ori
+    // block R B R^T: every lane loads and computes (its column clamped into
+    // the triangle; the block's lanes 3..5 and lanes >= 9 compute values that
+    // are not stored), only the stores are masked: no load waits in branches.
+    // The block is disjoint from the rows' entries, so its loads go first too.
+    double nb;
+    {
+      const int lc = l < DOF ? l : DOF - 1;
+      const int Tl = (lc * (lc + 1)) >> 1;
+      const int e0 = pidx_sel(3, lc, Tl), e1 = pidx_sel(4, lc, Tl), e2 = pidx_sel(5, lc, Tl);
+      double s0 = sm.S[e0], s1 = sm.S[e1], s2 = sm.S[e2];
+      asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2));  // loaded here, not sunk into the store branch
+      double B[9];
+#pragma unroll
+      for (int u = 0; u < 3; u++)
+#pragma unroll
+        for (int v = 0; v < 3; v++) B[u * 3 + v] = sm.S[pidx(3 + u, 3 + v)];
+      const int r = l / 3, c = l % 3;  // (r >= 3 for lanes >= 9: not stored)
+      double sb = 0.0;
+#pragma unroll
+      for (int u = 0; u < 3; u++) {
+        double t = 0.0;
+#pragma unroll
+        for (int v = 0; v < 3; v++) t += B[u * 3 + v] * sel3(R[v], R[3 + v], R[6 + v], c);
+        sb += sel3(R[u], R[3 + u], R[6 + u], r) * t;
+      }
+      nb = sb;
+      double n3[3];
+#pragma unroll
+      for (int i = 0; i < 3; i++) n3[i] = R[i * 3] * s0 + R[i * 3 + 1] * s1 + R[i * 3 + 2] * s2;
+      if (l < DOF && !(l >= 3 && l < 6)) {
+        sm.S[e0] = n3[0];
+        sm.S[e1] = n3[1];
+        sm.S[e2] = n3[2];
+      }
+    }
+#else
     // rows 3..5 of every column j outside the block
     if (l < DOF && !(l >= 3 && l < 6)) {
 #if PSP_PIDX_SEL
@@ -1987,10 +2106,16 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       }
       nb = s;
     }
+#endif
     // storage s = l takes tangent delta_{l} (l < 3) or delta_{l-1} (l >= 7): DPP wave_shr:1
     const double dsh = dpp_d<0x138, 0xf, 0xf>(dl);
+#if PSP_BAND_PRE
+    double mnew = sm.mu[l & 63] + 1.0 * (l < 3 ? dl : dsh);  // stored for the vector lanes only
+    asm volatile("" : "+v"(mnew));
+#else
     double mnew = 0.0;
     if (l < L::store && !(l >= 3 && l < 7)) mnew = sm.mu[l] + 1.0 * (l < 3 ? dl : dsh);
+#endif
     double qn[4];
     qplus_psp<SR>(eq, sm.mu + L::s_quat, qn);
     psync();

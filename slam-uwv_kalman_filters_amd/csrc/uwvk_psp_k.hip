@@ -166,16 +166,43 @@ UWVK_DEV void lane_proc(const PoseBufs& b, const PoseShared& sh, int64_t inst, i
   if (s < DOF && scaled_dof(s)) pc.nt_tan = tan_ntau_sel<DOF>(s, sh);
 }
 
+#ifndef PSP_STORE_PRE  // r04: the epilogue's LDS reads issued before the masked HBM stores
+#define PSP_STORE_PRE 1
+#endif
 template <int DOF>
 UWVK_DEV void store_psp(const PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst, int l = lane_id()) {
   using G = PG<DOF>;
   double* gs = b.sigma + inst * (int64_t)G::NP;
+#if PSP_STORE_PRE
+  // (r04) every slot's LDS read first (the last, partial slot's lanes past the
+  // triangle read the mean / staging area behind it, never stored), then the
+  // coalesced stores: the masked form waited for each read inside its branch
+  // in groups of SG slots (all of them at once held 30 more VGPRs at the
+  // epilogue: 178, 2 waves per SIMD)
+  static_assert(G::NSLOT * 64 <= G::NP + Lay<DOF>::store + PG<DOF>::STG, "slot over-read stays in PspSmem");
+  constexpr int SG = 6;
+#pragma unroll
+  for (int t0 = 0; t0 < G::NSLOT; t0 += SG) {
+    double v[SG];
+#pragma unroll
+    for (int u = 0; u < SG; u++)
+      if (t0 + u < G::NSLOT) v[u] = sm.S[l + 64 * (t0 + u)];
+#pragma unroll
+    for (int u = 0; u < SG; u++) {
+      const int t = t0 + u, e = l + 64 * t;
+      if (t < G::NSLOT && (t + 1 < G::NSLOT || e < G::NP)) gs[e] = v[u];
+    }
+  }
+  const double m = sm.mu[l & 63];
+  if (l < Lay<DOF>::store) b.mu[inst * Lay<DOF>::store + l] = m;
+#else
 #pragma unroll 4
   for (int t = 0; t < G::NSLOT; t++) {
     const int e = l + 64 * t;
     if (e < G::NP) gs[e] = sm.S[e];
   }
   if (l < Lay<DOF>::store) b.mu[inst * Lay<DOF>::store + l] = sm.mu[l];
+#endif
 }
 
 template <int M>
