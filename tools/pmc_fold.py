@@ -82,6 +82,23 @@ if has_mfma:
         "busy_definition": "SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CU_CYCLES",
         "counters": mfma,
     }
+# LDS passes (tools/pmc_lds.sh, r04), when present: LDS-array occupancy next to the VALU
+rows_l = []
+if os.path.exists(os.path.join(base, "lds", "run_counter_collection.csv")):
+    lds, _, rows_l1 = last("lds")
+    lds2, _, rows_l2 = last("lds2") if os.path.exists(os.path.join(base, "lds2", "run_counter_collection.csv")) else ({}, None, [])
+    rows_l = rows_l1 + rows_l2
+    cu_cycles = 256.0 * lds["GRBM_GUI_ACTIVE"] / 8.0
+    e["lds"] = {
+        "insts_per_wave_epoch": lds["SQ_INSTS_LDS"] / we,
+        "array_cycles_per_wave_epoch": lds["SQ_LDS_IDX_ACTIVE"] / we,
+        "bank_conflict_cycles_per_wave_epoch": lds["SQ_LDS_BANK_CONFLICT"] / we,
+        "array_busy_frac": lds["SQ_LDS_IDX_ACTIVE"] / cu_cycles,
+        "array_busy_definition": "SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM_GUI_ACTIVE / 8 XCDs)",
+        "counters": dict(lds, **lds2),
+    }
+    if lds2:
+        e["lds"]["wait_inst_lds_frac_of_wave_cycles"] = lds2["SQ_WAIT_INST_LDS"] / lds2["SQ_WAVE_CYCLES"]
 e["source"] = ("profiles/%s/pmc_%s_s%d.csv (rocprofv3 --pmc, one pass per counter group; dispatch %d = the %d-epoch "
                "timed launch; FETCH_SIZE doubled per MI355X_MICROARCH.md)" % (rdir, tag, steps, d3, steps))
 e["valu_source"] = "profiles/%s/pmc_%s_s%d.csv (dispatch %d)" % (rdir, tag, steps, d1)
@@ -95,11 +112,14 @@ keep = ("Dispatch_Id", "Kernel_Name", "Grid_Size", "VGPR_Count", "SGPR_Count", "
 with open(os.path.join(ROOT, "profiles", rdir, "pmc_%s_s%d.csv" % (tag, steps)), "w") as f:
     w = csv.DictWriter(f, fieldnames=list(keep))
     w.writeheader()
-    for rows in (rows_mix, rows_busy, rows_f, rows_w, rows_m):
+    for rows in (rows_mix, rows_busy, rows_f, rows_w, rows_m, rows_l):
         for r in rows:
             w.writerow({k: r[k] for k in keep})
 shutil.copy(os.path.join(base, "trace", "run_kernel_stats.csv"),
             os.path.join(ROOT, "profiles", rdir, "kernel_stats_%s_s%d.csv" % (tag, steps)))
+if os.path.exists(os.path.join(base, "trace", "run_kernel_trace.csv")):
+    shutil.copy(os.path.join(base, "trace", "run_kernel_trace.csv"),
+                os.path.join(ROOT, "profiles", rdir, "kernel_trace_%s_s%d.csv" % (tag, steps)))
 shutil.copy(os.path.join(base, "trace.json"), os.path.join(ROOT, "profiles", rdir, "bench_%s_s%d_traced.json" % (tag, steps)))
 print(json.dumps({k: v for k, v in e.items() if k != "valu_busy"}, indent=1))
 print("valu_busy", e["valu_busy"]["frac"], "model", e["valu_busy"]["model_frac"])
