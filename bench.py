@@ -136,6 +136,9 @@ def parse():
                          "0 one workgroup per instance, -1 the engine default")
     ap.add_argument("--tail-slots", type=int, default=0,
                     help="UWVK_OPT_TAIL_SLOTS: 0 runtime occupancy, > 0 blocks per XCD, < 0 no tail spreading")
+    ap.add_argument("--config", default="",
+                    help="YAML / JSON filter configuration (uwvk.config: PoseUKFConfig, UWVParameters, engine "
+                         "options) instead of the synthetic defaults; the line names it in config.config_file")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core available to this process")
     ap.add_argument("--init", default="mc", choices=["mc", "config"],
                     help="mc: Monte-Carlo start drawn around the truth from priors small enough for a consistent "
@@ -144,7 +147,7 @@ def parse():
     return ap.parse_args()
 
 
-def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance, c4_cycle=(30.0, 10.0)):
+def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance, c4_cycle=(30.0, 10.0), cfg=None):
     """Log of warmup+steps epochs whose 5 Hz DVL schedule puts at least one DVL
     epoch inside the timed window (exactly the 1-in-200 rate when steps >= 200)."""
     total = warmup + steps
@@ -156,7 +159,7 @@ def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance, c4_c
     # reports dvl_epochs_in_window either way
     shift += int(os.environ.get("UWVK_BENCH_WINDOW_OFFSET", "0"))
     log = synth.make_pose_log(batch, total + shift, mode=mode, dof=dof, first_instance=first_instance,
-                              dropout_on=c4_cycle[0], dropout_off=c4_cycle[1])
+                              dropout_on=c4_cycle[0], dropout_off=c4_cycle[1], cfg=cfg)
     return log, shift
 
 
@@ -231,7 +234,7 @@ def cpu_baseline(synth, cfg, uwv, mode, dof, threads, init="mc", right=False):
             return cpu_baseline(synth, cfg, uwv, mode, dof, threads, init, right=False)
     epochs = 2000
     # single core first: it sizes the multi-core sample to ~15 s of wall time
-    log1 = synth.make_pose_log(1, epochs, mode=mode, dof=dof)
+    log1 = synth.make_pose_log(1, epochs, mode=mode, dof=dof, cfg=cfg)
     o1 = O.OraclePoseBatch(1, dof, timing=True)
     initialise(o1, log1, cfg, uwv, init)
     o1.set_process_noise_from_config(cfg, log1["dt"])
@@ -241,7 +244,7 @@ def cpu_baseline(synth, cfg, uwv, mode, dof, threads, init="mc", right=False):
     rate1 = epochs / dt1
     per_thread = max(1, int(round(15.0 * rate1 / epochs)))
     batch = per_thread * threads
-    log = synth.make_pose_log(batch, epochs, mode=mode, dof=dof)
+    log = synth.make_pose_log(batch, epochs, mode=mode, dof=dof, cfg=cfg)
     o = O.OraclePoseBatch(batch, dof, timing=True)
     initialise(o, log, cfg, uwv, init)
     o.set_process_noise_from_config(cfg, log["dt"])
@@ -436,9 +439,16 @@ def main():
     if mode == "C2":
         return bench_vel(a, engine, synth, world, rank, local, dist, B)
     log_mode = "C3" if mode == "C5" else mode
-    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    cfg, uwv, eng_opts = synth.default_pose_config(), synth.default_uwv(), {}
+    if a.config:
+        from uwvk import config as uconfig
+        fc = uconfig.load(a.config)
+        cfg, uwv, eng_opts = fc.pose, fc.uwv, fc.engine
+        if eng_opts.get("so3_right"):
+            a.so3_right = True  # the side also selects the kernel name and the CPU baseline's side
     cyc = tuple(float(v) for v in a.c4_cycle.split(","))
-    log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, log_mode, a.dof, first_instance=rank * B, c4_cycle=cyc)
+    log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, log_mode, a.dof, first_instance=rank * B, c4_cycle=cyc,
+                                 cfg=cfg)
     f = engine.PoseUKFBatch(B, a.dof, device=local)
     f.set_tail_slots(a.tail_slots)
     if a.persist >= 0:
@@ -447,6 +457,8 @@ def main():
         f.set_tail_chunks(a.tail_chunks)
     if a.dense:
         f.set_dense_sigma(True)
+    if eng_opts:
+        uconfig.apply_engine_options(f, eng_opts)
     if a.so3_right:
         f.set_so3_right(True)
     initialise(f, log, cfg, uwv, a.init, first_instance=rank * B)
@@ -603,7 +615,8 @@ def main():
                            if a.init == "mc" else "first constructor (prior from the config)",
                    "path": "dense (all 2n+1 sigma points)" if a.dense else "PSP (partitioned sigma points)",
                    "so3_boxplus": "right (body frame, q exp(d))" if a.so3_right else "left (nav frame, exp(d) q)",
-                   "kernel": kname},
+                   "kernel": kname,
+                   "config_file": a.config or None},
         "collective_check": coll_check,
         "roofline": roof,
         "timing": {"wall_ms": wall * 1e3, "kernel_ms": kernel_ms, "outside_kernel_ms": wall * 1e3 - kernel_ms},
