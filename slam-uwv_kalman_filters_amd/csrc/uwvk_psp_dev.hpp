@@ -170,24 +170,36 @@ UWVK_DEV double wave_sum_dpp(double v) {
 // in the common case; truncation < 1e-20 relative inside the thresholds; the
 // library forms are the fallback).
 // ---------------------------------------------------------------------------
+// (r04) PSP_SCONST: a series coefficient as a uniform (SGPR) operand of its FMA.
+// Without it every coefficient was rebuilt in a VGPR pair by two v_mov_b32 per
+// use (~150 VALU per instance-epoch, on the kernel's bound unit); an empty asm
+// pins the value to an SGPR pair, made by two s_mov_b32 on the scalar unit.
+#ifndef PSP_SCONST
+#define PSP_SCONST 1
+#endif
+UWVK_DEV double sk(double c) {
+#if PSP_SCONST
+  asm volatile("" : "+s"(c));
+#endif
+  return c;
+}
 UWVK_DEV void so3_exp_psp(const double v[3], double o[4]) {
   const double t2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
   if (t2 < 0.0625) {  // |v| < 0.25: h = |v|/2 < 0.125, u = h^2
     const double u = 0.25 * t2;
-    // sin(h) / (2h) and cos(h), Horner in u
-    double s = 1.0 / 6227020800.0;
-    s = fma(s, u, -1.0 / 39916800.0);
-    s = fma(s, u, 1.0 / 362880.0);
-    s = fma(s, u, -1.0 / 5040.0);
-    s = fma(s, u, 1.0 / 120.0);
-    s = fma(s, u, -1.0 / 6.0);
+    // sin(h) / (2h) and cos(h), Horner in u; the next terms, u^6 / 13! and
+    // u^6 / 12!, are < 3e-20 relative for u < 1/64 (r04: dropped)
+    double s = u * sk(-1.0 / 39916800.0);
+    s = s + sk(1.0 / 362880.0);
+    s = fma(s, u, sk(-1.0 / 5040.0));
+    s = fma(s, u, sk(1.0 / 120.0));
+    s = fma(s, u, sk(-1.0 / 6.0));
     s = fma(s, u, 1.0);
     s = 0.5 * s;
-    double c = 1.0 / 479001600.0;
-    c = fma(c, u, -1.0 / 3628800.0);
-    c = fma(c, u, 1.0 / 40320.0);
-    c = fma(c, u, -1.0 / 720.0);
-    c = fma(c, u, 1.0 / 24.0);
+    double c = u * sk(-1.0 / 3628800.0);
+    c = c + sk(1.0 / 40320.0);
+    c = fma(c, u, sk(-1.0 / 720.0));
+    c = fma(c, u, sk(1.0 / 24.0));
     c = fma(c, u, -0.5);
     c = fma(c, u, 1.0);
     o[0] = c; o[1] = s * v[0]; o[2] = s * v[1]; o[3] = s * v[2];
@@ -209,15 +221,13 @@ UWVK_DEV void so3_log_psp(const double q[4], double o[3]) {
     const double iw = 1.0 / w;
 #endif
     const double r2 = n2 * (iw * iw);
-    // atan(r)/r = sum (-r^2)^k / (2k+1), k <= 8
-    double a = 1.0 / 17.0;
-    a = fma(a, -r2, 1.0 / 15.0);
-    a = fma(a, -r2, 1.0 / 13.0);
-    a = fma(a, -r2, 1.0 / 11.0);
-    a = fma(a, -r2, 1.0 / 9.0);
-    a = fma(a, -r2, 1.0 / 7.0);
-    a = fma(a, -r2, 1.0 / 5.0);
-    a = fma(a, -r2, 1.0 / 3.0);
+    // atan(r)/r = sum (-r^2)^k / (2k+1), k <= 6 (k = 7: < 5e-20 for r^2 < 0.0025)
+    double a = r2 * sk(-1.0 / 13.0);
+    a = fma(a, -r2, sk(1.0 / 11.0));
+    a = fma(a, -r2, sk(1.0 / 9.0));
+    a = fma(a, -r2, sk(1.0 / 7.0));
+    a = fma(a, -r2, sk(1.0 / 5.0));
+    a = fma(a, -r2, sk(1.0 / 3.0));
     a = fma(a, -r2, 1.0);
     const double k = 2.0 * a * iw;  // 2 atan2(|v|, w) / |v|
     o[0] = k * x; o[1] = k * y; o[2] = k * z;
@@ -551,8 +561,8 @@ UWVK_DEV void proc_orientation(const double x[Lay<DOF>::store], const PoseShared
   double sl, cl;
   if (fabs(dl) < 0.01) {
     const double u = dl * dl;
-    double sd = fma(fma(fma(fma(1.0 / 362880.0, u, -1.0 / 5040.0), u, 1.0 / 120.0), u, -1.0 / 6.0), u, 1.0) * dl;
-    double cd = fma(fma(fma(fma(1.0 / 40320.0, u, -1.0 / 720.0), u, 1.0 / 24.0), u, -0.5), u, 1.0);
+    double sd = fma(fma(fma(u * sk(1.0 / 362880.0) + sk(-1.0 / 5040.0), u, sk(1.0 / 120.0)), u, sk(-1.0 / 6.0)), u, 1.0) * dl;
+    double cd = fma(fma(fma(u * sk(1.0 / 40320.0) + sk(-1.0 / 720.0), u, sk(1.0 / 24.0)), u, -0.5), u, 1.0);
     sl = sh.slat0 * cd + sh.clat0 * sd;
     cl = sh.clat0 * cd - sh.slat0 * sd;
   } else {
