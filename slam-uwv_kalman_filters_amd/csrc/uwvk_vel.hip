@@ -61,6 +61,15 @@ UWVK_DEV LVS& vlaunder(LVS& p) {
   asm volatile("" : "+v"(q));
   return *q;
 }
+// (r04) VEL_SMEM: the device copy in the constant address space, its pointer
+// re-laundered (an SGPR pair) before every derivative, so that the matrices
+// arrive by scalar loads (s_load, the scalar data cache) next to their use
+using GVS = __attribute__((address_space(4))) const VelShared;
+UWVK_DEV GVS& vlaunder(GVS& p) {
+  GVS* q = &p;
+  asm volatile("" : "+s"(q));
+  return *q;
+}
 
 // ---- [EXT] ModelSimulation: M nu_dot + C(nu) nu + D(nu) nu + g(q) = tau, RK4 --
 template <class PS>
@@ -237,7 +246,8 @@ UWVK_DEV void v_cov(const double (&X)[9][4], const double mean[4], double S[16])
 }
 
 // processMotionModel, VelocityUKF.cpp:6-33
-UWVK_DEV void v_process(const VelShared& P, const double q[4], const double w[3], const double tau[6], double dt,
+template <class PS>
+UWVK_DEV void v_process(const PS& P, const double q[4], const double w[3], const double tau[6], double dt,
                         double x[4]) {
   double s[13], n[13], r[3], t[3];
   s[0] = s[1] = s[2] = 0.0;
@@ -253,7 +263,8 @@ UWVK_DEV void v_process(const VelShared& P, const double q[4], const double w[3]
   x[0] = t[0]; x[1] = t[1]; x[2] = t[2];
 }
 
-UWVK_DEV bool v_predict(const VelShared& P, double mu[4], double S[16], const double model[13], const double w[3],
+template <class PS>
+UWVK_DEV bool v_predict(const PS& P, double mu[4], double S[16], const double model[13], const double w[3],
                         const double tau[6], double dt) {
   double L[16], X[9][4];
   const bool ok = v_chol(S, L);
@@ -379,7 +390,22 @@ UWVK_DEV void v_store(const VelBufs& b, int64_t i, const double mu[4], const dou
   for (int k = 0; k < 16; k++) b.sigma[i * 16 + k] = S[k];
 }
 
-__global__ __launch_bounds__(64) void k_vel_predict(VelBufs b, VelShared P, double dt) {
+// (r04) the model parameters by scalar loads from the handle's device copy
+// (VEL_SMEM, vlaunder above): the by-value kernel argument (144 doubles of
+// matrices) did not fit the SGPRs, was spilled to VGPR lanes and read back by
+// ~1,000 v_readlane per epoch; C2 534.6-542.1 -> 620.3-620.9 M steps/s
+// (profiles/r04/c2smem/)
+#ifndef VEL_SMEM
+#define VEL_SMEM 1
+#endif
+#if VEL_SMEM
+#define VEL_PARAMS(b, P0) GVS& P = *(GVS*)(b).shared; (void)(P0)
+#else
+#define VEL_PARAMS(b, P0) const VelShared& P = (P0)
+#endif
+
+__global__ __launch_bounds__(64) void k_vel_predict(VelBufs b, VelShared P0, double dt) {
+  VEL_PARAMS(b, P0);
   const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= b.batch) return;
   double mu[4], S[16], m[13], w[3], tau[6];
@@ -417,7 +443,8 @@ __global__ __launch_bounds__(64) void k_vel_update(VelBufs b, const double* z, c
   (void)shared_cov0;
 }
 
-__global__ __launch_bounds__(64) void k_vel_epoch(VelBufs b, VelShared P, VelEpochArgs ea) {
+__global__ __launch_bounds__(64) void k_vel_epoch(VelBufs b, VelShared P0, VelEpochArgs ea) {
+  VEL_PARAMS(b, P0);
   const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= b.batch) return;
   const int64_t B = b.batch;
@@ -636,7 +663,9 @@ constexpr int VG = 16;  // lanes per filter
 #define VEL_LDS 0  // r04 A/B: 474.5 against 546.8 M steps/s on C2 (profiles/r04/c2ab/), not kept
 #endif
 __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, VelEpochArgs ea) {
-#if VEL_LDS
+#if VEL_SMEM
+  VEL_PARAMS(b, P0);
+#elif VEL_LDS
   // the model parameters in LDS (one copy per workgroup), read per derivative
   __shared__ VelShared sp;
   {
