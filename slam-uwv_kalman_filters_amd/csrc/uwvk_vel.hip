@@ -690,11 +690,37 @@ __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, Vel
   for (int k = 0; k < 13; k++) m[k] = b.model[i * 13 + k];
   double q[4] = {m[3], m[4], m[5], m[6]};
   bool ok = true;
+#ifndef VEL_PREFETCH
+#define VEL_PREFETCH 1
+#endif
+#if VEL_PREFETCH
+  // (r04) the next epoch's gyro / efforts / flag word issued one epoch ahead:
+  // at one wave per SIMD the loads' latency was exposed at the top of every epoch
+  double w_n[3] = {0, 0, 0}, tau_n[6] = {0, 0, 0, 0, 0, 0};
+  uint32_t fl_n = 0;
+  auto fetch = [&](int64_t e) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) w_n[k] = ea.gyro[(e * B + i) * 3 + k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) tau_n[k] = ea.efforts[(e * B + i) * 6 + k];
+    fl_n = ea.flags[e + (g >> 4)];  // a lane-dependent (zero) offset: a VGPR until used
+  };
+  if (ea.count > 0) fetch(ea.first);
+#endif
   for (int64_t e = ea.first; e < ea.first + ea.count; e++) {
+#if VEL_PREFETCH
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(fl_n);
+#pragma unroll
+    for (int k = 0; k < 3; k++) { w[k] = w_n[k]; m[10 + k] = w[k]; }
+#pragma unroll
+    for (int k = 0; k < 6; k++) tau[k] = tau_n[k];
+    if (e + 1 < ea.first + ea.count) fetch(e + 1);
+#else
 #pragma unroll
     for (int k = 0; k < 3; k++) { w[k] = ea.gyro[(e * B + i) * 3 + k]; m[10 + k] = w[k]; }
 #pragma unroll
     for (int k = 0; k < 6; k++) tau[k] = ea.efforts[(e * B + i) * 6 + k];
+#endif
     // predict (VelocityUKF.cpp:115-128): point lanes integrate their sigma
     // point, lane 9 the side model, in one RK4 pass
     double L[16], x[4];
@@ -729,7 +755,9 @@ __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, Vel
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) q[k] = row_bcast(side ? m[3 + k] : 0.0, 9);
+#if !VEL_PREFETCH
     const uint32_t fl = ea.flags[e];
+#endif
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + i) * 3;
       const double zz[3] = {z[0], z[1], z[2]};
