@@ -178,6 +178,60 @@ def test_velocity_ukf_process_noise(eng, orc, groups):
     assert cov_err(Pg, Po).max() < TOL_LOG
 
 
+@pytest.mark.parametrize("groups", [0, 1])
+def test_velocity_ukf_model_change_between_runs(eng, orc, groups):
+    """The VelocityUKF kernels read the model parameters from the handle's
+    device copy (VEL_SMEM): setupMotionModel (VelocityUKF.cpp:65-74) and
+    setProcessNoiseCovariance between two run_log calls must reach the second
+    run.  The second model has off-diagonal inertia / damping couplings (every
+    entry of the 6x6 matrices is used), and the single-call predict after it
+    goes through k_vel_predict."""
+    from uwvk import abi, synth
+    B = 12
+    log = synth.make_vel_log(B, 400)
+    uwv2 = synth.default_uwv()
+    M, Dl, Dq = synth.uwv_arrays(uwv2)
+    C = np.zeros((6, 6))
+    C[0, 4] = C[4, 0] = 8.0
+    C[1, 3] = C[3, 1] = -6.0
+    C[2, 5] = C[5, 2] = 3.0
+    abi.fill(uwv2.inertia_matrix, (M * 1.3 + C).ravel())
+    abi.fill(uwv2.damping_matrices[0], (Dl * 0.7 + 0.5 * C).ravel())
+    abi.fill(uwv2.damping_matrices[1], (Dq * 1.5 + 0.25 * np.abs(C)).ravel())
+    Q2 = np.diag([3e-2, 2e-2, 1e-2, 4e-3])
+    o, g = orc.OracleVelBatch(B), eng.VelocityUKFBatch(B)
+    g.set_lane_groups(groups)
+    for f in (o, g):
+        f.init(log["x0"], log["P0"])
+        f.set_gyro(log["gyro"][0])
+        f.setup_motion_model(synth.default_uwv())
+    o.run_log(log, 0, 200)
+    dlog = g.upload_log(log)
+    g.run_log(dlog, 0, 200)
+    for f in (o, g):
+        f.setup_motion_model(uwv2)
+        f.set_process_noise(Q2)
+    o.run_log(log, 200, 199)
+    g.run_log(dlog, 200, 199)
+    for f in (o, g):
+        f.set_gyro(log["gyro"][399])
+        f.set_efforts(log["efforts"][399])
+        f.predict(log["dt"])
+    (xo, Po, mo), (xg, Pg, mg) = o.get_state(model=True), g.get_state(model=True)
+    sd = np.sqrt(np.diagonal(Po, axis1=1, axis2=2))
+    assert np.max(np.abs(xg - xo) / sd) < TOL_LOG
+    assert cov_err(Pg, Po).max() < TOL_LOG
+    assert np.max(np.abs(mg - mo)) < 1e-9
+    # the change mattered: the default model over the same log ends elsewhere
+    d = eng.VelocityUKFBatch(B)
+    d.set_lane_groups(groups)
+    d.init(log["x0"], log["P0"])
+    d.set_gyro(log["gyro"][0])
+    d.setup_motion_model(synth.default_uwv())
+    d.run_log(d.upload_log(log), 0, 399)
+    assert np.max(np.abs(d.get_state()[0] - xo) / sd) > 1e-3
+
+
 def test_velocity_ukf_api(eng, orc):
     from uwvk import synth
     B = 8
