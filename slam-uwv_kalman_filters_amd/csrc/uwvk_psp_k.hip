@@ -407,30 +407,13 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
 #else
   (void)tlw;
 #endif
-  if (PERSIST && PSP_PREFETCH && pre->have) {
-    using G = PG<DOF>;
-    const int l = olane();
-#pragma unroll
-    for (int t = 0; t < G::NSLOT; t++) {
-      const int e = l + 64 * t;
-      if (e < G::NP) sm.S[e] = pre->v[t];
-    }
-    if (l < Lay<DOF>::store) sm.mu[l] = pre->m;
-    psync();
-  } else {
-    load_psp<DOF>(sm, b, inst, PERSIST ? olane() : lane_id());
-  }
-#ifdef UWVK_TIMELINE
-  tl_mark(tlw, 1);
+#ifndef PSP_EARLY_INPUTS
+#define PSP_EARLY_INPUTS 1
 #endif
-  UWVK_STAMP(40);
-  double ds = 1.0, ids = 1.0;  // time scale of the Markov DOFs (Sigma = D Sigma~ D)
-  if (tu0.chunk > 0) {  // the previous chunk's, unfolded: bitwise the one-block run
-    const double2 c = PERSIST ? reinterpret_cast<const double2*>(ea.tail_carry)[tu0.tslot * 64 + lane_id()]
-                              : tail_carry_in(ea, tu0.tslot);
-    ds = c.x;
-    ids = c.y;
-  }
+#if PSP_EARLY_INPUTS
+  // (r04) the unit's independent input loads (rotation rate, per-lane process
+  // constants, the first epoch's IMU) issued before Sigma~'s load is waited
+  // for: one HBM round trip at the unit's start instead of three in a row
   bool ok = true, nan = false;
   uint32_t cnt[4] = {0, 0, 0, 0};
   MeasArgs ma{};
@@ -478,6 +461,80 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     }
   };
   if (e_end > e_begin) fetch(e_begin);
+#endif
+  if (PERSIST && PSP_PREFETCH && pre->have) {
+    using G = PG<DOF>;
+    const int l = olane();
+#pragma unroll
+    for (int t = 0; t < G::NSLOT; t++) {
+      const int e = l + 64 * t;
+      if (e < G::NP) sm.S[e] = pre->v[t];
+    }
+    if (l < Lay<DOF>::store) sm.mu[l] = pre->m;
+    psync();
+  } else {
+    load_psp<DOF>(sm, b, inst, PERSIST ? olane() : lane_id());
+  }
+#ifdef UWVK_TIMELINE
+  tl_mark(tlw, 1);
+#endif
+  UWVK_STAMP(40);
+  double ds = 1.0, ids = 1.0;  // time scale of the Markov DOFs (Sigma = D Sigma~ D)
+  if (tu0.chunk > 0) {  // the previous chunk's, unfolded: bitwise the one-block run
+    const double2 c = PERSIST ? reinterpret_cast<const double2*>(ea.tail_carry)[tu0.tslot * 64 + lane_id()]
+                              : tail_carry_in(ea, tu0.tslot);
+    ds = c.x;
+    ids = c.y;
+  }
+#if !PSP_EARLY_INPUTS
+  bool ok = true, nan = false;
+  uint32_t cnt[4] = {0, 0, 0, 0};
+  MeasArgs ma{};
+  ma.v3[0] = ea.p_sens[0]; ma.v3[1] = ea.p_sens[1]; ma.v3[2] = ea.p_sens[2];
+  // the stored rotation rate (PoseUKF.cpp:492-496) lives in pc.w only (a
+  // second copy for the final store was a second set of loop-carried VGPRs)
+  ProcCtx pc;
+  for (int k = 0; k < 3; k++) pc.w[k] = b.rot[inst * 3 + k];
+#ifndef PSP_DT_VGPR
+#define PSP_DT_VGPR 1
+#endif
+#if PSP_DT_VGPR
+  // dt as a VGPR: a uniform kernel argument is an SGPR pair live across the
+  // whole epoch loop, which the allocator spilled to a VGPR lane and reloaded
+  // (four v_readlane, the whole 16-byte kernarg group) at each of its ~23
+  // uses per epoch (tools/isa_hot.py); as a VGPR each use is an operand
+  {
+    double dtv = ea.dt;
+    asm volatile("" : "+v"(dtv));
+    pc.dt = dtv;
+  }
+#else
+  pc.dt = ea.dt;
+#endif
+  pc.off = nullptr;
+  lane_proc<DOF>(b, *b.shared, inst, lp, pc);
+  // the next epoch's IMU inputs are prefetched one epoch ahead (their load
+  // latency overlaps this epoch's arithmetic)
+  uint32_t fl_n = 0;
+  double g_n[3] = {0, 0, 0}, a_n[3] = {0, 0, 0};
+  auto fetch = [&](int64_t e) {
+#if PSP_FLAG_VGPR
+    // a lane-dependent (always zero) offset keeps the prefetched flag word in a
+    // VGPR until the next epoch reads it: from a uniform address the compiler
+    // moved it to an SGPR at once (readfirstlane + a spill-lane write), waiting
+    // out the load's latency at the top of every epoch
+    fl_n = ea.flags[e + (olane() >> 6)];
+#else
+    fl_n = ea.flags[e];
+#endif
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      g_n[k] = ea.gyro[(e * B + inst) * 3 + k];
+      a_n[k] = ea.acc[(e * B + inst) * 3 + k];
+    }
+  };
+  if (e_end > e_begin) fetch(e_begin);
+#endif
   // persistent: the next unit's ticket, claimed behind the first inputs' loads
   // (a wait for those does not wait for the atomic; it has long returned when
   // the next epoch's loads are waited for)
