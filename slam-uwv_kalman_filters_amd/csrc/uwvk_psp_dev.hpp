@@ -134,6 +134,53 @@ UWVK_DEV int olane() {
   return l;  // (restoring the range with l & 63 measured 1% slower)
 }
 
+// (r04) PSP_LMASK: a condition on the lane id alone as a compile-time lane
+// mask (one wave per instance: lane l is bit l of EXEC).  LANE_IF(l, expr)
+// folds expr over the 64 lanes into a constant and hands it to
+// inverse_ballot: an s_mov of the mask into an SGPR pair, instead of a v_cmp
+// (plus the integer arithmetic on the laundered lane id) per use.  Every PSP
+// kernel is one 64-lane wave per workgroup (__launch_bounds__(64)).
+#ifndef PSP_LMASK
+#define PSP_LMASK 255  // bit set over the site groups (LMG, set per region below)
+#endif
+template <class F>
+UWVK_DEV constexpr unsigned long long lane_mask(F f) {
+  unsigned long long m = 0;
+  for (int i = 0; i < 64; i++)
+    if (f(i)) m |= 1ull << i;
+  return m;
+}
+// A 64-bit mask whose value is a sign-extended 32-bit number but not an
+// inline constant (e.g. lanes >= 5: 0xffffffffffffffe0) was emitted by the
+// compiler as s_mov_b64 with a 32-bit literal, which gfx950 ZERO-extends:
+// lanes 32..63 came out clear (tools/probe_lmask.hip, profiles/r04/lmask/).
+// Such masks are built from their two 32-bit halves through an opaque SGPR
+// pair instead; every other mask is a plain constant.
+UWVK_DEV constexpr bool mask_needs_split(unsigned long long m) {
+  return m >= 0xFFFFFFFF80000000ull && m < 0xFFFFFFFFFFFFFFF0ull;
+}
+UWVK_DEV bool lane_in_split(unsigned long long m) {
+  unsigned lo = (unsigned)m, hi = (unsigned)(m >> 32);
+  asm volatile("" : "+s"(lo), "+s"(hi));
+  return __builtin_amdgcn_inverse_ballot_w64(((unsigned long long)hi << 32) | lo);
+}
+template <unsigned long long M>
+UWVK_DEV bool lane_const() {
+  if constexpr (mask_needs_split(M)) return lane_in_split(M);
+  else return __builtin_amdgcn_inverse_ballot_w64(M);
+}
+#define LMG 0
+#define LANE_IF(l, expr)                                                                                       \
+  ((PSP_LMASK & LMG) ? ({                                                                                      \
+    constexpr unsigned long long m_ = ::uwvk::psp::lane_mask([](int l) constexpr { return (bool)(expr); });   \
+    ::uwvk::psp::lane_const<m_>();                                                                             \
+  })                                                                                                           \
+                     : (bool)(expr))
+#define LANE_IN(m)                                                                                         \
+  ((PSP_LMASK & LMG) ? (::uwvk::psp::mask_needs_split(m) ? ::uwvk::psp::lane_in_split(m)                     \
+                                                         : __builtin_amdgcn_inverse_ballot_w64(m))             \
+                     : ((((m) >> (olane() & 63)) & 1ull) != 0))
+
 // ---------------------------------------------------------------------------
 // DPP wave reductions (no LDS crossbar): row_shr 1/2/3 -> 4-lane sums,
 // row_shr 4/8 with bank masks -> row sums in lane 15 of each row, row_bcast
@@ -374,6 +421,8 @@ UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 // v_readlane per column step, tools/spill_report.py).  The sign test rides on
 // the rsqrt: rsqrt of a pivot <= 0 or NaN is NaN or +-inf, so chk += inv * 0
 // is NaN exactly when some pivot failed piv > 0 (pchol tests chk once).
+#undef LMG
+#define LMG 1
 template <int K, int J>
 UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, double* rows, int q, double piv,
                              double inv_in, double& chk) {
@@ -387,9 +436,9 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
 #if PSP_FAST & 16
     // lane J's own a[J] is the pivot (the look-ahead below evaluates the same
     // fma as the column update), so one product serves the diagonal too
-    a[J] = (r >= J) ? a[J] * inv : 0.0;
+    a[J] = LANE_IF(r, r >= J) ? a[J] * inv : 0.0;
 #else
-    a[J] = (r == J) ? piv * inv : (r > J ? a[J] * inv : 0.0);
+    a[J] = LANE_IF(r, r == J) ? piv * inv : (LANE_IF(r, r > J) ? a[J] * inv : 0.0);
 #endif
     // look-ahead: the next pivot is lane J+1's a[J+1] - L[J+1][J]^2 (its own
     // registers), so its rsqrt need not wait for the column broadcast
@@ -428,9 +477,9 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
       // lanes outside (J, K) store to their own throw-away slot past the column
       // (the rows area is written only after the last step): no exec-masked branch
       static_assert(K + 65 <= 115, "throw-away slots (PG::STG)");
-      cj[(r > J && r < K) ? r : K + (r & 63)] = a[J];
+      cj[LANE_IF(r, r > J && r < K) ? r : K + (r & 63)] = a[J];
 #else
-      if (r > J && r < K) cj[r] = a[J];
+      if (LANE_IF(r, r > J && r < K)) cj[r] = a[J];
 #endif
 #if PSP_CHOL_RL1
       // (r04) L[J+1][J], the one entry the next step's scale waits for, as a
@@ -529,15 +578,17 @@ UWVK_DEV constexpr bool has_rot() {
     if (RL::rows[q] >= 3 && RL::rows[q] < 6) return true;
   return false;
 }
+#undef LMG
+#define LMG 2
 template <class RL, int DOF, int K, int SR>
 UWVK_DEV void gen_rows(const double* mu, const double* stg, int p, double x[Lay<DOF>::store]) {
   using L = Lay<DOF>;
 #pragma unroll
   for (int s = 0; s < L::store; s++) x[s] = mu[s];
   if constexpr (K > 0) {
-    const bool in = p < 2 * K;
+    const bool in = LANE_IF(p, p < 2 * K);
     const int j = in ? (p >> 1) : 0;
-    const double sg = in ? ((p & 1) ? -1.0 : 1.0) : 0.0;  // the centre: mu + 0 (bitwise mu)
+    const double sg = in ? (LANE_IF(p, (p & 1) != 0) ? -1.0 : 1.0) : 0.0;  // the centre: mu + 0 (bitwise mu)
     double v[3] = {0.0, 0.0, 0.0};
     gen_rows_q<RL, DOF, K, 0>(mu, stg, j, sg, v, x);
     if constexpr (has_rot<RL>()) {
@@ -712,6 +763,8 @@ UWVK_DEV LaneQ lane_q(const double* fq, int l) {
 // (sh.q_simple: lane-resident band <= 2), 2 known general.  The epoch kernel is
 // instantiated for 1 and 2 and the host picks one: with both branches in one
 // kernel the epoch loop ran 0.7-0.8% slower (profiles/r03/qm/).
+#undef LMG
+#define LMG 4
 template <int DOF, int QM = 0, int SR = 0>
 UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q,
                           const double* fq, double& ds, double& ids, const LaneQ& lq,
@@ -723,7 +776,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   const double dt = pc.dt, dt2 = dt * dt;
   // process-noise shaping from the pre-predict mean (PoseUKF.cpp:448-460)
   double qo_lane = 0.0;  // lane a*3+b (< 9) keeps (R Q_ori R^T)[a][b]
-  if (l < 9) {
+  if (LANE_IF(l, l < 9)) {
     double R[9];
     qmatrix(sm.mu + L::s_quat, R);
     const int r = l / 3, c = l % 3;
@@ -755,7 +808,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #endif
   PSP_PHASE(20);
   // sigma points: lanes < 2K plus the centre lane 2K; orientation output only
-  const bool pt = l < 2 * K, ctr = l == 2 * K;
+  const bool pt = LANE_IF(l, l < 2 * K), ctr = LANE_IF(l, l == 2 * K);
   double o[4];
   {
     double x[L::store];
@@ -850,7 +903,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     // aligned ds_read_b128)
     constexpr int DS = PSP_LDS_ALIGN ? 4 : 3, D0 = PSP_LDS_ALIGN ? 1 : 0;
     static_assert(D0 + DS * K <= PG<DOF>::STG, "Delta (PG::STG)");
-    if ((l & 1) == 0 && l < 2 * K) {
+    if (LANE_IF(l, (l & 1) == 0 && l < 2 * K)) {
 #pragma unroll
       for (int i = 0; i < 3; i++) sm.stg[D0 + (l >> 1) * DS + i] = dd[i];
     }
@@ -914,7 +967,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   // loads need no exec branch (their products are selected away)
   const int jcc = jc >= 0 ? jc : jl;
   const int Tc = (jcc * (jcc + 1)) >> 1;
-  [[maybe_unused]] const double cf = jc >= 0 ? dt : 0.0;
+  [[maybe_unused]] const double cf = LANE_IF(l, proc_couple(l < DOF ? l : DOF - 1) >= 0) ? dt : 0.0;
 #pragma unroll
   for (int q = 0; q < 6; q++) {
     const int r = pv[q], rc = proc_couple(r);
@@ -944,7 +997,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   }
 #endif
   // new time scale d' = A_ll d (A_ll = 1 on the unscaled DOFs)
-  if (l < DOF && scaled_dof(l)) {
+  if (LANE_IF(l, l < DOF && scaled_dof(l))) {
     ds = aj * ds;
 #if PSP_FAST & 32
     double rc = __builtin_amdgcn_rcp(ds);  // d in (0, 1]: two Newton steps
@@ -987,8 +1040,8 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       return;
     }
 #endif
-    if (l < DOF && !(l >= 3 && l < 6)) {
-      const bool jpv = jc >= 0;
+    if (LANE_IF(l, l < DOF && !(l >= 3 && l < 6))) {
+      const bool jpv = LANE_IF(l, proc_couple(l < DOF ? l : DOF - 1) >= 0);
       const double2* f2 = reinterpret_cast<const double2*>(fq);
 #pragma unroll
       for (int q = 0; q < ((PSP_ABL & 64) ? 0 : 6); q++)
@@ -1018,7 +1071,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     rows_lt9(std::true_type{});
   else
     rows_lt9(std::false_type{});
-  if (l < 9 && (l / 3) >= (l % 3)) {
+  if (LANE_IF(l, l < 9 && (l / 3) >= (l % 3))) {
     const int a2 = l / 3, b2 = l % 3;
     sm.S[pidx(3 + a2, 3 + b2)] = sel6(oo[0], oo[1], oo[2], oo[3], oo[4], oo[5], a2 * (a2 + 1) / 2 + b2) + dt2 * qo_lane;
   }
@@ -1052,6 +1105,13 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
         int e[3];
         bool w[3];
         double idk = ids;  // 1 / d'_{l-k}
+#undef LMG
+#define LMG 8
+        // (PSP_LMASK) the band's lane conditions per k as constant masks
+        constexpr unsigned long long bandm[3] = {
+            lane_mask([](int l) constexpr { return l >= R0 && l < DOF && l >= R0; }),
+            lane_mask([](int l) constexpr { return l >= R0 && l < DOF && l - 1 >= R0; }),
+            lane_mask([](int l) constexpr { return l >= R0 && l < DOF && l - 2 >= R0; })};
 #pragma unroll
         for (int k = 0; k < 3; k++) {
           if (k > 0) idk = dpp_d<0x138, 0xf, 0xf>(idk);  // wave_shr:1 -> lane l - k
@@ -1059,12 +1119,12 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
           e[k] = T + (j >= 0 ? (j <= lc ? j : lc) : 0);
           v[k] = sm.S[e[k]];
           double q = k == 0 ? lq.q0 : (k == 1 ? lq.q1 : lq.q2);
-          if (k == 0 && l >= L::d_wv && l < L::d_wv + 4) {
+          if (k == 0 && LANE_IF(l, l >= L::d_wv && l < L::d_wv + 4)) {
             const int iw = l - L::d_wv;
             const double qw = iw == 0 ? qw4[0] : (iw == 1 ? qw4[1] : (iw == 2 ? qw4[2] : qw4[3]));
             q = dt2 * (qw + wv_add);
           }
-          w[k] = l >= R0 && l < DOF && j >= R0 && k <= bw && q != 0.0;
+          w[k] = LANE_IN(bandm[k]) && k <= bw && q != 0.0;
           f[k] = q * (ids * idk);
         }
 #pragma unroll
@@ -1147,6 +1207,8 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     }
   }
   PSP_PHASE(25);
+#undef LMG
+#define LMG 16
   // new mean: vect parts f(mu), orientation the manifold mean
 #if PSP_BAND_PRE
   // every lane evaluates (reads past mu land in the staging area, never
@@ -1159,8 +1221,8 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   if (l < L::store && !(l >= 3 && l < 7)) mv = proc_vect_lane(l, sm.mu, pc);
 #endif
   psync();
-  if (l < L::store && !(l >= 3 && l < 7)) sm.mu[l] = mv;
-  if (l < 4) sm.mu[3 + l] = mq[l];
+  if (LANE_IF(l, l < L::store && !(l >= 3 && l < 7))) sm.mu[l] = mv;
+  if (LANE_IF(l, l < 4)) sm.mu[3 + l] = mq[l];
   psync();
   PSP_PHASE(26);
   return ok;
@@ -1396,6 +1458,8 @@ UWVK_DEV void rankm_pairs(double* S, const double* stg, int p0, int l, const dou
 // Rows >= DOF are clamped on load and never stored; in diagonal tiles only
 // column <= row is stored.  The per-entry flops and their summation order
 // differ from the FMA-chain row sweep only in rounding.
+#undef LMG
+#define LMG 32
 template <int DOF, int M>
 UWVK_DEV void rankm_mfma(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
   static_assert(M <= 3, "rank <= 3 (K = 4 with zero padding)");
@@ -1414,10 +1478,10 @@ UWVK_DEV void rankm_mfma(double* S, double* stg, const double (&Ct)[M], const do
       }
     }
     wsync();
-    const int qq = q < M ? q : 0;
+    const int qq = LANE_IF(l, ((l >> 4) & 3) < M) ? q : 0;
     const double a = stg[c * M + qq], b = stg[16 * M + c * M + qq];
-    Aop[T] = q < M ? -a : 0.0;
-    Bop[T] = q < M ? b : 0.0;
+    Aop[T] = LANE_IF(l, ((l >> 4) & 3) < M) ? -a : 0.0;
+    Bop[T] = LANE_IF(l, ((l >> 4) & 3) < M) ? b : 0.0;
     wsync();  // the next block's writes after every lane's reads
   }
 #pragma unroll
@@ -1482,11 +1546,17 @@ UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop
     else if constexpr (I == 1) asm volatile("" : "+v"(acc[0]), "+v"(acc[1]));
     else if constexpr (I == 2) asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]));
     else asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
+    // (PSP_LMASK) the diagonal tile's lower-triangle lanes per i as constant masks
+    constexpr unsigned long long diagm[4] = {
+        lane_mask([](int l) constexpr { return (l & 15) <= ((l >> 4) & 3) + 0; }),
+        lane_mask([](int l) constexpr { return (l & 15) <= ((l >> 4) & 3) + 4; }),
+        lane_mask([](int l) constexpr { return (l & 15) <= ((l >> 4) & 3) + 8; }),
+        lane_mask([](int l) constexpr { return (l & 15) <= ((l >> 4) & 3) + 12; })};
 #pragma unroll
     for (int J = 0; J <= I; J++)
 #pragma unroll
       for (int i = 0; i < 4; i++)
-        if (J < I || c <= q + 4 * i) S[base[i] + 16 * J] = acc[J][i];
+        if (J < I || LANE_IN(diagm[i])) S[base[i] + 16 * J] = acc[J][i];
     rankm_block<DOF, I + 1, NT>(S, Aop, Bop, q, c, tq);
   }
 }
@@ -1520,15 +1590,15 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
         stg[16 * M + src * M + k] = Kt[k];
       }
     }
-    if (kStripLds && T == 0 && l < O) {  // K~ of the strip columns, read back as broadcasts
+    if (kStripLds && T == 0 && LANE_IF(l, l < O)) {  // K~ of the strip columns, read back as broadcasts
 #pragma unroll
       for (int k = 0; k < M; k++) stg[32 * M + l * M + k] = Kt[k];
     }
     wsync();
-    const int qq = q < M ? q : 0;
+    const int qq = LANE_IF(l, ((l >> 4) & 3) < M) ? q : 0;
     const double a = stg[c * M + qq], b = stg[16 * M + c * M + qq];
-    Aop[T] = q < M ? -a : 0.0;
-    Bop[T] = q < M ? b : 0.0;
+    Aop[T] = LANE_IF(l, ((l >> 4) & 3) < M) ? -a : 0.0;
+    Bop[T] = LANE_IF(l, ((l >> 4) & 3) < M) ? b : 0.0;
     wsync();  // the next block's writes after every lane's reads
   }
   // strip: lane i (row i) updates columns 0 .. min(i, O - 1).  Column j's
@@ -1611,10 +1681,10 @@ UWVK_DEV void rankm_mfma_all(double* S, double* stg, const double (&Ct)[M], cons
       }
     }
     wsync();
-    const int qq = q < M ? q : 0;
+    const int qq = LANE_IF(l, ((l >> 4) & 3) < M) ? q : 0;
     const double a = stg[c * M + qq], b = stg[16 * M + c * M + qq];
-    Aop[T] = q < M ? -a : 0.0;
-    Bop[T] = q < M ? b : 0.0;
+    Aop[T] = LANE_IF(l, ((l >> 4) & 3) < M) ? -a : 0.0;
+    Bop[T] = LANE_IF(l, ((l >> 4) & 3) < M) ? b : 0.0;
     wsync();
   }
   int base[NT][4];
@@ -1681,6 +1751,8 @@ UWVK_DEV double hfma(double h, double x, double acc) {
 // ukf::update [EXT], PSP form.  gate: 0 accept any, 1 d2p95.  Returns the gate
 // decision; *ok = false on a non-positive pivot of the partial Cholesky.
 // ---------------------------------------------------------------------------
+#undef LMG
+#define LMG 64
 template <int DOF, int SR, class HM>
 UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const double (&Rm)[HM::M * HM::M], int gate,
                          const HM& hm, bool* ok, double ds, double ids, Stamper* st = nullptr) {
@@ -1698,7 +1770,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
 #endif
   }
   PSP_PHASE(30);
-  [[maybe_unused]] const bool pt = l < 2 * K;  // the non-lds_sums path (PSP_FAST & 256 off)
+  [[maybe_unused]] const bool pt = LANE_IF(l, l < 2 * K);  // the non-lds_sums path (PSP_FAST & 256 off)
   double zp[M];
   {
     double x[L::store];
@@ -1725,7 +1797,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   }
   double Pl = 0.0;
   if constexpr (K > 0) {
-    const int q = l < M * K ? l : 0;
+    const int q = LANE_IF(l, l < M * K) ? l : 0;
     const int i = q / K, j = q - (q / K) * K;
 #pragma unroll
     for (int t = 0; t < NC; t++) {
@@ -1810,7 +1882,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   }
   double Pl = 0.0;
   if constexpr (K > 0) {
-    const int q = l < M * K ? l : 0;
+    const int q = LANE_IF(l, l < M * K) ? l : 0;
     const int i = q / K, j = q - (q / K) * K;
 #pragma unroll
     for (int t = 0; t < NC; t++) {
@@ -1849,8 +1921,8 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     // pair is one aligned ds_read_b128)
     constexpr int PS = (PSP_LDS_ALIGN && M == 3) ? 4 : M, P0 = (PSP_LDS_ALIGN && M >= 2) ? 1 : 0;
     static_assert(P0 + 2 * PS * K <= PG<DOF>::STG, "P and Dz (PG::STG)");
-    if (l < M * K) sm.stg[P0 + (l % K) * PS + l / K] = Pl;  // j-major: P[i][j] at j PS + i
-    if ((l & 1) == 0 && l < 2 * K) {
+    if (LANE_IF(l, l < M * K)) sm.stg[P0 + (l % K) * PS + l / K] = Pl;  // j-major: P[i][j] at j PS + i
+    if (LANE_IF(l, (l & 1) == 0 && l < 2 * K)) {
 #pragma unroll
       for (int i = 0; i < M; i++) sm.stg[P0 + PS * K + (l >> 1) * PS + i] = zd[i];
     }
@@ -2034,6 +2106,8 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     asm volatile("" ::"v"(dl));
     return true;
   }
+#undef LMG
+#define LMG 128
   // apply_delta, exact form: mu <- mu [+] delta, Sigma <- T Sigma T^T with T
   // the identity except on the orientation block.  ukfom re-spreads X_p =
   // mu [+] +-L_j, shifts every point by delta and takes the deviations from
@@ -2082,7 +2156,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       double n3[3];
 #pragma unroll
       for (int i = 0; i < 3; i++) n3[i] = R[i * 3] * s0 + R[i * 3 + 1] * s1 + R[i * 3 + 2] * s2;
-      if (l < DOF && !(l >= 3 && l < 6)) {
+      if (LANE_IF(l, l < DOF && !(l >= 3 && l < 6))) {
         sm.S[e0] = n3[0];
         sm.S[e1] = n3[1];
         sm.S[e2] = n3[2];
@@ -2120,7 +2194,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     // storage s = l takes tangent delta_{l} (l < 3) or delta_{l-1} (l >= 7): DPP wave_shr:1
     const double dsh = dpp_d<0x138, 0xf, 0xf>(dl);
 #if PSP_BAND_PRE
-    double mnew = sm.mu[l & 63] + 1.0 * (l < 3 ? dl : dsh);  // stored for the vector lanes only
+    double mnew = sm.mu[l & 63] + 1.0 * (LANE_IF(l, l < 3) ? dl : dsh);  // stored for the vector lanes only
     asm volatile("" : "+v"(mnew));
 #else
     double mnew = 0.0;
@@ -2129,9 +2203,9 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     double qn[4];
     qplus_psp<SR>(eq, sm.mu + L::s_quat, qn);
     psync();
-    if (l < 9 && (l / 3) >= (l % 3)) sm.S[pidx(3 + l / 3, 3 + l % 3)] = nb;
-    if (l < L::store && !(l >= 3 && l < 7)) sm.mu[l] = mnew;
-    if (l < 4) sm.mu[3 + l] = qn[l];
+    if (LANE_IF(l, l < 9 && (l / 3) >= (l % 3))) sm.S[pidx(3 + l / 3, 3 + l % 3)] = nb;
+    if (LANE_IF(l, l < L::store && !(l >= 3 && l < 7))) sm.mu[l] = mnew;
+    if (LANE_IF(l, l < 4)) sm.mu[3 + l] = qn[l];
     psync();
   }
   PSP_PHASE(35);
