@@ -180,6 +180,36 @@ UWVK_DEV bool lane_const() {
   ((PSP_LMASK & LMG) ? (::uwvk::psp::mask_needs_split(m) ? ::uwvk::psp::lane_in_split(m)                     \
                                                          : __builtin_amdgcn_inverse_ballot_w64(m))             \
                      : ((((m) >> (olane() & 63)) & 1ull) != 0))
+// lanes whose column j >= p, with j the lane clamped to the last DOF (jl) or its
+// A-coupled column (jcc: pos -> vel, vel -> acc, else jl), for pidx_sel_b
+UWVK_DEV constexpr int couple_c(int d) { return d < 3 ? d + 6 : (d >= 6 && d < 9 ? d + 3 : -1); }
+template <int DOF>
+UWVK_DEV constexpr unsigned long long col_ge_mask(int p, bool coupled) {
+  unsigned long long m = 0;
+  for (int l = 0; l < 64; l++) {
+    const int jl = l < DOF ? l : DOF - 1, jc = couple_c(jl);
+    const int j = coupled ? (jc >= 0 ? jc : jl) : jl;
+    if (j >= p) m |= 1ull << l;
+  }
+  return m;
+}
+// rows_lt9: lanes storing entry (p, l): uncoupled lanes, or coupled ones at l <= p
+template <int DOF>
+UWVK_DEV constexpr unsigned long long rows_store_mask(int p) {
+  unsigned long long m = 0;
+  for (int l = 0; l < 64; l++) {
+    const int jl = l < DOF ? l : DOF - 1;
+    if (!(couple_c(jl) >= 0) || l <= p) m |= 1ull << l;
+  }
+  return m;
+}
+// lanes of a compile-time row list
+template <class RL>
+UWVK_DEV constexpr unsigned long long rows_mask() {
+  unsigned long long m = 0;
+  for (int k = 0; k < RL::NR; k++) m |= 1ull << RL::rows[k];
+  return m;
+}
 
 // ---------------------------------------------------------------------------
 // DPP wave reductions (no LDS crossbar): row_shr 1/2/3 -> 4-lane sums,
@@ -313,6 +343,8 @@ UWVK_DEV double sel6(double v0, double v1, double v2, double v3, double v4, doub
 
 // pidx(p, j) for a compile-time p and lane-varying j, given Tj = j (j + 1) / 2
 UWVK_DEV int pidx_sel(int p, int j, int Tj) { return j >= p ? Tj + p : p * (p + 1) / 2 + j; }
+// the same with the branch given (a lane mask, PSP_LMASK)
+UWVK_DEV int pidx_sel_b(int p, int j, int Tj, bool ge) { return ge ? Tj + p : p * (p + 1) / 2 + j; }
 
 UWVK_DEV void wsync() {  // LDS ordering point between the lanes of one wave
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -523,7 +555,7 @@ UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* s
   bool ok = true;
   int q = -1;
 #pragma unroll
-  for (int k = 0; k < RL::NR; k++) q = (r == RL::rows[k]) ? k : q;
+  for (int k = 0; k < RL::NR; k++) q = LANE_IN(1ull << RL::rows[k]) ? k : q;
   static_assert(RL::NR >= 1 && STG_ROWS + RL::NR * K <= 115, "staging area (PG::STG)");
   const double p0 = readlane_d(a[0], 0);
   const double inv0 = rsqrt_f64(p0);
@@ -533,7 +565,7 @@ UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* s
   // staged after the last step, one lane-addressed run of K stores per row
   // lane, instead of one masked store (and its address product) per step
   pchol_step_lds<K, 0>(a, r, ok, stg + STG_ROWS, stg + STG_ROWS, q, p0, inv0, chk);
-  if (q >= 0) {
+  if (LANE_IN(rows_mask<RL>())) {  // q >= 0
     double* rp = stg + STG_ROWS + q * K;
 #pragma unroll
     for (int J = 0; J < K; J++) rp[J] = a[J];
@@ -942,7 +974,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #pragma unroll
     for (int i = 0; i < 3; i++) {
       const double yc = shfl_d(Y[i], src);
-      X[i] = 0.5 * (cp >= 0 ? (ar * Y[i] + dt * yc) : ar * Y[i]);
+      X[i] = 0.5 * (LANE_IF(l, proc_couple(l) >= 0) ? (ar * Y[i] + dt * yc) : ar * Y[i]);
     }
   }
   PSP_PHASE(23);
@@ -968,6 +1000,20 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   const int jcc = jc >= 0 ? jc : jl;
   const int Tc = (jcc * (jcc + 1)) >> 1;
   [[maybe_unused]] const double cf = LANE_IF(l, proc_couple(l < DOF ? l : DOF - 1) >= 0) ? dt : 0.0;
+  // (PSP_LMASK) pidx_sel's branch per row as lane masks: rows pv[q] and
+  // proc_couple(pv[q]), against the lane column jl and the coupled one jcc
+  constexpr unsigned long long ml_r[6] = {col_ge_mask<DOF>(0, false), col_ge_mask<DOF>(1, false),
+                                          col_ge_mask<DOF>(2, false), col_ge_mask<DOF>(6, false),
+                                          col_ge_mask<DOF>(7, false), col_ge_mask<DOF>(8, false)};
+  constexpr unsigned long long ml_rc[6] = {col_ge_mask<DOF>(6, false), col_ge_mask<DOF>(7, false),
+                                           col_ge_mask<DOF>(8, false), col_ge_mask<DOF>(9, false),
+                                           col_ge_mask<DOF>(10, false), col_ge_mask<DOF>(11, false)};
+  constexpr unsigned long long mc_r[6] = {col_ge_mask<DOF>(0, true), col_ge_mask<DOF>(1, true),
+                                          col_ge_mask<DOF>(2, true), col_ge_mask<DOF>(6, true),
+                                          col_ge_mask<DOF>(7, true), col_ge_mask<DOF>(8, true)};
+  constexpr unsigned long long mc_rc[6] = {col_ge_mask<DOF>(6, true), col_ge_mask<DOF>(7, true),
+                                           col_ge_mask<DOF>(8, true), col_ge_mask<DOF>(9, true),
+                                           col_ge_mask<DOF>(10, true), col_ge_mask<DOF>(11, true)};
 #pragma unroll
   for (int q = 0; q < 6; q++) {
     const int r = pv[q], rc = proc_couple(r);
@@ -979,8 +1025,10 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     // (r04) the coupled column's term as an FMA with cf = dt (coupled lanes) or
     // 0: the conditional form was compiled to 12 exec-masked branches, each
     // waiting for its own LDS load (lgkmcnt(0)); S~ is finite, so cf = 0 adds 0
-    const double t0 = fma(cf, sm.S[pidx_sel(r, jcc, Tc)], aj * (ds * sm.S[pidx_sel(r, jl, Tl)]));
-    const double t1 = fma(cf, sm.S[pidx_sel(rc, jcc, Tc)], aj * (ds * sm.S[pidx_sel(rc, jl, Tl)]));
+    const double t0 = fma(cf, sm.S[pidx_sel_b(r, jcc, Tc, LANE_IN(mc_r[q]))],
+                          aj * (ds * sm.S[pidx_sel_b(r, jl, Tl, LANE_IN(ml_r[q]))]));
+    const double t1 = fma(cf, sm.S[pidx_sel_b(rc, jcc, Tc, LANE_IN(mc_rc[q]))],
+                          aj * (ds * sm.S[pidx_sel_b(rc, jl, Tl, LANE_IN(ml_rc[q]))]));
 #else
     const double t0 = aj * (ds * sm.S[pidx_sel(r, jl, Tl)]) + (jc >= 0 ? dt * sm.S[pidx_sel(r, jcc, Tc)] : 0.0);
     const double t1 = aj * (ds * sm.S[pidx_sel(rc, jl, Tl)]) + (jc >= 0 ? dt * sm.S[pidx_sel(rc, jcc, Tc)] : 0.0);
@@ -1043,10 +1091,16 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     if (LANE_IF(l, l < DOF && !(l >= 3 && l < 6))) {
       const bool jpv = LANE_IF(l, proc_couple(l < DOF ? l : DOF - 1) >= 0);
       const double2* f2 = reinterpret_cast<const double2*>(fq);
+      constexpr unsigned long long smask[6] = {rows_store_mask<DOF>(0), rows_store_mask<DOF>(1),
+                                               rows_store_mask<DOF>(2), rows_store_mask<DOF>(6),
+                                               rows_store_mask<DOF>(7), rows_store_mask<DOF>(8)};
+      constexpr unsigned long long gmask[6] = {col_ge_mask<DOF>(0, false), col_ge_mask<DOF>(1, false),
+                                               col_ge_mask<DOF>(2, false), col_ge_mask<DOF>(6, false),
+                                               col_ge_mask<DOF>(7, false), col_ge_mask<DOF>(8, false)};
 #pragma unroll
       for (int q = 0; q < ((PSP_ABL & 64) ? 0 : 6); q++)
-        if (!jpv || l <= pv[q]) {
-          const int e = PSP_PIDX_SEL ? pidx_sel(pv[q], l, Tl) : pidx(pv[q], l);  // l < DOF: jl == l
+        if (LANE_IN(smask[q])) {  // !jpv || l <= pv[q]
+          const int e = PSP_PIDX_SEL ? pidx_sel_b(pv[q], l, Tl, LANE_IN(gmask[q])) : pidx(pv[q], l);  // l < DOF: jl == l
           double qq;
           if constexpr (kQS) qq = (PSP_QDIAG || l != pv[q]) ? 0.0 : lq.q0;
           else qq = f2[e].y;
@@ -1061,7 +1115,9 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #endif
 #pragma unroll
       for (int i = 0; i < 3; i++) {
-        const int e = PSP_PIDX_SEL ? pidx_sel(3 + i, l, Tl) : pidx(3 + i, l);
+        constexpr unsigned long long omask[3] = {col_ge_mask<DOF>(3, false), col_ge_mask<DOF>(4, false),
+                                                 col_ge_mask<DOF>(5, false)};
+        const int e = PSP_PIDX_SEL ? pidx_sel_b(3 + i, l, Tl, LANE_IN(omask[i])) : pidx(3 + i, l);
         if constexpr (kQS) sm.S[e] = X[i] * ids;
         else sm.S[e] = (X[i] + f2[e].y) * ids;
       }
@@ -2135,7 +2191,9 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     {
       const int lc = l < DOF ? l : DOF - 1;
       const int Tl = (lc * (lc + 1)) >> 1;
-      const int e0 = pidx_sel(3, lc, Tl), e1 = pidx_sel(4, lc, Tl), e2 = pidx_sel(5, lc, Tl);
+      const int e0 = pidx_sel_b(3, lc, Tl, LANE_IN(col_ge_mask<DOF>(3, false))),
+                e1 = pidx_sel_b(4, lc, Tl, LANE_IN(col_ge_mask<DOF>(4, false))),
+                e2 = pidx_sel_b(5, lc, Tl, LANE_IN(col_ge_mask<DOF>(5, false)));
       double s0 = sm.S[e0], s1 = sm.S[e1], s2 = sm.S[e2];
       asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2));  // loaded here, not sunk into the store branch
       double B[9];
