@@ -68,3 +68,47 @@ def test_psp_epoch_kernels_keep_three_waves_per_simd(src, side):
         assert name.endswith("ELi%dEEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % side), name
         # VGPRs and AGPRs share one 512-entry file per SIMD lane: 3 waves need <= 168 together
         assert r["vgpr"] + r.get("agpr", 0) <= 168 and r["scratch"] == 0 and r["occupancy"] >= 3, (name, r)
+
+
+# A 64-bit scalar operand written as a 32-bit literal: gfx950 zero-extends it,
+# so a value that is a sign-extended 32-bit number (0xffffffff8xxxxxxx ..
+# 0xffffffffffffffef, not an inline constant) comes out with the upper half
+# clear.  The compiler emitted exactly that for lane masks such as lanes >= 5
+# (s_mov_b64 sX, 0xffffffffffffffe0; tools/probe_lmask.hip),
+# so the PSP lane masks build those values from two 32-bit halves.  This scan
+# keeps such an instruction out of the shipped ISA.
+LIT64 = re.compile(r"^\s*(s_\w+_[biu]64)\s+(.*)$")
+
+
+def sext32_literals(asm_text):
+    bad = []
+    for line in asm_text.splitlines():
+        m = LIT64.match(line)
+        if not m:
+            continue
+        for op in (x.strip() for x in m.group(2).split(",")):
+            if not re.fullmatch(r"0x[0-9a-f]+|-?\d+", op):
+                continue
+            v = int(op, 16) if op.startswith("0x") else int(op)
+            v &= (1 << 64) - 1
+            inline = v <= 64 or v >= (1 << 64) - 16
+            if not inline and v >= 0xFFFFFFFF80000000:
+                bad.append(line.strip())
+    return bad
+
+
+def test_sext32_literal_scan_catches_the_hazard():
+    assert sext32_literals("  s_mov_b64 s[4:5], 0xffffffffffffffe0\n")
+    assert not sext32_literals("  s_mov_b64 s[4:5], -2\n  s_mov_b64 vcc, 0x3fffffff\n  s_movk_i32 s2, 0xffe0\n")
+
+
+@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
+@pytest.mark.parametrize("src", ["csrc/uwvk_psp_k.hip", "csrc/uwvk_psp_k_r.hip"])
+def test_psp_isa_has_no_zero_extended_64bit_literal(src, tmp_path):
+    out = str(tmp_path / "psp.s")
+    cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
+           *psp_flags(), "-S", src, "-o", out]
+    r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    bad = sext32_literals(open(out).read())
+    assert not bad, bad[:10]
