@@ -520,6 +520,9 @@ UWVK_DEV double row_bcast(double v, int src) {
   return __hiloint2double(hi, lo);
 }
 
+#ifndef VEL_PT_SEL
+#define VEL_PT_SEL 1
+#endif
 // sigma point g of (mu, L) [EXT ukfom]: 0 = mu, 2j+1 = mu + L_j, 2j+2 = mu - L_j
 UWVK_DEV void vg_point(const double mu[4], const double L[16], int g, double x[4]) {
   const int j = g >= 1 && g < 9 ? (g - 1) >> 1 : 0;
@@ -528,7 +531,12 @@ UWVK_DEV void vg_point(const double mu[4], const double L[16], int g, double x[4
   for (int k = 0; k < 4; k++) {
     double c = L[k * 4];
 #pragma unroll
-    for (int jj = 1; jj < 4; jj++) c = (j == jj) ? L[k * 4 + jj] : c;
+    for (int jj = 1; jj < 4; jj++) {
+      c = (j == jj) ? L[k * 4 + jj] : c;
+#if VEL_PT_SEL
+      asm volatile("" : "+v"(c));  // keep the selects: as one lane-indexed L[k][j] the compiler put L in scratch
+#endif
+    }
     x[k] = sg == 0.0 ? mu[k] : mu[k] + sg * c;
   }
 }

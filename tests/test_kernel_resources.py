@@ -29,11 +29,12 @@ def psp_flags():
     raise AssertionError("PSP_FLAGS not found in the Makefile")
 
 
-def kernel_usage(src, mangled_prefixes, extra=()):
+def kernel_usage(src, mangled_prefixes, extra=(), flags=None):
     """{mangled name: {vgpr, agpr, scratch, occupancy}} for every kernel whose
-    mangled name starts with one of mangled_prefixes."""
+    mangled name starts with one of mangled_prefixes (flags: the unit's extra
+    Makefile flags, PSP_FLAGS by default)."""
     cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-           *psp_flags(), *extra, "-c", src, "-o", os.devnull,
+           *(psp_flags() if flags is None else flags), *extra, "-c", src, "-o", os.devnull,
            "-Rpass-analysis=kernel-resource-usage"]
     r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -68,6 +69,20 @@ def test_psp_epoch_kernels_keep_three_waves_per_simd(src, side):
         assert name.endswith("ELi%dEEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % side), name
         # VGPRs and AGPRs share one 512-entry file per SIMD lane: 3 waves need <= 168 together
         assert r["vgpr"] + r.get("agpr", 0) <= 168 and r["scratch"] == 0 and r["occupancy"] >= 3, (name, r)
+
+
+# The VelocityUKF kernels: no scratch.  k_vel_epoch_g (C2) had 272 B/lane until
+# r04: vg_point's select chain over L[k][0..3] by the lane's column was turned
+# into one lane-indexed load from a private copy of L, i.e. L stored to scratch
+# and reloaded in every predict and update (VEL_PT_SEL keeps the selects;
+# C2 633-635 -> 741-745 M steps/s, profiles/r04/vpt/).
+@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
+def test_velocity_kernels_have_no_scratch():
+    u = kernel_usage("csrc/uwvk_vel.hip", ("_ZN12_GLOBAL__N_1", "_ZN4uwvk"), flags=[])
+    names = [n for n in u if "k_vel_" in n]
+    assert any("k_vel_epoch_g" in n for n in names) and len(names) >= 6, sorted(u)
+    for n in names:
+        assert u[n]["scratch"] == 0, (n, u[n])
 
 
 # A 64-bit scalar operand written as a 32-bit literal: gfx950 zero-extends it,
