@@ -17,10 +17,12 @@ timeout -k 10 240 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/sm
 tail -2 "$OUT/smoke.txt"
 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > "$OUT/bench_c3.json" 2> "$OUT/bench_c3.err" || { tail -5 "$OUT/bench_c3.err"; exit 1; }
 tail -c 400 "$OUT/bench_c3.json"; echo
-bash tools/pmc_r03.sh "$TAG" 20 || exit 1
-bash tools/pmc_r03.sh "$TAG" 200 || exit 1
-bash tools/pmc_lds.sh "$TAG" 20 || exit 1
-bash tools/pmc_lds.sh "$TAG" 200 || exit 1
+if [ -z "${SKIP_PMC:-}" ]; then  # SKIP_PMC=1: the PSP kernel unchanged since the last counter passes
+  bash tools/pmc_r03.sh "$TAG" 20 || exit 1
+  bash tools/pmc_r03.sh "$TAG" 200 || exit 1
+  bash tools/pmc_lds.sh "$TAG" 20 || exit 1
+  bash tools/pmc_lds.sh "$TAG" 200 || exit 1
+fi
 timeout -k 10 300 python3 bench.py --mode C4 --steps 2000 --warmup 5 --no-cpu-baseline > "$OUT/c4.json" 2> "$OUT/c4.err" || { tail -5 "$OUT/c4.err"; exit 1; }
 timeout -k 10 300 python3 bench.py --mode C5 --steps 200 --warmup 5 --no-cpu-baseline > "$OUT/c5shard.json" 2> "$OUT/c5shard.err" || { tail -5 "$OUT/c5shard.err"; exit 1; }
 timeout -k 10 300 python3 bench.py --mode C2 --steps 2000 --warmup 5 > "$OUT/c2.json" 2> "$OUT/c2.err" || { tail -5 "$OUT/c2.err"; exit 1; }
