@@ -498,10 +498,22 @@ __global__ __launch_bounds__(64) void k_vel_epoch(VelBufs b, VelShared P0, VelEp
 // lane.  4 filters per wave: batch 4096 fills 1024 waves, one per SIMD,
 // where the lane-per-filter kernel occupies 64.
 // ---------------------------------------------------------------------------
+#ifndef VEL_DPP_NOOLD
+#define VEL_DPP_NOOLD 1
+#endif
+// (r04, VEL_DPP_NOOLD) every lane has a source lane under the controls used here
+// (quad_perm, row_half_mirror, row_mirror, all rows and banks), so the old value
+// is never read: mov_dpp leaves it undefined, where update_dpp's explicit 0 cost
+// a v_mov_b32 before every DPP move (~490 per wave-epoch pass of the C2 kernel)
 template <int CTRL>
 UWVK_DEV double vdpp(double v) {
+#if VEL_DPP_NOOLD
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
+#else
   const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
   const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+#endif
   return __hiloint2double(hi, lo);
 }
 // sum over the 16 lanes of this lane's DPP row, identical in every lane
