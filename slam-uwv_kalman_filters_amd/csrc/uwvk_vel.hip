@@ -679,6 +679,13 @@ UWVK_DEV bool vg_update(double mu[4], double S[16], const double z[M], const dou
 
 constexpr int VG = 16;  // lanes per filter
 
+#ifndef VEL_NOHOIST
+// (r04) loop-invariant scalar data (Q0, the DVL covariance) loaded where it is
+// used: hoisted out of the epoch loop it held 50 SGPRs, which the register
+// allocator spilled to VGPR lanes and restored with v_readlane every epoch
+#define VEL_NOHOIST 1
+#endif
+
 #ifndef VEL_LDS
 #define VEL_LDS 0  // r04 A/B: 474.5 against 546.8 M steps/s on C2 (profiles/r04/c2ab/), not kept
 #endif
@@ -767,8 +774,16 @@ __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, Vel
     }
     vg_mean<4>(x, pt, mu);
     vg_cov(x, mu, pt, S);
+#if VEL_NOHOIST
+    {  // Q0 by scalar loads here, not hoisted out of the loop into 32 SGPRs held across it
+      const auto& PQ = vlaunder(P);
+#pragma unroll
+      for (int k = 0; k < 16; k++) S[k] += ea.dt * PQ.Q0[k];
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 16; k++) S[k] += ea.dt * P.Q0[k];
+#endif
     if (side) {
 #pragma unroll
       for (int k = 0; k < 13; k++) m[k] = n13[k];
@@ -781,7 +796,13 @@ __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, Vel
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + i) * 3;
       const double zz[3] = {z[0], z[1], z[2]};
+#if VEL_NOHOIST
+      const double* Rd = ea.dvl_cov;
+      asm volatile("" : "+s"(Rd));  // R loaded in the branch, not held in SGPRs across the loop
+      ok = vg_update<3, 0>(mu, S, zz, Rd, g) && ok;
+#else
       ok = vg_update<3, 0>(mu, S, zz, ea.dvl_cov, g) && ok;
+#endif
     }
     if (fl & UWVK_EV_PRESSURE) {
       const double zz[1] = {ea.pressure[(int64_t)ea.p_index[e] * B + i]};
