@@ -21,6 +21,7 @@ struct VelShared {  // batch-shared model parameters (by value)
   double M[36], Dl[36], Dq[36], Minv[36];
   double weight, buoyancy, cog[3], cob[3];
   double Q0[16];  // process_noise_cov (VelocityUKF.cpp:54-55)
+  double gk, gm[3];  // weight - buoyancy, weight cog - buoyancy cob (VEL_GLIN)
 };
 
 struct VelBufs {
@@ -72,6 +73,9 @@ UWVK_DEV GVS& vlaunder(GVS& p) {
 }
 
 // ---- [EXT] ModelSimulation: M nu_dot + C(nu) nu + D(nu) nu + g(q) = tau, RK4 --
+#ifndef VEL_GLIN
+#define VEL_GLIN 1
+#endif
 template <class PS>
 UWVK_DEV void v_coriolis(const PS& P, const double nu[6], double c[6]) {
   double a[3], b[3], t0[3], t1[3], t2[3];
@@ -115,6 +119,21 @@ UWVK_DEV void v_deriv(const PS& P, const double tau[6], const double s[13], doub
     }
     d[i] = sl + sq;
   }
+#if VEL_GLIN
+  // (r04) the restoring forces through one rotation: qrot_inv is linear in its
+  // vector and both forces lie along the nav z axis, so with r = R^T e_z
+  //   -(fg + fb) = (W - B) r,   -(cog x fg + cob x fb) = (W cog - B cob) x r
+  // (the same quantities, one rotation and one cross product instead of two)
+  {
+    const double ez[3] = {0, 0, 1};
+    double r[3], m3[3];
+    qrot_inv(q, ez, r);
+    const double gm[3] = {P.gm[0], P.gm[1], P.gm[2]};
+    cross3(gm, r, m3);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { g[i] = P.gk * r[i]; g[3 + i] = m3[i]; }
+  }
+#else
   const double fw[3] = {0, 0, -P.weight}, fb[3] = {0, 0, P.buoyancy};
   const double cog[3] = {P.cog[0], P.cog[1], P.cog[2]}, cob[3] = {P.cob[0], P.cob[1], P.cob[2]};
   double fg[3], fbb[3], mg[3], mb[3];
@@ -124,6 +143,7 @@ UWVK_DEV void v_deriv(const PS& P, const double tau[6], const double s[13], doub
   cross3(cob, fbb, mb);
 #pragma unroll
   for (int i = 0; i < 3; i++) { g[i] = -(fg[i] + fbb[i]); g[3 + i] = -(mg[i] + mb[i]); }
+#endif
 #pragma unroll
   for (int i = 0; i < 6; i++) r[i] = tau[i] - c[i] - d[i] - g[i];
 #pragma unroll
@@ -1005,6 +1025,9 @@ uwvk_status uwvk_vel_setup_motion_model(uwvk_vel* h, const uwvk_uwv_params* u) {
     h->P.cog[k] = u->distance_body2centerofgravity[k];
     h->P.cob[k] = u->distance_body2centerofbuoyancy[k];
   }
+  h->P.gk = u->weight - u->buoyancy;
+  for (int k = 0; k < 3; k++)
+    h->P.gm[k] = u->weight * u->distance_body2centerofgravity[k] - u->buoyancy * u->distance_body2centerofbuoyancy[k];
   HIPCHK(hipStreamSynchronize(h->stream));  // a running kernel may read the previous copy
   HIPCHK(hipMemcpyAsync(h->d_shared, &h->P, sizeof(VelShared), hipMemcpyHostToDevice, h->stream));
   hipLaunchKernelGGL(k_vel_setup, dim3(vgrid(h->batch)), dim3(64), 0, h->stream, vbufs(h));

@@ -184,8 +184,9 @@ def test_velocity_ukf_model_change_between_runs(eng, orc, groups):
     device copy (VEL_SMEM): setupMotionModel (VelocityUKF.cpp:65-74) and
     setProcessNoiseCovariance between two run_log calls must reach the second
     run.  The second model has off-diagonal inertia / damping couplings (every
-    entry of the 6x6 matrices is used), and the single-call predict after it
-    goes through k_vel_predict."""
+    entry of the 6x6 matrices is used) and unequal weight / buoyancy with
+    general centres, and the single-call predict after it goes through
+    k_vel_predict."""
     from uwvk import abi, synth
     B = 12
     log = synth.make_vel_log(B, 400)
@@ -198,6 +199,12 @@ def test_velocity_ukf_model_change_between_runs(eng, orc, groups):
     abi.fill(uwv2.inertia_matrix, (M * 1.3 + C).ravel())
     abi.fill(uwv2.damping_matrices[0], (Dl * 0.7 + 0.5 * C).ravel())
     abi.fill(uwv2.damping_matrices[1], (Dq * 1.5 + 0.25 * np.abs(C)).ravel())
+    # unequal weight / buoyancy and general centres (the default model has
+    # W = B and cog = 0): every term of the restoring forces, which the kernels
+    # evaluate through one rotation (VEL_GLIN, uwvk_vel.hip v_deriv)
+    uwv2.weight, uwv2.buoyancy = 2100.0, 1950.0
+    abi.fill(uwv2.distance_body2centerofgravity, [0.02, -0.01, 0.03])
+    abi.fill(uwv2.distance_body2centerofbuoyancy, [0.01, 0.015, 0.06])
     Q2 = np.diag([3e-2, 2e-2, 1e-2, 4e-3])
     o, g = orc.OracleVelBatch(B), eng.VelocityUKFBatch(B)
     g.set_lane_groups(groups)
