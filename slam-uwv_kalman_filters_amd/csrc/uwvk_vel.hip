@@ -76,6 +76,29 @@ UWVK_DEV GVS& vlaunder(GVS& p) {
 #ifndef VEL_GLIN
 #define VEL_GLIN 1
 #endif
+// (r04) VEL_FASTDIV: fp64 sqrt and division are ~10-15 VALU sequences each on
+// gfx950; the Cholesky, the quaternion normalisation and the means' 1/N use
+// 1/sqrt (hardware seed + one Halley step, < 1 ulp) and products instead, the
+// means' x / N as x (1/N) with one FMA correction (correctly rounded quotient).
+// Rounding-level differences from the literal forms, inside the tolerances.
+#ifndef VEL_FASTDIV
+#define VEL_FASTDIV 1
+#endif
+UWVK_DEV double v_rsqrt(double x) {
+  const double r = __builtin_amdgcn_rsq(x);
+  const double e = fma(-(x * r), r, 1.0);
+  return fma(r * e, fma(0.375, e, 0.5), r);
+}
+template <int N>
+UWVK_DEV double v_divn(double x) {
+#if VEL_FASTDIV
+  constexpr double y = 1.0 / N;
+  const double q = x * y;
+  return fma(fma(-q, (double)N, x), y, q);
+#else
+  return x / (double)N;
+#endif
+}
 template <class PS>
 UWVK_DEV void v_coriolis(const PS& P, const double nu[6], double c[6]) {
   double a[3], b[3], t0[3], t1[3], t2[3];
@@ -181,14 +204,21 @@ UWVK_DEV void v_rk4(const PS& P, const double tau[6], double dt, const double s[
   v_deriv(vlaunder(P), tau, t, k);
 #pragma unroll
   for (int i = 0; i < 13; i++) o[i] = s[i] + (dt / 6.0) * (acc[i] + k[i]);
+#if VEL_FASTDIV
+  const double in = v_rsqrt(o[3] * o[3] + o[4] * o[4] + o[5] * o[5] + o[6] * o[6]);
+#pragma unroll
+  for (int i = 3; i < 7; i++) o[i] *= in;
+#else
   const double n = sqrt(o[3] * o[3] + o[4] * o[4] + o[5] * o[5] + o[6] * o[6]);
 #pragma unroll
   for (int i = 3; i < 7; i++) o[i] /= n;
+#endif
 }
 
 // ---- 4-DOF vector-manifold UKF core in registers [EXT ukfom] -----------------
 UWVK_DEV bool v_chol(const double A[16], double L[16]) {
   bool ok = true;
+  double inv[4];
 #pragma unroll
   for (int i = 0; i < 16; i++) L[i] = 0.0;
 #pragma unroll
@@ -198,12 +228,22 @@ UWVK_DEV bool v_chol(const double A[16], double L[16]) {
       double s = A[i * 4 + j];
 #pragma unroll
       for (int k = 0; k < j; k++) s -= L[i * 4 + k] * L[j * 4 + k];
+#if VEL_FASTDIV
+      if (i == j) {
+        ok = ok && (s > 0.0);
+        inv[i] = v_rsqrt(s);
+        L[i * 4 + i] = s * inv[i];
+      } else {
+        L[i * 4 + j] = s * inv[j];
+      }
+#else
       if (i == j) {
         ok = ok && (s > 0.0);
         L[i * 4 + i] = sqrt(s);
       } else {
         L[i * 4 + j] = s / L[j * 4 + j];
       }
+#endif
     }
   }
   return ok;
@@ -239,13 +279,17 @@ UWVK_DEV void v_mean(const double (&X)[N][M], double ref[M]) {
     nrm = 0.0;
 #pragma unroll
     for (int k = 0; k < M; k++) {
-      d[k] /= (double)N;
+      d[k] = v_divn<N>(d[k]);
       nrm += d[k] * d[k];
     }
 #pragma unroll
     for (int k = 0; k < M; k++) ref[k] = ref[k] + 1.0 * d[k];
+#if VEL_FASTDIV
+  } while (nrm > 1e-12 && ++it < 10000);  // |delta|^2 against (1e-6)^2: no sqrt
+#else
     nrm = sqrt(nrm);
   } while (nrm > 1e-6 && ++it < 10000);
+#endif
 }
 
 UWVK_DEV void v_cov(const double (&X)[9][4], const double mean[4], double S[16]) {
@@ -585,13 +629,17 @@ UWVK_DEV void vg_mean(const double x[M], bool pt, double ref[M]) {
     nrm = 0.0;
 #pragma unroll
     for (int k = 0; k < M; k++) {
-      d[k] = row_sum16(pt ? x[k] - ref[k] : 0.0) / 9.0;
+      d[k] = v_divn<9>(row_sum16(pt ? x[k] - ref[k] : 0.0));
       nrm += d[k] * d[k];
     }
 #pragma unroll
     for (int k = 0; k < M; k++) ref[k] = ref[k] + 1.0 * d[k];
+#if VEL_FASTDIV
+  } while (nrm > 1e-12 && ++it < 10000);
+#else
     nrm = sqrt(nrm);
   } while (nrm > 1e-6 && ++it < 10000);
+#endif
 }
 
 // Sigma = 1/2 sum_p d_p d_p^T over the point lanes (+ add)
