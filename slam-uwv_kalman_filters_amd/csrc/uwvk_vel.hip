@@ -81,6 +81,9 @@ UWVK_DEV GVS& vlaunder(GVS& p) {
 // 1/sqrt (hardware seed + one Halley step, < 1 ulp) and products instead, the
 // means' x / N as x (1/N) with one FMA correction (correctly rounded quotient).
 // Rounding-level differences from the literal forms, inside the tolerances.
+#ifndef VEL_LAUNDER_MAT
+#define VEL_LAUNDER_MAT 0  // r04 A/B: 892.7-897.6 against 878.0-892.6 M steps/s (profiles/r04/lm/), a tie, not kept
+#endif
 #ifndef VEL_FASTDIV
 #define VEL_FASTDIV 1
 #endif
@@ -132,13 +135,20 @@ UWVK_DEV void v_deriv(const PS& P, const double tau[6], const double s[13], doub
   for (int i = 0; i < 4; i++) ds[3 + i] = 0.5 * qd[i];
   double c[6], d[6], g[6], r[6];
   v_coriolis(P, nu, c);
+#if VEL_LAUNDER_MAT
+  // (r04) each matrix's scalar loads after its own launder point: fewer
+  // matrices live in SGPRs at once (spilled to VGPR lanes otherwise)
+  const auto& PD = vlaunder(P);
+#else
+  const auto& PD = P;
+#endif
 #pragma unroll
   for (int i = 0; i < 6; i++) {
     double sl = 0, sq = 0;
 #pragma unroll
     for (int j = 0; j < 6; j++) {
-      sl += P.Dl[i * 6 + j] * nu[j];
-      sq += P.Dq[i * 6 + j] * (fabs(nu[j]) * nu[j]);
+      sl += PD.Dl[i * 6 + j] * nu[j];
+      sq += PD.Dq[i * 6 + j] * (fabs(nu[j]) * nu[j]);
     }
     d[i] = sl + sq;
   }
@@ -169,11 +179,16 @@ UWVK_DEV void v_deriv(const PS& P, const double tau[6], const double s[13], doub
 #endif
 #pragma unroll
   for (int i = 0; i < 6; i++) r[i] = tau[i] - c[i] - d[i] - g[i];
+#if VEL_LAUNDER_MAT
+  const auto& PI = vlaunder(P);
+#else
+  const auto& PI = P;
+#endif
 #pragma unroll
   for (int i = 0; i < 6; i++) {
     double a = 0;
 #pragma unroll
-    for (int j = 0; j < 6; j++) a += P.Minv[i * 6 + j] * r[j];
+    for (int j = 0; j < 6; j++) a += PI.Minv[i * 6 + j] * r[j];
     ds[7 + i] = a;
   }
 }
