@@ -103,6 +103,9 @@ PEAK_HBM_GBS = 8000.0
 # + stage sums / normalisation ~170 = 2,290 flop; a predict integrates the 9
 # sigma points and the side model (10 RK4) plus ~900 flop of 4-DOF UKF algebra;
 # DVL (5 Hz) and pressure (10 Hz) updates add ~20 flop per step on average.
+# This is the reference's formulation; since r04 the kernel evaluates the
+# restoring forces with one rotation (~45 flop instead of 90, VEL_GLIN), so
+# the C2 frac counts ~180 flop per RK4 the kernel no longer spends (~8%).
 F_VEL_RK4 = 2_290
 F_VEL_STEP = 10 * F_VEL_RK4 + 900 + 20  # 23,820
 
