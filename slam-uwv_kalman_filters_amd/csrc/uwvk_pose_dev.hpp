@@ -304,6 +304,93 @@ UWVK_DEV void chol2g_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, 
   }
 }
 
+// Look-ahead form of chol2g_step (UWVK_CHOL_LA): after a group's barrier the
+// owner of the NEXT group first applies this group's columns to the next
+// group's columns only, takes the next group's pivots and publishes them, and
+// only then applies this group's columns to the rest of its own columns.  The
+// serial pivot chain (readlane -> rsqrt -> scale) and the independent trailing
+// update are then in one barrier interval, where the wave's instruction stream
+// interleaves them, instead of the chain starting after the whole update.
+// Each entry still sees the same fused multiply-adds in the same order (this
+// group's columns in order, then the next group's), so the factor is bitwise
+// chol2g_step's.  PRE: this group's pivots were taken in the previous step.
+#ifndef UWVK_CHOL_LA
+#define UWVK_CHOL_LA 0  // r04 A/B: bitwise equal, 2.51 against 2.42-2.44 ms per efforts epoch (profiles/r04/effla/), not kept
+#endif
+template <int DOF, int C0, int C1, int J, int g>
+UWVK_DEV void chol_group_pivots(double (&a)[C1 - C0], double* buf, int r, bool& ok, double piv) {
+  constexpr int jj = J - C0;
+#pragma unroll
+  for (int k = 0; k < g; k++) {
+    const double p = k == 0 ? piv : readlane_d(a[jj + k], J + k);
+    ok = ok && (p > 0.0);
+    const double inv = rsqrt_f64(p);
+    const double d = p * inv;
+    a[jj + k] = (r == J + k) ? d : a[jj + k] * inv;
+    buf[k * 64 + r] = a[jj + k];
+#pragma unroll
+    for (int m = k + 1; m < g; m++) {
+      const double lmk = readlane_d(a[jj + k], J + m);  // L[J+m][J+k]
+      a[jj + m] -= a[jj + k] * lmk;
+      asm volatile("" : "+v"(a[jj + m]));
+    }
+  }
+}
+template <int DOF, int W, int C0, int C1, int J, int S, bool PRE>
+UWVK_DEV void chol2la_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, double piv) {
+  if constexpr (J < DOF) {
+    constexpr int H = (DOF + 1) / 2;
+    constexpr bool own = (J < H) == (W == 0);
+    constexpr int g = chol_group<DOF, J, UWVK_CHOL_GROUP>();
+    constexpr int JN = J + g;
+    static_assert(Geo<DOF>::LPSZ >= 2 * UWVK_CHOL_GROUP * 64, "column buffers in the factor region");
+    double* buf = sm.Lp + (S & 1) * UWVK_CHOL_GROUP * 64;
+    if constexpr (own && !PRE) chol_group_pivots<DOF, C0, C1, J, g>(a, buf, r, ok, piv);
+    __syncthreads();
+    constexpr int cs = JN > C0 ? JN : C0;
+    constexpr bool ownN = JN < DOF && ((JN < H) == (W == 0));
+    constexpr int gN = JN < DOF ? chol_group<DOF, JN, UWVK_CHOL_GROUP>() : 0;
+    constexpr bool la = ownN && cs == JN && JN + gN <= C1;
+    // L[r][J + k]: the owner's own register, the others' the published column
+    double lk[g];
+#pragma unroll
+    for (int k = 0; k < g; k++)
+      lk[k] = own ? a[(J + k - C0) >= 0 && (J + k - C0) < (C1 - C0) ? J + k - C0 : 0] : buf[k * 64 + r];
+    if constexpr (la) {
+      constexpr int e1 = JN + gN;
+#pragma unroll
+      for (int k = 0; k < g; k++)
+#pragma unroll
+        for (int c = JN; c < e1; c++) a[c - C0] -= lk[k] * buf[k * 64 + c];
+#pragma unroll
+      for (int c = JN; c < e1; c++) asm volatile("" : "+v"(a[c - C0]));
+      double* bufN = sm.Lp + ((S + 1) & 1) * UWVK_CHOL_GROUP * 64;
+      chol_group_pivots<DOF, C0, C1, JN, gN>(a, bufN, r, ok, readlane_d(a[JN - C0], JN));
+      if constexpr (e1 < C1) {
+#pragma unroll
+        for (int k = 0; k < g; k++)
+#pragma unroll
+          for (int c = e1; c < C1; c++) a[c - C0] -= lk[k] * buf[k * 64 + c];
+#pragma unroll
+        for (int c = e1; c < C1; c++) asm volatile("" : "+v"(a[c - C0]));
+      }
+      chol2la_step<DOF, W, C0, C1, JN, S + 1, true>(a, sm, r, ok, 0.0);
+    } else {
+      if constexpr (cs < C1) {
+#pragma unroll
+        for (int k = 0; k < g; k++)
+#pragma unroll
+          for (int c = cs; c < C1; c++) a[c - C0] -= lk[k] * buf[k * 64 + c];
+#pragma unroll
+        for (int c = cs; c < C1; c++) asm volatile("" : "+v"(a[c - C0]));
+      }
+      double pnext = 0.0;
+      if constexpr (JN < DOF && JN >= C0 && JN < C1) pnext = readlane_d(a[JN - C0], JN);
+      chol2la_step<DOF, W, C0, C1, JN, S + 1, false>(a, sm, r, ok, pnext);
+    }
+  }
+}
+
 // Cyclic form (UWVK_CHOL_CYCLIC): column blocks [tG, tG + G) alternate between
 // the two waves (block t to wave t & 1) instead of one half per wave, so that
 // both waves keep later columns to update until the end of the factorisation
@@ -394,7 +481,9 @@ UWVK_DEV void chol2_wave(Smem<DOF>& sm) {
 #pragma unroll
   for (int c = C0; c < C1; c++) a[c - C0] = sm.S[rr * DOF + c];
   bool ok = true;
-#if UWVK_CHOL_GROUP > 1
+#if UWVK_CHOL_GROUP > 1 && UWVK_CHOL_LA
+  chol2la_step<DOF, W, C0, C1, 0, 0, false>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
+#elif UWVK_CHOL_GROUP > 1
   chol2g_step<DOF, W, C0, C1, 0, 0>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
 #else
   chol2_step<DOF, W, C0, C1, 0>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
