@@ -603,6 +603,26 @@ UWVK_DEV double row_sum16(double v) {
   v = v + vdpp<0x140>(v);  // row_mirror
   return v;
 }
+// (r04) VEL_ROW_DPP: the row broadcast as DPP row_newbcast (lane SRC of each
+// 16-lane row to the whole row, two v_mov_b32_dpp) instead of two ds_bpermute
+// round trips through the LDS crossbar
+#ifndef VEL_ROW_DPP
+#define VEL_ROW_DPP 0  // r04 A/B: 883.7-891.3 against 880.5-885.8 M steps/s (profiles/r04/rb/), a tie, not kept
+#endif
+template <int SRC>
+UWVK_DEV double row_bcast_c(double v) {
+  static_assert(SRC >= 0 && SRC < 16, "row lane");
+#if VEL_ROW_DPP
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x150 + SRC, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x150 + SRC, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+#else
+  const int ba = (((int)threadIdx.x & ~15) + SRC) * 4;
+  const int lo = __builtin_amdgcn_ds_bpermute(ba, __double2loint(v));
+  const int hi = __builtin_amdgcn_ds_bpermute(ba, __double2hiint(v));
+  return __hiloint2double(hi, lo);
+#endif
+}
 // value of row lane src (0..15) in every lane of the row
 UWVK_DEV double row_bcast(double v, int src) {
   const int ba = (((int)threadIdx.x & ~15) + src) * 4;
@@ -636,7 +656,7 @@ UWVK_DEV void vg_point(const double mu[4], const double L[16], int g, double x[4
 template <int M>
 UWVK_DEV void vg_mean(const double x[M], bool pt, double ref[M]) {
 #pragma unroll
-  for (int k = 0; k < M; k++) ref[k] = row_bcast(x[k], 0);
+  for (int k = 0; k < M; k++) ref[k] = row_bcast_c<0>(x[k]);
   int it = 0;
   double nrm;
   do {
@@ -872,7 +892,7 @@ __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, Vel
       for (int k = 0; k < 13; k++) m[k] = n13[k];
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) q[k] = row_bcast(side ? m[3 + k] : 0.0, 9);
+    for (int k = 0; k < 4; k++) q[k] = row_bcast_c<9>(side ? m[3 + k] : 0.0);
 #if !VEL_PREFETCH
     const uint32_t fl = ea.flags[e];
 #endif
