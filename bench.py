@@ -667,7 +667,7 @@ def bench_vel(a, engine, synth, world, rank, local, dist, B):
         w = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
-    groups = a.vel_groups if a.vel_groups >= 0 else int(B <= 24576)  # uwvk_vel.hip kVelGroupsMaxBatch
+    groups = a.vel_groups if a.vel_groups >= 0 else int(B <= 30720)  # uwvk_vel.hip kVelGroupsMaxBatch
     launches = (a.steps + 4095) // 4096
     flops = B * F_VEL_STEP * a.steps
     tf = flops / (kernel_ms * 1e-3) / 1e12

@@ -959,11 +959,11 @@ struct uwvk_vel {
   int groups = -1;  // UWVK_VEL_OPT_LANE_GROUPS: -1 auto, 0 lane per filter, 1 16 lanes per filter
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
-// auto: lane groups below the measured crossover (C2 on MI355X: the lane-per-
-// filter kernel's epoch latency is flat at ~38-40 us up to batch 65536, one
-// wave per SIMD; the lane-group kernel takes 7.4 us at 4096 and ~1.74 ns per
-// instance once the chip is full, 114 us at 65536)
-static constexpr int64_t kVelGroupsMaxBatch = 24576;
+// auto: lane groups below the measured crossover (MI355X, r04 kernels,
+// profiles/r04/velx/: the lane-per-filter kernel's epoch takes ~32-34 us at any
+// batch up to 65536, one wave per SIMD; the lane-group kernel 4.6 us at 4096
+// and ~1.04 ns per instance once the chip is full: equal near 31k; r03: 24576)
+static constexpr int64_t kVelGroupsMaxBatch = 30720;
 
 static VelBufs vbufs(const uwvk_vel* h) {
   VelBufs b;
