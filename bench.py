@@ -98,16 +98,22 @@ PEAK_HBM_GBS = 8000.0
 
 
 # VelocityUKF (config C2) work per step, frozen from the kernel's code
-# (uwvk_vel.hip): one RK4 step of the Fossen model = 4 derivative evaluations
-# x ~530 flop (rotations 90, Coriolis 102, damping 186, restoring 90, M^-1 72)
-# + stage sums / normalisation ~170 = 2,290 flop; a predict integrates the 9
-# sigma points and the side model (10 RK4) plus ~900 flop of 4-DOF UKF algebra;
-# DVL (5 Hz) and pressure (10 Hz) updates add ~20 flop per step on average.
-# This is the reference's formulation; since r04 the kernel evaluates the
-# restoring forces with one rotation (~45 flop instead of 90, VEL_GLIN), so
-# the C2 frac counts ~180 flop per RK4 the kernel no longer spends (~8%).
-F_VEL_RK4 = 2_290
-F_VEL_STEP = 10 * F_VEL_RK4 + 900 + 20  # 23,820
+# (uwvk_vel.hip v_deriv / v_rk4), an FMA counted as 2.  One derivative
+# evaluation of the Fossen model: the kinematics (position rotation 30,
+# quaternion rate 32) ~60, Coriolis 102, linear + quadratic damping 186, the
+# restoring forces 42 (VEL_GLIN: with r = R^T e_z, -(f_g + f_b) = (W - B) r and
+# -(cog x f_g + cob x f_b) = (W cog - B cob) x r, one rotation + one cross
+# product), tau - C - D - g 18, M^-1 72: ~485 flop; an RK4 step = 4 of them +
+# the stage sums and normalisation ~170 = 2,110 flop.  A predict integrates the
+# 9 sigma points and the side model (10 RK4) plus ~900 flop of 4-DOF UKF
+# algebra; DVL (5 Hz) and pressure (10 Hz) updates add ~20 flop per step on
+# average.  The reference's own formulation (two rotations and two cross
+# products for the restoring forces, ModelSimulation [EXT]) is 90 flop per
+# derivative, 2,290 per RK4: reported beside the executed figure.
+F_VEL_RK4 = 2_110
+F_VEL_RK4_REF = 2_290
+F_VEL_STEP = 10 * F_VEL_RK4 + 900 + 20          # 22,020: what k_vel_epoch_g executes
+F_VEL_STEP_REF = 10 * F_VEL_RK4_REF + 900 + 20  # 23,820: the reference's formulation
 
 
 def parse():
@@ -118,20 +124,25 @@ def parse():
     ap.add_argument("--batch-per-gpu", type=int, default=0,
                     help="0: 65536 (C3/C4 at N = 1), 131072 (C5: N > 1), 4096 (C2)")
     ap.add_argument("--dof", type=int, default=53)
-    ap.add_argument("--mode", default="auto", choices=["auto", "C2", "C3", "C4", "C5"],
-                    help="auto: C3 at N = 1 (headline), C5 at N > 1; C4: ADCP + drop-outs; C2: VelocityUKF")
+    ap.add_argument("--mode", default="auto", choices=["auto", "C1", "C2", "C3", "C4", "C5"],
+                    help="auto: C3 at N = 1 (headline), C5 at N > 1; C4: ADCP + drop-outs; C2: VelocityUKF; "
+                         "C1: one PoseUKF on one CPU core (the oracle's timing build, no GPU)")
     ap.add_argument("--stats-every", type=int, default=1000,
                     help="epochs between ensemble-statistics all-reduces inside the timed region (C5: 1000); "
                          "one more at its end")
+    ap.add_argument("--segment-epochs", type=int, default=0,
+                    help="generate + upload the log in segments of this many epochs, outside the timed region "
+                         "(0: automatic when the IMU log of the whole run exceeds 24 GiB, e.g. C4's full "
+                         "40,000-epoch drop-out cycle)")
     ap.add_argument("--c4-cycle", default="30,10",
                     help="C4 DVL drop-out cycle 'on,off' in s; e.g. 0.3,0.1 keeps every event rate of the 30/10 "
                          "cycle (0.25%% efforts epochs) inside a 2000-epoch window")
     ap.add_argument("--vel-groups", type=int, default=-1, help="C2: -1 auto, 0 lane per filter, 1 16-lane rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true", help="literal kernels (all 2n+1 sigma points)")
-    ap.add_argument("--so3-right", action="store_true",
-                    help="UWVK_OPT_SO3_RIGHT: the body-frame SO3 boxplus q exp(d) (classic MTK) instead of the "
-                         "nav-frame exp(d) q; the PSP kernels' SR = 1 instantiations (DESIGN.md 4.3)")
+    ap.add_argument("--so3-left", action="store_true",
+                    help="UWVK_OPT_SO3_RIGHT = 0: the nav-frame SO3 boxplus exp(d) q instead of the default body-frame "
+                         "q exp(d) (MTK's SO3::boxplus); the PSP kernels' SR = 0 instantiations (DESIGN.md 4.3)")
     ap.add_argument("--tail-chunks", type=int, default=0,
                     help="UWVK_OPT_TAIL_CHUNKS (diagnostic A/B): force this many chunks per tail instance, 0 = planner")
     ap.add_argument("--persist", type=int, default=-1,
@@ -150,20 +161,58 @@ def parse():
     return ap.parse_args()
 
 
-def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance, c4_cycle=(30.0, 10.0), cfg=None):
-    """Log of warmup+steps epochs whose 5 Hz DVL schedule puts at least one DVL
-    epoch inside the timed window (exactly the 1-in-200 rate when steps >= 200)."""
-    total = warmup + steps
-    # shift the start so that a DVL epoch (k % 200 == 0) lands mid-window
+def window_shift(warmup, steps):
+    """Epochs run before the warm-up so that the 5 Hz DVL schedule puts at least
+    one DVL epoch inside the timed window (exactly the 1-in-200 rate when
+    steps >= 200): a DVL epoch (k % 200 == 0) lands mid-window."""
     target = warmup + min(steps, 200) // 2
     shift = (200 - (target + 1) % 200) % 200
     # diagnostic only (never the headline): UWVK_BENCH_WINDOW_OFFSET moves the window
     # off the DVL epoch (100: no DVL update in a window of < 100 epochs); the line
     # reports dvl_epochs_in_window either way
-    shift += int(os.environ.get("UWVK_BENCH_WINDOW_OFFSET", "0"))
-    log = synth.make_pose_log(batch, total + shift, mode=mode, dof=dof, first_instance=first_instance,
-                              dropout_on=c4_cycle[0], dropout_off=c4_cycle[1], cfg=cfg)
+    return shift + int(os.environ.get("UWVK_BENCH_WINDOW_OFFSET", "0"))
+
+
+def dvl_aligned_log(synth, batch, warmup, steps, mode, dof, first_instance, c4_cycle=(30.0, 10.0), cfg=None,
+                    epoch0=0, epochs=None):
+    """Log of shift + warmup + steps epochs (window_shift), or its segment
+    [epoch0, epoch0 + epochs) (synth.make_pose_log epoch0: a bitwise slice)."""
+    shift = window_shift(warmup, steps)
+    total = shift + warmup + steps
+    n = total - epoch0 if epochs is None else epochs
+    log = synth.make_pose_log(batch, n, mode=mode, dof=dof, first_instance=first_instance,
+                              dropout_on=c4_cycle[0], dropout_off=c4_cycle[1], cfg=cfg, epoch0=epoch0)
     return log, shift
+
+
+# host + device bytes of the IMU part of a log per instance-epoch (gyro + acc, fp64):
+# above SEGMENT_AUTO_BYTES the window is generated and uploaded in segments
+LOG_BYTES_PER_INSTANCE_EPOCH = 48
+SEGMENT_AUTO_BYTES = 24 << 30
+
+
+def timed_run(f, dlog, base, e_from, e_to, cut_abs, reduce_stats, truth, dof, barrier):
+    """One timed region: absolute epochs [e_from, e_to) of a device log whose
+    epoch 0 is absolute epoch `base`, the ensemble statistics reduced at the
+    absolute epochs of cut_abs inside (e_from, e_to].  Barrier + device sync on
+    both sides; HIP events on the handle's stream around the epoch launches.
+    Returns (wall_s, kernel_ms, last statistics or None, run_log calls)."""
+    pts = sorted({c for c in cut_abs if e_from < c <= e_to} | {e_to})
+    barrier()
+    f.synchronize()
+    t0 = time.perf_counter()
+    f.timer_start()
+    prev, stats = e_from, None
+    for k, c in enumerate(pts):
+        f.run_log(dlog, prev - base, c - prev, sync=False)
+        if k == len(pts) - 1:
+            f.timer_mark()  # HIP events on the handle's stream around the epoch launches (no host wait)
+        if c in cut_abs:
+            stats = reduce_stats(truth.state(c, dof))  # synchronous
+        prev = c
+    f.synchronize()
+    barrier()
+    return time.perf_counter() - t0, f.timer_elapsed(), stats, len(pts)
 
 
 def pmc_entry(workload, steps=None):
@@ -225,16 +274,16 @@ def initialise(f, log, cfg, uwv, init, first_instance=0):
     del x, P
 
 
-def cpu_baseline(synth, cfg, uwv, mode, dof, threads, init="mc", right=False):
+def cpu_baseline(synth, cfg, uwv, mode, dof, threads, init="mc", right=True):
     """The fp64 C oracle's timing build (oracle/liboracle_fast.so: -O3,
     x86-64-v4, one instance per task, pthreads) on a bounded sample of the same
     workload, on every core this process may use; plus one instance on one
     core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as O
-    if right:  # the oracle's switch is process-wide: the whole sample on the right side
-        with O.so3_right():
-            return cpu_baseline(synth, cfg, uwv, mode, dof, threads, init, right=False)
+    if right is not None:  # the oracle's switch is process-wide (both builds): the whole sample on that side
+        with O.so3_side(right):
+            return cpu_baseline(synth, cfg, uwv, mode, dof, threads, init, right=None)
     epochs = 2000
     # single core first: it sizes the multi-core sample to ~15 s of wall time
     log1 = synth.make_pose_log(1, epochs, mode=mode, dof=dof, cfg=cfg)
@@ -431,6 +480,8 @@ def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(sys.argv[1:], a.gpus))
+    if a.mode == "C1":
+        return bench_c1(a)
     world, rank, local = resolve_world(a)
     # UWVK_BENCH_SAME_DEVICE=1: rehearsal of the N-rank path on one GPU (all ranks on device 0)
     same_dev = os.environ.get("UWVK_BENCH_SAME_DEVICE") == "1"
@@ -447,11 +498,31 @@ def main():
         from uwvk import config as uconfig
         fc = uconfig.load(a.config)
         cfg, uwv, eng_opts = fc.pose, fc.uwv, fc.engine
-        if eng_opts.get("so3_right"):
-            a.so3_right = True  # the side also selects the kernel name and the CPU baseline's side
+        # the file's engine options win over the command line (config.apply_engine_options);
+        # mirror them into the arguments, which name the kernel, the flop model and the
+        # CPU baseline's side
+        if "so3_right" in eng_opts:
+            if a.so3_left and eng_opts["so3_right"]:
+                print("warning: --so3-left overridden by %s (engine.so3_right: true)" % a.config, file=sys.stderr)
+            a.so3_left = not eng_opts["so3_right"]
+        if eng_opts.get("dense_sigma") or eng_opts.get("literal_apply_delta"):
+            a.dense = True  # either option switches the handle to the literal kernels (use_dense)
+        a.literal_apply_delta = bool(eng_opts.get("literal_apply_delta"))
+        for k, flag in (("tail_slots", "tail_slots"), ("persist", "persist")):
+            if k in eng_opts and getattr(a, flag) != eng_opts[k] and getattr(a, flag) not in (0, -1):
+                print("warning: --%s %s overridden by %s (engine.%s: %s)" % (flag.replace("_", "-"), getattr(a, flag),
+                                                                             a.config, k, eng_opts[k]), file=sys.stderr)
     cyc = tuple(float(v) for v in a.c4_cycle.split(","))
-    log, shift = dvl_aligned_log(synth, B, a.warmup, a.steps, log_mode, a.dof, first_instance=rank * B, c4_cycle=cyc,
-                                 cfg=cfg)
+    shift = window_shift(a.warmup, a.steps)
+    total = shift + a.warmup + a.steps
+    e0 = shift + a.warmup
+    seg = a.segment_epochs
+    if seg == 0 and B * total * LOG_BYTES_PER_INSTANCE_EPOCH > SEGMENT_AUTO_BYTES:
+        seg = 4000
+    seg = seg if 0 < seg < total else 0
+    seg_bounds = [(s0, min(total, s0 + seg)) for s0 in range(0, total, seg)] if seg else [(0, total)]
+    log, _ = dvl_aligned_log(synth, B, a.warmup, a.steps, log_mode, a.dof, first_instance=rank * B, c4_cycle=cyc,
+                             cfg=cfg, epochs=seg_bounds[0][1])
     f = engine.PoseUKFBatch(B, a.dof, device=local)
     f.set_tail_slots(a.tail_slots)
     if a.persist >= 0:
@@ -462,19 +533,9 @@ def main():
         f.set_dense_sigma(True)
     if eng_opts:
         uconfig.apply_engine_options(f, eng_opts)
-    if a.so3_right:
-        f.set_so3_right(True)
+    f.set_so3_right(not a.so3_left)
     initialise(f, log, cfg, uwv, a.init, first_instance=rank * B)
     f.set_process_noise_from_config(cfg, log["dt"])
-    dlog = f.upload_log(log)
-    flags = log["flags"]
-    # advance through the alignment shift (untimed)
-    if shift:
-        f.run_log(dlog, 0, shift)
-    f.run_log(dlog, shift, a.warmup)  # warmup (untimed)
-    e0 = shift + a.warmup
-    window = flags[e0:e0 + a.steps]
-    n_dvl = int(((window & 2) != 0).sum())
     # The collective (C5): the per-rank ensemble statistics summed over the
     # engine's RCCL communicator on the handle's stream (uwvk_pose_ensemble_
     # allreduce), every --stats-every epochs and at the end of the window.  The
@@ -494,33 +555,45 @@ def main():
             st = ensemble.allreduce_stats(st, dist)
         return st
 
-    # statistics points inside the window: every --stats-every epochs, and its end
-    every = max(1, a.stats_every)
-    cuts = sorted({min(a.steps, k) for k in range(every, a.steps, every)} | {a.steps})
-    # warm the statistics kernels and the collective (module load, RCCL
-    # channel set-up) outside the timed region
-    reduce_stats(log["truth"].state(e0, a.dof))
-
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    barrier()
-    f.synchronize()
-    t0 = time.perf_counter()
-    f.timer_start()
-    prev = 0
-    stats = None
-    for k, cut in enumerate(cuts):
-        f.run_log(dlog, e0 + prev, cut - prev, sync=False)
-        if k == len(cuts) - 1:
-            f.timer_mark()  # HIP events on the handle's stream around the epoch launches (no host wait)
-        stats = reduce_stats(log["truth"].state(e0 + cut, a.dof))  # synchronous
-        prev = cut
-    f.synchronize()
-    barrier()
-    wall = time.perf_counter() - t0
-    kernel_ms = f.timer_elapsed()
+    # statistics points inside the window: every --stats-every epochs, and its end
+    every = max(1, a.stats_every)
+    cuts = sorted({min(a.steps, k) for k in range(every, a.steps, every)} | {a.steps})
+    cut_abs = {e0 + c for c in cuts}
+    # Segments (a window whose log does not fit host / device memory at once, e.g.
+    # C4's full 40,000-epoch drop-out cycle): each segment's inputs are generated
+    # and uploaded outside the timed region (bitwise slices of the whole log), the
+    # filter state stays on the device, and the window's time is the sum of the
+    # segments' timed runs.  Without segments this is one timed region.
+    wall, kernel_ms, stats, pieces, windows = 0.0, 0.0, None, 0, []
+    truth = log["truth"]
+    for si, (s0, s1) in enumerate(seg_bounds):
+        if seg:
+            print("segment %d/%d: epochs [%d, %d)" % (si + 1, len(seg_bounds), s0, s1), file=sys.stderr, flush=True)
+        if si:
+            del dlog
+            log, _ = dvl_aligned_log(synth, B, a.warmup, a.steps, log_mode, a.dof, first_instance=rank * B,
+                                     c4_cycle=cyc, cfg=cfg, epoch0=s0, epochs=s1 - s0)
+            truth = log["truth"]
+        dlog = f.upload_log(log)
+        if s0 < e0:  # the alignment shift and the warm-up (untimed)
+            f.run_log(dlog, 0, min(s1, e0) - s0)
+        if si == 0:
+            # warm the statistics kernels and the collective (module load, RCCL
+            # channel set-up) outside the timed region
+            reduce_stats(truth.state(min(max(e0, s0), s1), a.dof))
+        lo = max(s0, e0)
+        if lo < s1:
+            windows.append(log["flags"][lo - s0:])
+            w_s, k_ms, st, n = timed_run(f, dlog, s0, lo, s1, cut_abs, reduce_stats, truth, a.dof, barrier)
+            wall, kernel_ms, pieces = wall + w_s, kernel_ms + k_ms, pieces + n
+            stats = st if st is not None else stats
+    window = np.concatenate(windows)
+    assert len(window) == a.steps
+    n_dvl = int(((window & 2) != 0).sum())
     if dist is not None:
         import torch
         w = torch.tensor([wall, kernel_ms], dtype=torch.float64)
@@ -530,7 +603,7 @@ def main():
     # per-rank statistics (same fixed-order kernel sums on every rank)
     coll_check = None
     if dist is not None and world > 1:
-        local_st = f.ensemble_stats(log["truth"].state(e0 + a.steps, a.dof))
+        local_st = f.ensemble_stats(truth.state(e0 + a.steps, a.dof))
         host_sum = ensemble.allreduce_stats(local_st, dist)
         # the two sums add the same per-rank values in different orders: they
         # agree to world x eps x the sum of the magnitudes (elementwise), which
@@ -548,21 +621,24 @@ def main():
     # launches in the timed window: the PSP path runs each statistics interval
     # in one k_psp_epoch launch (efforts epochs split it); the literal path one per epoch
     n_eff = int(((window & 0x10) != 0).sum())
-    launches = a.steps if a.dense else len(cuts) + 2 * n_eff
+    launches = a.steps if a.dense else pieces + 2 * n_eff
     per_launch_ms = kernel_ms / launches
     # reference-equivalent work (the literal ukfom algorithm)
     flops_ref = B * (F_STEP * a.steps + F_UPD3 * n_dvl)
     # the engine's own flop model: the useful work it does
-    flops_model = B * ((F_STEP_EXEC * a.steps + F_UPD3_EXEC * n_dvl) if a.dense
-                       else (F_STEP_PSP * a.steps + F_UPD3_PSP * n_dvl))
+    lad = getattr(a, "literal_apply_delta", False)  # the literal re-spread: the reference's own flops
+    step_model, upd_model = ((F_STEP, F_UPD3) if lad else (F_STEP_EXEC, F_UPD3_EXEC)) if a.dense \
+        else (F_STEP_PSP, F_UPD3_PSP)
+    flops_model = B * (step_model * a.steps + upd_model * n_dvl)
     eff_tf = flops_ref / (kernel_ms * 1e-3) / 1e12
     model_tf = flops_model / (kernel_ms * 1e-3) / 1e12
     # the PSP instantiation run (uwvk_psp_k.hip launch_epoch_dof): Q shape, and
     # 1 when the window holds no pressure / ADCP epoch (0x4 | 0x8)
     evs = 0 if (f.epoch_qshape() != 1 or bool(((window & 0xC) != 0).any())) else 1
-    sr = 1 if a.so3_right else 0
+    sr = 0 if a.so3_left else 1
     kname = ("k_pose_epoch<%d>" % a.dof) if a.dense else ("k_psp_epoch<%d, %d, %d, %d>" % (a.dof, f.epoch_qshape(), evs, sr))
-    workload = "%s-dof%d-b%d%s%s" % (log_mode, a.dof, B, "-dense" if a.dense else "", "-right" if sr else "")
+    workload = "%s-dof%d-b%d%s%s%s" % (log_mode, a.dof, B, "-dense" if a.dense else "",
+                                       "-lad" if getattr(a, "literal_apply_delta", False) else "", "" if sr else "-left")
     pmc = pmc_entry(workload, a.steps)
     cr = None if a.dense or launches != 1 else counter_roofline(pmc, B, a.steps, kernel_ms)
     traffic = pmc.get("bytes_per_launch") if pmc.get("epochs_per_launch") == a.steps and launches == 1 else None
@@ -584,7 +660,7 @@ def main():
             "frac_active_source": ("VALU lane-slot flops x SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / 64 (%.1f of 64 lanes "
                                    "active per VALU cycle), plus the MFMA flops" % lanes) if frac_active is not None else None,
             "counters": cr,
-            "model_flop_per_step": (F_STEP_EXEC if a.dense else F_STEP_PSP),
+            "model_flop_per_step": step_model,
             "model_tflops": model_tf,
             "effective_tflops": eff_tf,
             "effective_note": "reference-equivalent rate: SURVEY 8(d)'s literal-ukfom work (1,554,084 flop per "
@@ -609,6 +685,11 @@ def main():
                    "efforts_epochs_in_window": n_eff,
                    "adcp_epochs_in_window": int(((window & 8) != 0).sum()),
                    "c4_cycle_s": list(cyc) if mode == "C4" else None,
+                   "segments": ({"count": len(seg_bounds), "epochs_per_segment": seg,
+                                 "note": "each segment's inputs generated and uploaded outside the timed region "
+                                         "(bitwise slices of the whole log, synth.make_pose_log epoch0); the "
+                                         "filter state stays in HBM; value = steps / the sum of the segments' "
+                                         "timed runs"} if seg else None),
                    "parallelism": "instance-sharded x%d (no data-path collective)" % world,
                    "collective": coll_desc,
                    "stats_allreduces_in_window": len(cuts) if world > 1 else 0,
@@ -617,7 +698,7 @@ def main():
                             "sd %g m/s), second constructor" % (list(synth.MC_ROT_SD), synth.MC_VEL_SD))
                            if a.init == "mc" else "first constructor (prior from the config)",
                    "path": "dense (all 2n+1 sigma points)" if a.dense else "PSP (partitioned sigma points)",
-                   "so3_boxplus": "right (body frame, q exp(d))" if a.so3_right else "left (nav frame, exp(d) q)",
+                   "so3_boxplus": "left (nav frame, exp(d) q)" if a.so3_left else "right (body frame, q exp(d))",
                    "kernel": kname,
                    "config_file": a.config or None},
         "collective_check": coll_check,
@@ -628,7 +709,7 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(synth, cfg, uwv, log_mode, a.dof, a.cpu_threads or available_cores(),
-                                           a.init, right=a.so3_right)
+                                           a.init, right=not a.so3_left)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:
@@ -637,6 +718,58 @@ def main():
         dist.destroy_process_group()
     if coll_check is False:
         sys.exit(3)
+
+
+def bench_c1(a):
+    """Config C1: one PoseUKF, the kinematic n = 26 layout (the
+    config's "~30-dim state") and the full n = 53, a 60 s log = 60,000 IMU
+    epochs with 300 DVL updates (5 Hz), on ONE CPU core: the fp64 C oracle's
+    timing build (oracle/liboracle_fast.so, -O3 x86-64-v4), i.e. ukfom's literal
+    algorithm (all 2n+1 sigma points) restated -- the reference itself cannot be
+    built here.  No GPU is used.  --steps sets the epochs (default
+    60,000 when --steps is left at its default)."""
+    from uwvk import synth
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ctypes as O
+    epochs = 60_000 if a.steps == 200 else a.steps
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    avail = available_cores()
+    if cpus:
+        os.sched_setaffinity(0, {cpus[0]})  # one core, as SURVEY 8(d)(i)
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    res = {}
+    with O.so3_side(not a.so3_left):
+        for dof in (26, 53):
+            log = synth.make_pose_log(1, epochs, mode="C3", dof=dof, cfg=cfg)
+            o = O.OraclePoseBatch(1, dof, timing=True)
+            initialise(o, log, cfg, uwv, a.init)
+            o.set_process_noise_from_config(cfg, log["dt"])
+            t0 = time.perf_counter()
+            counts = o.run_log(log, nthreads=1)
+            dt = time.perf_counter() - t0
+            x, P = o.get_state()
+            res[dof] = {"value": epochs / dt, "seconds": dt, "epochs": epochs,
+                        "dvl_updates": int(((log["flags"] & 2) != 0).sum()),
+                        "accepted_updates": [int(v) for v in counts[0]],
+                        "finite": bool(np.all(np.isfinite(x)) and np.all(np.isfinite(P))),
+                        "flop_per_step": (F_STEP if dof == 53 else 192_366)}
+            del log, o
+    out = {"metric": "PoseUKF predict+update steps/sec, 1 instance on 1 CPU core (config C1)",
+           "value": res[26]["value"], "unit": "steps/s", "n_gpus": 0, "steps": epochs, "warmup": 0,
+           "ms_per_step": 1e3 / res[26]["value"], "higher_is_better": True, "scaling": None, "vs_baseline": None,
+           "dtype": "f64", "data": "synthetic",
+           "config": {"workload": "C1: one PoseUKF, n = 26 (kinematic subset, the config's ~30-dim state; value) and "
+                                  "n = 53 (full state), %d epochs of 1 kHz IMU + 5 Hz DVL" % epochs,
+                      "global_batch": 1, "so3_boxplus": "left (nav frame, exp(d) q)" if a.so3_left
+                      else "right (body frame, q exp(d))",
+                      "implementation": "fp64 C oracle, timing build (oracle/liboracle_fast.so: -O3 "
+                                        "-march=x86-64-v4), ukfom's literal algorithm; the reference is unbuildable "
+                                        "here (SURVEY K3)",
+                      "init": "Monte-Carlo start (second constructor)" if a.init == "mc" else "first constructor"},
+           "dof26": res[26], "dof53": res[53],
+           "host": {"cpu": _cpu_model(), "nproc": os.cpu_count(), "available_to_job": avail,
+                    "pinned_cpu": cpus[0] if cpus else None}}
+    print(json.dumps(out), flush=True)
 
 
 def bench_vel(a, engine, synth, world, rank, local, dist, B):
@@ -671,6 +804,7 @@ def bench_vel(a, engine, synth, world, rank, local, dist, B):
     launches = (a.steps + 4095) // 4096
     flops = B * F_VEL_STEP * a.steps
     tf = flops / (kernel_ms * 1e-3) / 1e12
+    tf_ref = B * F_VEL_STEP_REF * a.steps / (kernel_ms * 1e-3) / 1e12
     kname = "k_vel_epoch_g" if groups else "k_vel_epoch"
     out = {
         "metric": "VelocityUKF predict+update steps/sec at batch=%d (config C2)" % B, "value": B * world * a.steps / wall,
@@ -682,7 +816,13 @@ def bench_vel(a, engine, synth, world, rank, local, dist, B):
                    "layout": "16 lanes per filter" if groups else "one filter per lane", "kernel": kname},
         "roofline": {"bound": "valu-fp64", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                      "frac": tf / PEAK_FP64_TFLOPS, "traffic": None, "kernel": kname, "launches": launches,
-                     "kernel_ms_per_launch": kernel_ms / launches, "algorithmic_flop_per_step": F_VEL_STEP},
+                     "kernel_ms_per_launch": kernel_ms / launches, "algorithmic_flop_per_step": F_VEL_STEP,
+                     "achieved_source": "the kernel's executed formulation (bench.py F_VEL_STEP: restoring forces "
+                                        "through one rotation, VEL_GLIN) over the HIP-event kernel time",
+                     "reference_formulation": {"flop_per_step": F_VEL_STEP_REF, "tflops": tf_ref,
+                                               "frac": tf_ref / PEAK_FP64_TFLOPS,
+                                               "note": "the same time priced at the reference's formulation "
+                                                       "(two rotations for the restoring forces); not a roofline"}},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         threads = a.cpu_threads or available_cores()

@@ -205,6 +205,12 @@ uwvk_status uwvk_memcpy_d2h_on(void* dst, const void* src, size_t bytes, void* s
  * runs therefore draw bitwise the rows of the full batch. */
 uwvk_status uwvk_synth_normal(uint64_t seed, int64_t first_instance, int64_t batch, uint32_t stream, int64_t count,
                               double* out);
+/* The variates [offset, offset + count) of the same per-(instance, stream)
+ * sequences (uwvk_synth_normal is offset 0, group 0).  group 0: out[batch][count];
+ * group g > 0 (count a multiple of g): record-major out[count / g][batch][g],
+ * the logs' [epoch][instance][component] layout. */
+uwvk_status uwvk_synth_normal_at(uint64_t seed, int64_t first_instance, int64_t batch, uint32_t stream,
+                                 int64_t offset, int64_t count, int32_t group, double* out);
 
 /* ======================================================================== */
 /* PoseUKF                                                                   */
@@ -419,15 +425,17 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   any kind runs only where uwvk_xcd_round_robin(device) is 1. */
 #define UWVK_OPT_TAIL_CHUNKS 4
 /* UWVK_OPT_SO3_RIGHT: the side of the SO3 [+] / [-] [EXT MTK], SURVEY 8(c)
- *   item 5, the largest unpinned semantic.  0 (default): nav frame (left),
- *   q [+] d = exp(d) q, the convention the reference's usage implies
- *   (PoseUKF.cpp:31-32, :451).  1: body frame (right, classic MTK
- *   SO3::boxplus), q [+] d = q exp(d), in every orientation [+] / [-]: sigma
- *   points, processModel's orientation step (PoseUKF.cpp:32), manifold mean,
- *   apply_delta, the visual update's filter and marker orientations and the
- *   ensemble statistics' orientation error (log(t^-1 q)).  Every engine path
- *   runs either side (the PSP kernels are instantiated per side, SR); the
- *   oracle's or_set_so3_right is the same switch. */
+ *   item 5, the largest unpinned semantic.  1 (default since r05): body frame
+ *   (right), q [+] d = q exp(d), MTK's published SO3::boxplus, through which the
+ *   reference's orientation.boxplus runs (mtkwrap<MTK::SO3<double>>,
+ *   PoseState.hpp:15; PoseUKF.cpp:32), in every orientation [+] / [-]: sigma
+ *   points, processModel's orientation step, manifold mean, apply_delta, the
+ *   visual update's filter and marker orientations and the ensemble
+ *   statistics' orientation error (log(t^-1 q)).  0: nav frame (left),
+ *   q [+] d = exp(d) q, an option (the convention SURVEY 8(c) had inferred
+ *   from PoseUKF.cpp:31 / :451).  Every engine path runs either side (the PSP
+ *   kernels are instantiated per side, SR); the oracle's or_set_so3_right is
+ *   the same switch. */
 #define UWVK_OPT_SO3_RIGHT 5
 /* UWVK_OPT_PERSIST: scheduling of the PSP run_log launch.  0 (default): one
  *   workgroup per instance (plus UWVK_OPT_TAIL_SLOTS spreading, which needs the
@@ -615,6 +623,10 @@ typedef struct uwvk_ipose uwvk_ipose;
 uwvk_status uwvk_ipose_create(int64_t batch, int device, uwvk_ipose** out);
 void uwvk_ipose_destroy(uwvk_ipose* h);
 void* uwvk_ipose_stream(const uwvk_ipose* h);
+/* UWVK_OPT_SO3_RIGHT only: the side of the orientation_error [+] / [-] (an
+ * MTK::SO3, IndirectPoseUKF.hpp:21), 1 (default) body frame q exp(d), 0 nav
+ * frame exp(d) q, as uwvk_pose_set_option; the oracle's or_set_so3_right. */
+uwvk_status uwvk_ipose_set_option(uwvk_ipose* h, int option, int value);
 /* IndirectPoseUKF(position_error_std, orientation_error_std, orientation_error_tau,
  * initial_position_error, initial_position_error_std) (IndirectPoseUKF.cpp:53-78):
  * stds shared; initial_position_error batch*3 (NULL = zero); initial std NULL = ones. */

@@ -66,9 +66,26 @@ def so3_log(q):
 
 
 # ---------------------------------------------------------------- layout
+# SO3 [+] side, process-wide like the C oracle's switch:
+# True = body frame q exp(d) (default since r05, MTK's SO3::boxplus), False =
+# nav frame exp(d) q.  Set it before constructing a twin.
+SO3_RIGHT = True
+
+
+def so3_plus(q, d, right):
+    """q [+] d for an already scaled rotation vector d."""
+    return qmul(q, so3_exp(d)) if right else qmul(so3_exp(d), q)
+
+
+def so3_minus(a, b, right):
+    """a [-] b: log(b^-1 a) (right) or log(a b^-1) (left)."""
+    return so3_log(qmul(qconj(b), a)) if right else so3_log(qmul(a, qconj(b)))
+
+
 class Layout:
-    def __init__(self, dof):
+    def __init__(self, dof, right=None):
         self.dof = dof
+        self.right = SO3_RIGHT if right is None else right
         self.full = dof == 53
         self.store = dof + 1
         # tangent -> storage for vect DOFs
@@ -86,16 +103,16 @@ class Layout:
             self.d.update(inertia=19, lin=28, quad=37)
 
     def boxplus(self, X, D):
-        """X [..., store] (+) D [..., dof]: vect + D; SO3 exp(D) * q (nav-frame)."""
+        """X [..., store] (+) D [..., dof]: vect + D; SO3 q exp(D) (right) or exp(D) q (left)."""
         Y = np.array(X, dtype=float, copy=True)
         Y[..., self.vec_s] = X[..., self.vec_s] + D[..., self.vec_d]
-        Y[..., 3:7] = qmul(so3_exp(D[..., 3:6]), X[..., 3:7])
+        Y[..., 3:7] = so3_plus(X[..., 3:7], D[..., 3:6], self.right)
         return Y
 
     def boxminus(self, X, M):
         D = np.zeros(X.shape[:-1] + (self.dof,))
         D[..., self.vec_d] = X[..., self.vec_s] - M[..., self.vec_s]
-        D[..., 3:6] = so3_log(qmul(X[..., 3:7], qconj(M[..., 3:7])))
+        D[..., 3:6] = so3_minus(X[..., 3:7], M[..., 3:7], self.right)
         return D
 
 
@@ -335,7 +352,7 @@ class PoseTwin:
         lat, _ = nav_to_world(self.loc, X[:, 0], X[:, 1])
         er = EARTHW * np.stack([np.cos(lat), np.zeros_like(lat), np.sin(lat)], -1)
         wn = qrot(X[:, 3:7], self.w - X[:, s["bg"]:s["bg"] + 3]) - er
-        Y[:, 3:7] = qmul(so3_exp(wn * dt), X[:, 3:7])
+        Y[:, 3:7] = so3_plus(X[:, 3:7], wn * dt, self.lay.right)  # orientation.boxplus, :32
         Y[:, 7:10] = X[:, 7:10] + dt * X[:, 10:13]
 
         def decay(sl, tau, off):

@@ -53,18 +53,37 @@ def lib_timing():
     return _LIB_FAST
 
 
-class so3_right:
-    """Context manager: run the oracle with the body-frame (right) SO3 [+]
-    instead of the default nav-frame (left) one."""
+class so3_side:
+    """Context manager: run the oracle with the given SO3 [+] side (SURVEY
+    §8(c) item 5), right = body frame q exp(d) (the default since r05, MTK's
+    SO3::boxplus), left = nav frame exp(d) q.  The switch is a process-wide
+    global of each oracle library, so it is set in the parity build and in the
+    timing build alike."""
+
+    def __init__(self, right):
+        self.right = 1 if right else 0
 
     def __enter__(self):
-        self.prev = lib().or_get_so3_right()
-        lib().or_set_so3_right(1)
+        self.libs = [lib(), lib_timing()]
+        self.prev = [L.or_get_so3_right() for L in self.libs]
+        for L in self.libs:
+            L.or_set_so3_right(self.right)
         return self
 
     def __exit__(self, *exc):
-        lib().or_set_so3_right(self.prev)
+        for L, p in zip(self.libs, self.prev):
+            L.or_set_so3_right(p)
         return False
+
+
+def so3_right():
+    """The body-frame side (the default; explicit for parametrised tests)."""
+    return so3_side(True)
+
+
+def so3_left():
+    """The nav-frame side, exp(d) q (the non-default option)."""
+    return so3_side(False)
 
 
 def dp(a):

@@ -109,15 +109,18 @@ void or_so3_log(const double q[4], double o[3]) {
 }
 
 /* SO3 boxplus side [EXT MTK], SURVEY §8(c) item 5: the largest unpinned semantic.
- * 0 (default): nav-frame / left, q [+] d = exp(d) * q, the convention the reference's
- *   usage implies (omega rotated into nav, PoseUKF.cpp:31-32; Q_o rotated by R, :451);
- * 1: body-frame / right, q [+] d = q * exp(d), classic MTK SO3::boxplus.
+ * 1 (default since r05): body-frame / right, q [+] d = q * exp(d), MTK's published
+ *   SO3::boxplus (Hertzberg et al. 2013).  The reference's arithmetic goes through
+ *   MTK (mtkwrap<MTK::SO3<double>>, PoseState.hpp:15; orientation.boxplus,
+ *   PoseUKF.cpp:32), whatever frame the caller meant when it rotated omega into
+ *   nav (PoseUKF.cpp:31) -- this overrides SURVEY §8(c) item 5's left default
+ *   (DESIGN.md §3).
+ * 0: nav-frame / left, q [+] d = exp(d) * q, kept as an option (or_set_so3_right(0)).
  * Applies to every PoseUKF orientation [+]/[-], including processModel's
- * new_state.orientation.boxplus (PoseUKF.cpp:32).  The HIP engine implements the
- * default only; the switch exists so the pin can be applied once the semantics
- * of the real MTK binary are known (tests/test_oracle_kat.py shows the two
- * conventions give materially different C3 trajectories). */
-static int g_so3_right = 0;
+ * new_state.orientation.boxplus (PoseUKF.cpp:32).  The HIP engine has the same
+ * switch (UWVK_OPT_SO3_RIGHT, default 1); tests/test_oracle_kat.py shows the two
+ * conventions give materially different C3 trajectories. */
+static int g_so3_right = 1;
 void or_set_so3_right(int on) { g_so3_right = on ? 1 : 0; }
 int or_get_so3_right(void) { return g_so3_right; }
 

@@ -68,8 +68,9 @@ void or_calc_efforts(const uwvk_uwv_params* p, const double acc6[6], const doubl
                      double tau[6]);
 void or_boxplus(const or_layout* L, const double* x, const double* delta, double scale, double* out);
 void or_boxminus(const or_layout* L, const double* a, const double* b, double* out);
-/* SO3 [+] side, process-wide: 0 = nav-frame/left (default,
- * what the HIP engine implements), 1 = body-frame/right (classic MTK). */
+/* SO3 [+] side, process-wide: 1 = body-frame/right, q exp(d)
+ * (default since r05: MTK's SO3::boxplus, through which PoseUKF.cpp:32 runs),
+ * 0 = nav-frame/left, exp(d) q (option).  The HIP engine's UWVK_OPT_SO3_RIGHT. */
 void or_set_so3_right(int on);
 int or_get_so3_right(void);
 

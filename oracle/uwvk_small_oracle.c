@@ -361,11 +361,14 @@ int or_bottom_update_normal(or_bottom* f, const double mu[3], const double cov[4
 /* ======================================================================== */
 static sm_manifold ipose_manifold(int with_marker) {
   sm_manifold M = {0};
+  /* orientation_error is an MTK::SO3 like PoseUKF's orientation: the same side
+   * switch (or_set_so3_right; the default right, q exp(d)) */
+  const int so3 = or_get_so3_right() ? SEG_SO3R : SEG_SO3;
   sm_add(&M, SEG_V, 3);  /* position_error, IndirectPoseUKF.hpp:20 */
-  sm_add(&M, SEG_SO3, 3); /* orientation_error, :21 */
+  sm_add(&M, so3, 3);    /* orientation_error, :21 */
   if (with_marker) {      /* FilterStateWithMarker, IndirectPoseUKF.cpp:25-29 */
     sm_add(&M, SEG_V, 3);
-    sm_add(&M, SEG_SO3, 3);
+    sm_add(&M, so3, 3);
   }
   return M;
 }
@@ -397,7 +400,10 @@ static void ipose_process(void* ctx, const double* x, double* o) {
   for (int k = 0; k < 3; k++) d[k] = (-1.0 / c[0]) * l[k] * c[1];
   or_so3_exp(d, e);
   memcpy(tmp, x, sizeof(tmp));
-  or_quat_mul(e, x + 3, tmp + 3);
+  /* orientation_error.boxplus(d, dt), :17, on the side of the switch (e is a
+   * power of x's own rotation, so the two products agree) */
+  if (or_get_so3_right()) or_quat_mul(x + 3, e, tmp + 3);
+  else or_quat_mul(e, x + 3, tmp + 3);
   memcpy(o, tmp, sizeof(tmp));
 }
 

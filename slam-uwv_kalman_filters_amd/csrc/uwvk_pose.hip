@@ -220,6 +220,7 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
   h->dof = dof;
   h->store = dof == 53 ? 54 : 27;
   h->device = device;
+  h->sh.so3_right = 1;  // MTK's SO3::boxplus, q exp(d): the default side since r05 (UWVK_OPT_SO3_RIGHT)
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     return UWVK_EDEVICE;

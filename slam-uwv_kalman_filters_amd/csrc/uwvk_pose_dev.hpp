@@ -42,7 +42,7 @@ struct PoseShared {
   int qlo[56], qoff[56], q_band;
   int q_bw;  // max band width below the diagonal over rows >= 9 (PSP keeps <= 2 in registers)
   int q_simple;  // PSP: lane-resident dt^2 Q suffices (see psp::LaneQ)
-  int so3_right;  // UWVK_OPT_SO3_RIGHT: body-frame SO3 [+]/[-] (literal kernels only; qplus_side)
+  int so3_right;  // UWVK_OPT_SO3_RIGHT: body-frame SO3 [+]/[-] (default 1; literal kernels: qplus_side, PSP: the SR instantiation)
   // run_log's per-log measurement covariances, read by the PSP epoch kernel
   // through the per-epoch constant-space pointer (scalar loads where used):
   // from the kernel arguments they were SGPRs live across the epoch loop,
@@ -234,7 +234,7 @@ UWVK_DEV void chol2_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, d
   }
 }
 
-// The same two-wave factor with up to UWVK_CHOL_GROUP columns per barrier
+// The same two-wave factor with up to kCholGroup columns per barrier
 // (columns J .. J+g-1 of one owner): the owner takes each pivot in turn from
 // its own lanes (readlane), scales the column and applies it to the group's
 // later columns (L[m][k] by readlane), then publishes the g columns; after the
@@ -244,12 +244,10 @@ UWVK_DEV void chol2_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, d
 // with 18 barriers instead of 53 at g = 3.  S counts barriers (the buffer set);
 // the 2 x g 64-double column buffers live in the factor region sm.Lp, which
 // takes the factor only after the last barrier (no buffer is read after it).
-#ifndef UWVK_CHOL_GROUP
-#define UWVK_CHOL_GROUP 3
-#endif
-#ifndef UWVK_CHOL_CYCLIC
-#define UWVK_CHOL_CYCLIC 0
-#endif
+// r05: kept form only; the look-ahead (2.51 against 2.42-2.44 ms per efforts
+// epoch, profiles/r04/effla/) and cyclic block forms and the one-wave factor
+// were measured and dropped (profiles/EXPERIMENTS.md).
+constexpr int kCholGroup = 3;
 template <int DOF, int J, int GS>
 constexpr int chol_group() {  // columns J .. J+g-1 with one owner (the halves of the two waves)
   constexpr int H = (DOF + 1) / 2;
@@ -262,10 +260,10 @@ UWVK_DEV void chol2g_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, 
   if constexpr (J < DOF) {
     constexpr int H = (DOF + 1) / 2;
     constexpr bool own = (J < H) == (W == 0);
-    constexpr int g = chol_group<DOF, J, UWVK_CHOL_GROUP>();
-    constexpr int b0 = (S & 1) * UWVK_CHOL_GROUP;
+    constexpr int g = chol_group<DOF, J, kCholGroup>();
+    constexpr int b0 = (S & 1) * kCholGroup;
     constexpr int JN = J + g;  // first column after this step
-    static_assert(Geo<DOF>::LPSZ >= 2 * UWVK_CHOL_GROUP * 64, "column buffers in the factor region");
+    static_assert(Geo<DOF>::LPSZ >= 2 * kCholGroup * 64, "column buffers in the factor region");
     double* buf = sm.Lp + b0 * 64;
     if constexpr (own) {
       constexpr int jj = J - C0;
@@ -304,175 +302,6 @@ UWVK_DEV void chol2g_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, 
   }
 }
 
-// Look-ahead form of chol2g_step (UWVK_CHOL_LA): after a group's barrier the
-// owner of the NEXT group first applies this group's columns to the next
-// group's columns only, takes the next group's pivots and publishes them, and
-// only then applies this group's columns to the rest of its own columns.  The
-// serial pivot chain (readlane -> rsqrt -> scale) and the independent trailing
-// update are then in one barrier interval, where the wave's instruction stream
-// interleaves them, instead of the chain starting after the whole update.
-// Each entry still sees the same fused multiply-adds in the same order (this
-// group's columns in order, then the next group's), so the factor is bitwise
-// chol2g_step's.  PRE: this group's pivots were taken in the previous step.
-#ifndef UWVK_CHOL_LA
-#define UWVK_CHOL_LA 0  // r04 A/B: bitwise equal, 2.51 against 2.42-2.44 ms per efforts epoch (profiles/r04/effla/), not kept
-#endif
-template <int DOF, int C0, int C1, int J, int g>
-UWVK_DEV void chol_group_pivots(double (&a)[C1 - C0], double* buf, int r, bool& ok, double piv) {
-  constexpr int jj = J - C0;
-#pragma unroll
-  for (int k = 0; k < g; k++) {
-    const double p = k == 0 ? piv : readlane_d(a[jj + k], J + k);
-    ok = ok && (p > 0.0);
-    const double inv = rsqrt_f64(p);
-    const double d = p * inv;
-    a[jj + k] = (r == J + k) ? d : a[jj + k] * inv;
-    buf[k * 64 + r] = a[jj + k];
-#pragma unroll
-    for (int m = k + 1; m < g; m++) {
-      const double lmk = readlane_d(a[jj + k], J + m);  // L[J+m][J+k]
-      a[jj + m] -= a[jj + k] * lmk;
-      asm volatile("" : "+v"(a[jj + m]));
-    }
-  }
-}
-template <int DOF, int W, int C0, int C1, int J, int S, bool PRE>
-UWVK_DEV void chol2la_step(double (&a)[C1 - C0], Smem<DOF>& sm, int r, bool& ok, double piv) {
-  if constexpr (J < DOF) {
-    constexpr int H = (DOF + 1) / 2;
-    constexpr bool own = (J < H) == (W == 0);
-    constexpr int g = chol_group<DOF, J, UWVK_CHOL_GROUP>();
-    constexpr int JN = J + g;
-    static_assert(Geo<DOF>::LPSZ >= 2 * UWVK_CHOL_GROUP * 64, "column buffers in the factor region");
-    double* buf = sm.Lp + (S & 1) * UWVK_CHOL_GROUP * 64;
-    if constexpr (own && !PRE) chol_group_pivots<DOF, C0, C1, J, g>(a, buf, r, ok, piv);
-    __syncthreads();
-    constexpr int cs = JN > C0 ? JN : C0;
-    constexpr bool ownN = JN < DOF && ((JN < H) == (W == 0));
-    constexpr int gN = JN < DOF ? chol_group<DOF, JN, UWVK_CHOL_GROUP>() : 0;
-    constexpr bool la = ownN && cs == JN && JN + gN <= C1;
-    // L[r][J + k]: the owner's own register, the others' the published column
-    double lk[g];
-#pragma unroll
-    for (int k = 0; k < g; k++)
-      lk[k] = own ? a[(J + k - C0) >= 0 && (J + k - C0) < (C1 - C0) ? J + k - C0 : 0] : buf[k * 64 + r];
-    if constexpr (la) {
-      constexpr int e1 = JN + gN;
-#pragma unroll
-      for (int k = 0; k < g; k++)
-#pragma unroll
-        for (int c = JN; c < e1; c++) a[c - C0] -= lk[k] * buf[k * 64 + c];
-#pragma unroll
-      for (int c = JN; c < e1; c++) asm volatile("" : "+v"(a[c - C0]));
-      double* bufN = sm.Lp + ((S + 1) & 1) * UWVK_CHOL_GROUP * 64;
-      chol_group_pivots<DOF, C0, C1, JN, gN>(a, bufN, r, ok, readlane_d(a[JN - C0], JN));
-      if constexpr (e1 < C1) {
-#pragma unroll
-        for (int k = 0; k < g; k++)
-#pragma unroll
-          for (int c = e1; c < C1; c++) a[c - C0] -= lk[k] * buf[k * 64 + c];
-#pragma unroll
-        for (int c = e1; c < C1; c++) asm volatile("" : "+v"(a[c - C0]));
-      }
-      chol2la_step<DOF, W, C0, C1, JN, S + 1, true>(a, sm, r, ok, 0.0);
-    } else {
-      if constexpr (cs < C1) {
-#pragma unroll
-        for (int k = 0; k < g; k++)
-#pragma unroll
-          for (int c = cs; c < C1; c++) a[c - C0] -= lk[k] * buf[k * 64 + c];
-#pragma unroll
-        for (int c = cs; c < C1; c++) asm volatile("" : "+v"(a[c - C0]));
-      }
-      double pnext = 0.0;
-      if constexpr (JN < DOF && JN >= C0 && JN < C1) pnext = readlane_d(a[JN - C0], JN);
-      chol2la_step<DOF, W, C0, C1, JN, S + 1, false>(a, sm, r, ok, pnext);
-    }
-  }
-}
-
-// Cyclic form (UWVK_CHOL_CYCLIC): column blocks [tG, tG + G) alternate between
-// the two waves (block t to wave t & 1) instead of one half per wave, so that
-// both waves keep later columns to update until the end of the factorisation
-// (with halves, wave 0 only waits at the barriers of the second half while wave
-// 1 runs every column chain and every update alone).  Per entry the same fused
-// multiply-adds in the same order: the factor is bitwise chol2g_step's for
-// G = UWVK_CHOL_GROUP (its groups are the blocks, 27 being a multiple of 3).
-template <int DOF, int W, int G>
-struct CholCyc {
-  __host__ __device__ static constexpr bool own(int c) { return ((c / G) & 1) == W; }
-  __host__ __device__ static constexpr int lc(int c) { return (c / (2 * G)) * G + c % G; }  // local slot of an own column
-  __host__ __device__ static constexpr int n() {
-    int k = 0;
-    for (int c = 0; c < DOF; c++) k += own(c) ? 1 : 0;
-    return k;
-  }
-};
-template <int DOF, int W, int G, int J, int S, int NC>
-UWVK_DEV void chol2c_step(double (&a)[NC], Smem<DOF>& sm, int r, bool& ok, double piv) {
-  if constexpr (J < DOF) {
-    using CC = CholCyc<DOF, W, G>;
-    constexpr bool own = CC::own(J);
-    constexpr int g = (DOF - J) < G ? (DOF - J) : G;
-    constexpr int JN = J + g;
-    constexpr int b0 = (S & 1) * G;
-    static_assert(Geo<DOF>::LPSZ >= 2 * G * 64, "column buffers in the factor region");
-    double* buf = sm.Lp + b0 * 64;
-    if constexpr (own) {
-#pragma unroll
-      for (int k = 0; k < g; k++) {
-        const double p = k == 0 ? piv : readlane_d(a[CC::lc(J + k)], J + k);
-        ok = ok && (p > 0.0);
-        const double inv = rsqrt_f64(p);
-        const double d = p * inv;
-        a[CC::lc(J + k)] = (r == J + k) ? d : a[CC::lc(J + k)] * inv;
-        buf[k * 64 + r] = a[CC::lc(J + k)];
-#pragma unroll
-        for (int m = k + 1; m < g; m++) {
-          const double lmk = readlane_d(a[CC::lc(J + k)], J + m);  // L[J+m][J+k]
-          a[CC::lc(J + m)] -= a[CC::lc(J + k)] * lmk;
-          asm volatile("" : "+v"(a[CC::lc(J + m)]));
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < g; k++) {
-      const double lk = own ? a[CC::lc(own ? J + k : 0)] : buf[k * 64 + r];
-#pragma unroll
-      for (int c = JN; c < DOF; c++)
-        if (CC::own(c)) a[CC::lc(c)] -= lk * buf[k * 64 + c];
-    }
-#pragma unroll
-    for (int c = JN; c < DOF; c++)
-      if (CC::own(c)) asm volatile("" : "+v"(a[CC::lc(c)]));
-    double pnext = 0.0;
-    if constexpr (JN < DOF && CC::own(JN)) pnext = readlane_d(a[CC::lc(JN)], JN);
-    chol2c_step<DOF, W, G, JN, S + 1, NC>(a, sm, r, ok, pnext);
-  }
-}
-template <int DOF, int W>
-UWVK_DEV void chol2c_wave(Smem<DOF>& sm) {
-  constexpr int G = UWVK_CHOL_GROUP;
-  using CC = CholCyc<DOF, W, G>;
-  const int r = lane_id();
-  const int rr = r < DOF ? r : DOF - 1;  // lanes >= DOF shadow the last row (discarded)
-  constexpr int NC = CC::n();
-  double a[NC];
-#pragma unroll
-  for (int c = 0; c < DOF; c++)
-    if (CC::own(c)) a[CC::lc(c)] = sm.S[rr * DOF + c];
-  bool ok = true;
-  chol2c_step<DOF, W, G, 0, 0, NC>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
-  if (r < DOF) {
-    const int base = r * (r + 1) / 2;
-#pragma unroll
-    for (int c = 0; c < DOF; c++)
-      if (CC::own(c) && c <= r) sm.Lp[base + c] = a[CC::lc(c)];
-  }
-  if (r == 0) sm.vec[62 + W] = ok ? 1.0 : 0.0;
-}
-
 template <int DOF, int W, int C0, int C1>
 UWVK_DEV void chol2_wave(Smem<DOF>& sm) {
   const int r = lane_id();
@@ -481,13 +310,7 @@ UWVK_DEV void chol2_wave(Smem<DOF>& sm) {
 #pragma unroll
   for (int c = C0; c < C1; c++) a[c - C0] = sm.S[rr * DOF + c];
   bool ok = true;
-#if UWVK_CHOL_GROUP > 1 && UWVK_CHOL_LA
-  chol2la_step<DOF, W, C0, C1, 0, 0, false>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
-#elif UWVK_CHOL_GROUP > 1
   chol2g_step<DOF, W, C0, C1, 0, 0>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
-#else
-  chol2_step<DOF, W, C0, C1, 0>(a, sm, r, ok, W == 0 ? readlane_d(a[0], 0) : 0.0);
-#endif
   if (r < DOF) {
     const int base = r * (r + 1) / 2;
 #pragma unroll
@@ -497,24 +320,14 @@ UWVK_DEV void chol2_wave(Smem<DOF>& sm) {
   if (r == 0) sm.vec[62 + W] = ok ? 1.0 : 0.0;
 }
 
-#ifndef UWVK_CHOL_ONEWAVE  // A/B: the 53-DOF factor on wave 0 alone (chol_step, no workgroup barrier per column)
-#define UWVK_CHOL_ONEWAVE 0
-#endif
 template <int DOF>
 UWVK_DEV bool chol_lds(Smem<DOF>& sm) {
-  if constexpr (Geo<DOF>::NW == 2 && !UWVK_CHOL_ONEWAVE) {
-#if UWVK_CHOL_CYCLIC
-    if (wid() == 0)
-      chol2c_wave<DOF, 0>(sm);
-    else
-      chol2c_wave<DOF, 1>(sm);
-#else
+  if constexpr (Geo<DOF>::NW == 2) {
     constexpr int H = (DOF + 1) / 2;
     if (wid() == 0)
       chol2_wave<DOF, 0, 0, H>(sm);
     else
       chol2_wave<DOF, 1, H, DOF>(sm);
-#endif
     __syncthreads();
     const bool ok = sm.vec[62] != 0.0 && sm.vec[63] != 0.0;
     __syncthreads();

@@ -35,67 +35,16 @@
 // Execution: one wavefront (64 lanes) per filter instance, Sigma packed
 // (lower triangle, row i at i(i+1)/2) in LDS for the whole multi-epoch run.
 #pragma once
+#include <cstddef>
+
 #include "uwvk_pose_dev.hpp"
 
-// performance variants (A/B builds: make variant V=... VFLAGS=-D...)
-#ifndef PSP_RB
-#define PSP_RB 8          // rows per block of the row-block sweeps
-#endif
-#ifndef PSP_DELTA_LDS  // r03: the predict's Delta_j broadcast through LDS (one j at a time) instead of v_readlane
-#define PSP_DELTA_LDS 1
-#endif
-#ifndef PSP_UPD_LDS  // r03: the update's P and Dz broadcast through LDS instead of v_readlane
-#define PSP_UPD_LDS 1
-#endif
-#ifndef PSP_RANKM_MFMA  // r03: the update's rank-M pass on v_mfma_f64_16x16x4_f64 tiles: 1 rankm_mfma (16-aligned
-#define PSP_RANKM_MFMA 2      // frame), 2 rankm_mfma_o (frame shifted by DOF % 16, row-block MFMAs back to back),
-                              // 3 rankm_mfma_all (all tiles in flight).  DELTA_LDS + UPD_LDS + 1: A/B 79.6 -> 73.4 ms
-                              // per 200-epoch launch (profiles/r03/ab1); 2: 73.5-73.9 -> 72.5 (ab2), 3: 72.7-73.0
-#endif
-#ifndef PSP_PAIR_MASK  // r03: rankm_pairs' half selection by lane-mask arithmetic (no exec branches)
-#define PSP_PAIR_MASK 1
-#endif
-#ifndef PSP_RBP
-#define PSP_RBP 6         // row pairs per block of the paired rank-M sweep (rankm_pairs); 8 -> 6: 167 -> 150 VGPRs, A/B +0.3%
-#endif
-// ablation knobs for timing analysis only (results are invalid when set):
-// PSP_ABL = bitmask: 1 mean 1 iteration, 2 no rank-m pass, 4 no L Delta / X,
-// 8 no predict Cholesky, 16 no predict points, 32 no update Cholesky, (r04)
-// 64 no A-coupled rows (pos / vel rows and columns), 128 no flat pass (the Q
-// band), 256 no apply_delta (tools/abl_pmc.sh: per-phase counter budgets)
-#ifndef PSP_ABL
-#define PSP_ABL 0
-#endif
-// instruction-count trims (A/B bitmask): 1 lane-limited wave sums, 2 manifold
-// mean without sqrt / division, 4 rank-m rows as one FMA chain, 8 reciprocal
-// by v_rcp_f64 + Newton in the small-angle SO3 log, 16 one product for the
-// Cholesky column incl. its diagonal, 32 v_rcp_f64 + Newton for 1/d, 64 the
-// Cholesky panel read with immediate offsets from the row start, 256 the
-// update's z-bar and S sums as one LDS-transposed round (lds_sums), 512 the
-// same for the predict's ori x ori sums, 2048 (r02) the rank-M pass over the
-// short rows 0..31 two rows per instruction (rankm_pairs: 88.4 -> 86.0 ms,
-// 148.0 -> 152.1M steps/s), 4096 (r02) a fresh laundered lane id per phase
-// (PSP_PHASE: 85.8 -> 85.4 ms).
-// Measured on the C3 bench (kernel ms per 200-epoch launch): none 103.2,
-// 1-8 97.5, +16 95.4, +32 within noise, +64 94.3, +256/512 92.0.  Rejected:
-// Delta_j as LDS broadcasts instead of v_readlane (105.9), the same for Dz / P
-// (no change), lds_sums in the manifold-mean loop (+0.7%), s_setprio around
-// the Cholesky column chain (within noise).
-#ifndef PSP_NT_TAN  // r03: A_ll from a per-lane constant set once per launch (ProcCtx::nt_tan), not 8 selects per use
-#define PSP_NT_TAN 1
-#endif
-#ifndef PSP_DIAG_SEL  // per-lane decay factors and water-velocity noise by uniform selects (r02)
-#define PSP_DIAG_SEL 1
-#endif
-#ifndef PSP_FAST
-#define PSP_FAST 7039
-#endif
-// PSP_DIAG_HOT (tools/isa_hot.py only, results invalid): the cold fallbacks
-// (library SO3 exp/log and sincos, the general-Q branches, the periodic fold)
-// compiled out, so that the static code of the epoch loop is the C3 hot path
-#ifndef PSP_DIAG_HOT
-#define PSP_DIAG_HOT 0
-#endif
+// r05: the compile-time A/B knobs of rounds 1-4 (PSP_*: lane-limited wave
+// sums, LDS broadcasts, the three rank-M MFMA forms, lane masks, SGPR series
+// constants, ...) are resolved to the measured winners; the ablation and
+// hot-path-only diagnostics are gone from the product source.  The rejected
+// arms, their measurements and the last commit that still builds them are
+// listed in profiles/EXPERIMENTS.md ("r05: knob pruning").
 
 namespace uwvk {
 namespace psp {
@@ -122,6 +71,24 @@ struct alignas(16) PspSmem {
   // lane registers or uniform SGPRs
 };
 static_assert(sizeof(PspSmem<53>) <= 12800, "12 instances per CU");
+// S, mu and stg are contiguous: every-lane loads that run past one member (the
+// epilogue's slot loop, the mean's lanes >= store) land in the next one and are
+// never stored.  Such reads go through flat(), a view of the whole PspSmem as
+// one double array, not through an out-of-range index of a member array.
+static_assert(offsetof(PspSmem<53>, mu) == sizeof(double) * PG<53>::NP, "mu follows S");
+static_assert(offsetof(PspSmem<53>, stg) == sizeof(double) * (PG<53>::NP + Lay<53>::store), "stg follows mu");
+static_assert(offsetof(PspSmem<26>, mu) == sizeof(double) * PG<26>::NP, "mu follows S");
+static_assert(offsetof(PspSmem<26>, stg) == sizeof(double) * (PG<26>::NP + Lay<26>::store), "stg follows mu");
+template <int DOF>
+UWVK_DEV double* flat(PspSmem<DOF>& sm) {
+  return reinterpret_cast<double*>(&sm);
+}
+template <int DOF>
+UWVK_DEV const double* flat(const PspSmem<DOF>& sm) {
+  return reinterpret_cast<const double*>(&sm);
+}
+template <int DOF>
+constexpr int kFlatMu = PG<DOF>::NP;  // mu's offset in flat()
 
 // pidx / unpack: uwvk_dev.hpp (the HBM layout is the same packed triangle)
 
@@ -134,15 +101,12 @@ UWVK_DEV int olane() {
   return l;  // (restoring the range with l & 63 measured 1% slower)
 }
 
-// (r04) PSP_LMASK: a condition on the lane id alone as a compile-time lane
+// (r04) A condition on the lane id alone as a compile-time lane
 // mask (one wave per instance: lane l is bit l of EXEC).  LANE_IF(l, expr)
 // folds expr over the 64 lanes into a constant and hands it to
 // inverse_ballot: an s_mov of the mask into an SGPR pair, instead of a v_cmp
 // (plus the integer arithmetic on the laundered lane id) per use.  Every PSP
 // kernel is one 64-lane wave per workgroup (__launch_bounds__(64)).
-#ifndef PSP_LMASK
-#define PSP_LMASK 255  // bit set over the site groups (LMG, set per region below)
-#endif
 template <class F>
 UWVK_DEV constexpr unsigned long long lane_mask(F f) {
   unsigned long long m = 0;
@@ -169,17 +133,13 @@ UWVK_DEV bool lane_const() {
   if constexpr (mask_needs_split(M)) return lane_in_split(M);
   else return __builtin_amdgcn_inverse_ballot_w64(M);
 }
-#define LMG 0
-#define LANE_IF(l, expr)                                                                                       \
-  ((PSP_LMASK & LMG) ? ({                                                                                      \
-    constexpr unsigned long long m_ = ::uwvk::psp::lane_mask([](int l) constexpr { return (bool)(expr); });   \
-    ::uwvk::psp::lane_const<m_>();                                                                             \
-  })                                                                                                           \
-                     : (bool)(expr))
-#define LANE_IN(m)                                                                                         \
-  ((PSP_LMASK & LMG) ? (::uwvk::psp::mask_needs_split(m) ? ::uwvk::psp::lane_in_split(m)                     \
-                                                         : __builtin_amdgcn_inverse_ballot_w64(m))             \
-                     : ((((m) >> (olane() & 63)) & 1ull) != 0))
+#define LANE_IF(l, expr)                                                                                     \
+  ({                                                                                                         \
+    constexpr unsigned long long m_ = ::uwvk::psp::lane_mask([](int l) constexpr { return (bool)(expr); }); \
+    ::uwvk::psp::lane_const<m_>();                                                                           \
+  })
+#define LANE_IN(m) \
+  (::uwvk::psp::mask_needs_split(m) ? ::uwvk::psp::lane_in_split(m) : __builtin_amdgcn_inverse_ballot_w64(m))
 // lanes whose column j >= p, with j the lane clamped to the last DOF (jl) or its
 // A-coupled column (jcc: pos -> vel, vel -> acc, else jl), for pidx_sel_b
 UWVK_DEV constexpr int couple_c(int d) { return d < 3 ? d + 6 : (d >= 6 && d < 9 ? d + 3 : -1); }
@@ -231,13 +191,9 @@ UWVK_DEV double wave_sum_dpp(double v) {
   s = s + dpp_d<0x113, 0xf, 0xf>(v);          // row_shr:3
   s = s + dpp_d<0x114, 0xf, 0xe>(s);          // row_shr:4, banks 1-3
   s = s + dpp_d<0x118, 0xf, 0xc>(s);          // row_shr:8, banks 2-3
-#if PSP_FAST & 1
   if constexpr (NL <= 16) return readlane_d(s, 15);
-#endif
   s = s + dpp_d<0x142, 0xa, 0xf>(s);          // row_bcast:15, rows 1,3
-#if PSP_FAST & 1
   if constexpr (NL <= 32) return readlane_d(s, 31);
-#endif
   s = s + dpp_d<0x143, 0xc, 0xf>(s);          // row_bcast:31, rows 2,3
   return readlane_d(s, 63);
 }
@@ -251,13 +207,8 @@ UWVK_DEV double wave_sum_dpp(double v) {
 // Without it every coefficient was rebuilt in a VGPR pair by two v_mov_b32 per
 // use (~150 VALU per instance-epoch, on the kernel's bound unit); an empty asm
 // pins the value to an SGPR pair, made by two s_mov_b32 on the scalar unit.
-#ifndef PSP_SCONST
-#define PSP_SCONST 1
-#endif
 UWVK_DEV double sk(double c) {
-#if PSP_SCONST
   asm volatile("" : "+s"(c));
-#endif
   return c;
 }
 UWVK_DEV void so3_exp_psp(const double v[3], double o[4]) {
@@ -281,8 +232,7 @@ UWVK_DEV void so3_exp_psp(const double v[3], double o[4]) {
     c = fma(c, u, 1.0);
     o[0] = c; o[1] = s * v[0]; o[2] = s * v[1]; o[3] = s * v[2];
   } else {
-    if (PSP_DIAG_HOT) o[0] = 1.0, o[1] = o[2] = o[3] = 0.0;
-    else so3_exp(v, o);
+    so3_exp(v, o);
   }
 }
 UWVK_DEV void so3_log_psp(const double q[4], double o[3]) {
@@ -290,13 +240,9 @@ UWVK_DEV void so3_log_psp(const double q[4], double o[3]) {
   if (w < 0) { w = -w; x = -x; y = -y; z = -z; }
   const double n2 = x * x + y * y + z * z, w2 = w * w;
   if (n2 < 0.0025 * w2) {  // r = |v|/w < 0.05 (rotation < 0.1 rad)
-#if PSP_FAST & 8
     double iw = __builtin_amdgcn_rcp(w);  // w in (0.99, 1]: two Newton steps -> correctly rounded to ~1 ulp
     iw = fma(iw, fma(-w, iw, 1.0), iw);
     iw = fma(iw, fma(-w, iw, 1.0), iw);
-#else
-    const double iw = 1.0 / w;
-#endif
     const double r2 = n2 * (iw * iw);
     // atan(r)/r = sum (-r^2)^k / (2k+1), k <= 6 (k = 7: < 5e-20 for r^2 < 0.0025)
     double a = r2 * sk(-1.0 / 13.0);
@@ -309,8 +255,7 @@ UWVK_DEV void so3_log_psp(const double q[4], double o[3]) {
     const double k = 2.0 * a * iw;  // 2 atan2(|v|, w) / |v|
     o[0] = k * x; o[1] = k * y; o[2] = k * z;
   } else {
-    if (PSP_DIAG_HOT) o[0] = o[1] = o[2] = 0.0;
-    else so3_log(q, o);
+    so3_log(q, o);
   }
 }
 // SO3 [+] / [-] of side SR (a template parameter of every PSP kernel, DESIGN.md
@@ -343,7 +288,7 @@ UWVK_DEV double sel6(double v0, double v1, double v2, double v3, double v4, doub
 
 // pidx(p, j) for a compile-time p and lane-varying j, given Tj = j (j + 1) / 2
 UWVK_DEV int pidx_sel(int p, int j, int Tj) { return j >= p ? Tj + p : p * (p + 1) / 2 + j; }
-// the same with the branch given (a lane mask, PSP_LMASK)
+// the same with the branch given (a lane mask)
 UWVK_DEV int pidx_sel_b(int p, int j, int Tj, bool ge) { return ge ? Tj + p : p * (p + 1) / 2 + j; }
 
 UWVK_DEV void wsync() {  // LDS ordering point between the lanes of one wave
@@ -380,15 +325,11 @@ UWVK_DEV void lds_sums(const double (&v)[R], double* buf, int l, double (&out)[R
 // fresh laundered lane id, so that lane masks are recomputed per phase (one
 // v_cmp each) instead of being kept as SGPR pairs across the epoch, where they
 // were spilled to VGPR lanes and reloaded (two v_readlane each) in every phase
-#if PSP_FAST & 4096
 #define PSP_PHASE(ph) \
   do {                \
     UWVK_STAMP(ph);   \
     l = olane();      \
   } while (0)
-#else
-#define PSP_PHASE(ph) UWVK_STAMP(ph)
-#endif
 
 UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -406,30 +347,6 @@ UWVK_DEV void psync() {  // LDS ordering point for the single wave of the block
 // acceleration and gravity keep d = 1.
 UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 
-#ifndef PSP_PIDX_SEL  // r03: packed indices of the predict's rows < 12 by pidx_sel
-#define PSP_PIDX_SEL 1
-#endif
-#ifndef PSP_CHOL_RL1  // r04 A/B: the partial Cholesky's next-column entry by readlane instead of LDS
-#define PSP_CHOL_RL1 0
-#endif
-#ifndef PSP_BAND_PRE  // r04: the Q band's three entries loaded before the masked stores (no waits in branches)
-#define PSP_BAND_PRE 1
-#endif
-#ifndef PSP_CPL_FMA  // r04: the predict's A-coupled rows read the coupled column unconditionally (FMA with 0 / dt)
-#define PSP_CPL_FMA 1
-#endif
-#ifndef PSP_QDIAG  // r04: the lane-resident Q's pos / vel diagonal added per lane (rows_lt9), not selected per row
-#define PSP_QDIAG 1
-#endif
-#ifndef PSP_ROWS_SEL  // r03 A/B: the predict's rows < 9 and Q-band stores branch-free (throw-away slots)
-#define PSP_ROWS_SEL 0
-#endif
-#ifndef PSP_COL_SEL  // r03: the Cholesky column broadcast stored branch-free (pchol_step_lds); r04: 2 unconditional
-#define PSP_COL_SEL 2
-#endif
-#ifndef PSP_STAGE_LATE  // r03: the L_a rows staged after the last column step (pchol)
-#define PSP_STAGE_LATE 1
-#endif
 // r04: broadcast reads from the staging area 16-byte aligned, so that pairs of
 // doubles are one ds_read_b128 (4 LDS-array cycles, one address) instead of a
 // ds_read2_b64 (8 cycles) with a per-pair address.  sm.stg starts 8 bytes past a
@@ -437,12 +354,6 @@ UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 // The Cholesky column of step J is shifted by one slot when J + 1 is even; the
 // predict's Delta_j and the update's P / Dz rows are padded to 4 per j.
 // (LDS-array cycles per instance-epoch: 1,987 measured before, r04b lds pass.)
-#ifndef PSP_LDS_ALIGN
-#define PSP_LDS_ALIGN 1
-#endif
-#ifndef PSP_PIV_EARLY
-#define PSP_PIV_EARLY 0  // r03: fewer VALU (-56 per epoch) but 176 VGPRs (2 waves per SIMD), not kept
-#endif
 // column J broadcast through an LDS column (no readlanes); the rows the
 // sigma-point lanes need (RL::rows) are staged in the same step: lane r with
 // q = row_pos(r) writes L[r][J] to rows[q*K + J] (one write per column).
@@ -453,39 +364,21 @@ UWVK_DEV constexpr bool scaled_dof(int d) { return d >= 12 && d != 18; }
 // v_readlane per column step, tools/spill_report.py).  The sign test rides on
 // the rsqrt: rsqrt of a pivot <= 0 or NaN is NaN or +-inf, so chk += inv * 0
 // is NaN exactly when some pivot failed piv > 0 (pchol tests chk once).
-#undef LMG
-#define LMG 1
 template <int K, int J>
 UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, double* rows, int q, double piv,
                              double inv_in, double& chk) {
   if constexpr (J < K) {
-#if PSP_PIV_EARLY && (PSP_FAST & 16)
-    const double inv = inv_in;  // sign of piv already folded into ok
-#else
     ok = ok && (piv > 0.0);
     const double inv = rsqrt_f64(piv);
-#endif
-#if PSP_FAST & 16
     // lane J's own a[J] is the pivot (the look-ahead below evaluates the same
     // fma as the column update), so one product serves the diagonal too
     a[J] = LANE_IF(r, r >= J) ? a[J] * inv : 0.0;
-#else
-    a[J] = LANE_IF(r, r == J) ? piv * inv : (LANE_IF(r, r > J) ? a[J] * inv : 0.0);
-#endif
     // look-ahead: the next pivot is lane J+1's a[J+1] - L[J+1][J]^2 (its own
     // registers), so its rsqrt need not wait for the column broadcast
     double pnext = 0.0, invn = 0.0;
     if constexpr (J + 1 < K) {
       pnext = readlane_d(a[J + 1] - a[J] * a[J], J + 1);
-#if PSP_PIV_EARLY && (PSP_FAST & 16)
-      invn = rsqrt_f64(pnext);
-      asm volatile("" : "+v"(invn));  // here, not sunk to its use behind the column update
-      chk = fma(invn, 0.0, chk);
-#endif
     }
-#if !PSP_STAGE_LATE
-    if (q >= 0) rows[q * K + J] = a[J];
-#endif
     if constexpr (J + 1 < K) {
       // col aliases the LAST staged row's not-yet-written slots J+1 .. K-1:
       // only L[c][J] for c > J is read, and that row's own L[.][c] lands in
@@ -494,9 +387,8 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
       // that the reads start on a 16-byte boundary; col is odd-aligned)
       // (PSP_CHOL_RL1: the next column's entry L[J+1][J] by readlane, the
       // LDS reads start at J + 2 and are aligned from there)
-      constexpr int C0 = PSP_CHOL_RL1 ? J + 2 : J + 1;
-      double* const cj = col + ((PSP_LDS_ALIGN && PSP_STAGE_LATE && (C0 & 1) == 0) ? 1 : 0);
-#if PSP_STAGE_LATE && PSP_COL_SEL == 2
+      constexpr int C0 = J + 1;
+      double* const cj = col + (((C0 & 1) == 0) ? 1 : 0);
       // r04: every lane stores its a[J] to slot r: the slots read this step
       // are (J, K), which only the lanes r in (J, K) write; the others land in
       // slots that are not read now and that nothing else holds while the
@@ -505,21 +397,6 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
       // instead of a select per step (4 VALU)
       static_assert(64 + 1 <= 115, "column slots (PG::STG)");
       cj[r & 63] = a[J];
-#elif PSP_STAGE_LATE && PSP_COL_SEL
-      // lanes outside (J, K) store to their own throw-away slot past the column
-      // (the rows area is written only after the last step): no exec-masked branch
-      static_assert(K + 65 <= 115, "throw-away slots (PG::STG)");
-      cj[LANE_IF(r, r > J && r < K) ? r : K + (r & 63)] = a[J];
-#else
-      if (LANE_IF(r, r > J && r < K)) cj[r] = a[J];
-#endif
-#if PSP_CHOL_RL1
-      // (r04) L[J+1][J], the one entry the next step's scale waits for, as a
-      // readlane of lane J + 1 (two SGPR reads, no LDS round trip on the
-      // step-to-step chain); the rest of the column through LDS as before
-      const double cn = readlane_d(a[J], J + 1);
-      a[J + 1] -= a[J] * cn;
-#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -541,17 +418,12 @@ constexpr int STG_ROWS = 0;
 template <int DOF, int K, class RL>
 UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* stg) {
   const int rr = r < DOF ? r : DOF - 1;
-#if PSP_FAST & 64
   // row rr from its packed start with immediate offsets: for c > rr this reads
   // a later (finite) entry of Sigma~, which the column steps never use (they
   // zero L[r][c] for r < c before it is read)
   const double* Sr = S + rr * (rr + 1) / 2;
 #pragma unroll
   for (int c = 0; c < K; c++) a[c] = Sr[c] * (scaled_dof(c) ? dl * readlane_d(dl, c) : dl);
-#else
-#pragma unroll
-  for (int c = 0; c < K; c++) a[c] = S[pidx(rr, c)] * (scaled_dof(c) ? dl * readlane_d(dl, c) : dl);
-#endif
   bool ok = true;
   int q = -1;
 #pragma unroll
@@ -560,7 +432,6 @@ UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* s
   const double p0 = readlane_d(a[0], 0);
   const double inv0 = rsqrt_f64(p0);
   double chk = fma(inv0, 0.0, 0.0);
-#if PSP_STAGE_LATE
   // the column buffer anywhere in the (not yet written) rows area; the rows are
   // staged after the last step, one lane-addressed run of K stores per row
   // lane, instead of one masked store (and its address product) per step
@@ -570,12 +441,6 @@ UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* s
 #pragma unroll
     for (int J = 0; J < K; J++) rp[J] = a[J];
   }
-#else
-  pchol_step_lds<K, 0>(a, r, ok, stg + STG_ROWS + (RL::NR - 1) * K, stg + STG_ROWS, q, p0, inv0, chk);
-#endif
-#if PSP_PIV_EARLY && (PSP_FAST & 16)
-  ok = chk == 0.0;
-#endif
   psync();  // the staged rows are read by the point lanes next
   return ok;
 }
@@ -610,8 +475,6 @@ UWVK_DEV constexpr bool has_rot() {
     if (RL::rows[q] >= 3 && RL::rows[q] < 6) return true;
   return false;
 }
-#undef LMG
-#define LMG 2
 template <class RL, int DOF, int K, int SR>
 UWVK_DEV void gen_rows(const double* mu, const double* stg, int p, double x[Lay<DOF>::store]) {
   using L = Lay<DOF>;
@@ -649,8 +512,7 @@ UWVK_DEV void proc_orientation(const double x[Lay<DOF>::store], const PoseShared
     sl = sh.slat0 * cd + sh.clat0 * sd;
     cl = sh.clat0 * cd - sh.slat0 * sd;
   } else {
-    if (PSP_DIAG_HOT) sl = cl = 0.0;
-    else sincos(sh.lat0 + dl, &sl, &cl);
+    sincos(sh.lat0 + dl, &sl, &cl);
   }
   const double er[3] = {kEarthW * cl, 0.0, kEarthW * sl};
   double wb[3], wn[3];
@@ -664,51 +526,6 @@ UWVK_DEV void proc_orientation(const double x[Lay<DOF>::store], const PoseShared
   qplus_psp<SR>(e, x + L::s_quat, o);  // new_state.orientation.boxplus (PoseUKF.cpp:32)
 }
 
-// storage component s (not orientation) of f(mu)
-template <int DOF>
-UWVK_DEV double proc_vect(int s, const double* mu, const PoseShared& sh, const ProcCtx& c) {
-  using L = Lay<DOF>;
-  const uwvk_pose_parameter& P = sh.p;
-  const double dt = c.dt, x = mu[s];
-  if (s < 3) return x + dt * mu[L::s_vel + s];
-  if (s >= L::s_vel && s < L::s_vel + 3) return x + dt * mu[L::s_acc + s - L::s_vel];
-  if (s >= L::s_bg && s < L::s_bg + 3) {
-    const double d = sh.ntau[0] * (x - P.gyro_bias_offset[s - L::s_bg]);
-    return x + dt * d;
-  }
-  if (s >= L::s_ba && s < L::s_ba + 3) {
-    const double d = sh.ntau[1] * (x - P.acc_bias_offset[s - L::s_ba]);
-    return x + dt * d;
-  }
-  if constexpr (L::has_params) {
-    if (s >= L::s_inertia && s < L::s_inertia + 9) {
-      const double d = sh.ntau[2] * (x - c.off_lane);
-      return x + dt * d;
-    }
-    if (s >= L::s_lin && s < L::s_lin + 9) {
-      const double d = sh.ntau[3] * (x - c.off_lane);
-      return x + dt * d;
-    }
-    if (s >= L::s_quad && s < L::s_quad + 9) {
-      const double d = sh.ntau[4] * (x - c.off_lane);
-      return x + dt * d;
-    }
-  }
-  if (s >= L::s_wv && s < L::s_wv + 4) {
-    const double d = sh.ntau[5] * x;
-    return x + dt * d;
-  }
-  if (s >= L::s_badcp && s < L::s_badcp + 2) {
-    const double d = sh.ntau[6] * x;
-    return x + dt * d;
-  }
-  if (s == L::s_rho) {
-    const double d = sh.ntau[7] * (x - c.off_lane);
-    return x + dt * d;
-  }
-  return x;  // acceleration, gravity
-}
-
 // the same, branch-free from the lane constants (psp::lane_proc, set once per
 // launch): x + dt * mu[vpart] | x + dt * (nt (x - off)) | x
 UWVK_DEV double proc_vect_lane(int s, const double* mu, const ProcCtx& c) {
@@ -718,22 +535,6 @@ UWVK_DEV double proc_vect_lane(int s, const double* mu, const ProcCtx& c) {
   return (c.vpart >= 0 || c.nt_lane != 0.0) ? x + c.dt * d : x;
 }
 
-// Jacobian of the affine rows of f: A = diag(ad) + dt * (pos <- vel, vel <- acc)
-template <int DOF>
-UWVK_DEV double proc_diag(int d, const PoseShared& sh, double dt) {
-  using L = Lay<DOF>;
-  if (d >= L::d_bg && d < L::d_bg + 3) return 1.0 + dt * sh.ntau[0];
-  if (d >= L::d_ba && d < L::d_ba + 3) return 1.0 + dt * sh.ntau[1];
-  if constexpr (L::has_params) {
-    if (d >= L::d_inertia && d < L::d_inertia + 9) return 1.0 + dt * sh.ntau[2];
-    if (d >= L::d_lin && d < L::d_lin + 9) return 1.0 + dt * sh.ntau[3];
-    if (d >= L::d_quad && d < L::d_quad + 9) return 1.0 + dt * sh.ntau[4];
-  }
-  if (d >= L::d_wv && d < L::d_wv + 4) return 1.0 + dt * sh.ntau[5];
-  if (d >= L::d_badcp && d < L::d_badcp + 2) return 1.0 + dt * sh.ntau[6];
-  if (d == L::d_rho) return 1.0 + dt * sh.ntau[7];
-  return 1.0;
-}
 // the same per lane from the eight uniform decay rates by selects: a runtime
 // index into sh.ntau was a per-lane global load whose s_waitcnt vmcnt(0) also
 // drained the next epoch's IMU prefetch on the predict's critical path
@@ -752,12 +553,6 @@ UWVK_DEV double tan_ntau_sel(int d, const PoseShared& sh) {
   nt = (d >= L::d_badcp && d < L::d_badcp + 2) ? sh.ntau[6] : nt;
   nt = (d == L::d_rho) ? sh.ntau[7] : nt;
   return nt;
-}
-template <int DOF>
-UWVK_DEV double proc_diag_sel(int d, const PoseShared& sh, double dt) {
-  const double nt = tan_ntau_sel<DOF>(d, sh);
-  const bool markov = scaled_dof(d) && d < DOF;
-  return markov ? 1.0 + dt * nt : 1.0;
 }
 // coupled column of row d (pos -> vel, vel -> acc) or -1
 UWVK_DEV constexpr int proc_couple(int d) { return d < 3 ? d + 6 : (d >= 6 && d < 9 ? d + 3 : -1); }
@@ -795,8 +590,6 @@ UWVK_DEV LaneQ lane_q(const double* fq, int l) {
 // (sh.q_simple: lane-resident band <= 2), 2 known general.  The epoch kernel is
 // instantiated for 1 and 2 and the host picks one: with both branches in one
 // kernel the epoch loop ran 0.7-0.8% slower (profiles/r03/qm/).
-#undef LMG
-#define LMG 4
 template <int DOF, int QM = 0, int SR = 0>
 UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q,
                           const double* fq, double& ds, double& ids, const LaneQ& lq,
@@ -832,12 +625,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   const double wv_add = sh.p.water_velocity_scale * (vs0 * vs0 + vs1 * vs1 + vs2 * vs2) * dt;
   // partial Cholesky and row staging
   double a[K];
-#if PSP_ABL & 8
-  bool ok = true;
-  for (int c = 0; c < K; c++) a[c] = sm.S[pidx(l < DOF ? l : DOF - 1, c)];
-#else
   const bool ok = pchol<DOF, K, PredRows>(sm.S, l, a, ds, sm.stg);
-#endif
   PSP_PHASE(20);
   // sigma points: lanes < 2K plus the centre lane 2K; orientation output only
   const bool pt = LANE_IF(l, l < 2 * K), ctr = LANE_IF(l, l == 2 * K);
@@ -845,11 +633,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   {
     double x[L::store];
     gen_rows<PredRows, DOF, K, SR>(sm.mu, sm.stg + STG_ROWS, l, x);
-#if PSP_ABL & 16
-    for (int i = 0; i < 4; i++) o[i] = x[3 + i];
-#else
     proc_orientation<DOF, SR>(x, sh, pc, o);
-#endif
   }
   PSP_PHASE(21);
   // manifold mean of the orientations (ukfom: ref = X_0, Gauss-Newton, |d| <= 1e-6)
@@ -867,11 +651,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       nrm = 0.0;
 #pragma unroll
       for (int i = 0; i < 3; i++) {
-#if PSP_FAST & 2
         d[i] = wave_sum_dpp<2 * K + 1>(w * d[i]) * (1.0 / (double)G::N);
-#else
-        d[i] = wave_sum_dpp<2 * K + 1>(w * d[i]) / (double)G::N;
-#endif
         nrm += d[i] * d[i];
       }
       double e[4], q[4];
@@ -879,12 +659,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       qplus_psp<SR>(e, mq, q);
 #pragma unroll
       for (int i = 0; i < 4; i++) mq[i] = q[i];
-#if PSP_FAST & 2
-    } while (!(PSP_ABL & 1) && nrm > 1e-12 && ++it < 10000);  // |delta| > 1e-6
-#else
-      nrm = sqrt(nrm);
-    } while (!(PSP_ABL & 1) && nrm > 1e-6 && ++it < 10000);
-#endif
+    } while (nrm > 1e-12 && ++it < 10000);  // |delta| > 1e-6
   }
   PSP_PHASE(22);
   // deviations; ori x ori block; Delta_j = d_{j+} - d_{j-}
@@ -893,7 +668,6 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   double oo[6];
   {
     const double w = pt ? 1.0 : (ctr ? wc : 0.0);
-#if PSP_FAST & 512
     // six sums over lanes 0..2K: pair sums by one DPP swap, then the 16 even
     // lanes' values transposed through LDS (stg is free after the points)
     double v[6];
@@ -909,13 +683,6 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     lds_sums<6, 16, 2>(v, sm.stg, l, oo);
 #pragma unroll
     for (int i = 0; i < 6; i++) oo[i] = 0.5 * oo[i];
-#else
-    int k = 0;
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int j = 0; j <= i; j++) oo[k++] = 0.5 * wave_sum_dpp<2 * K + 1>(w * d[i] * d[j]);
-#endif
   }
   // Delta_j = d_{j+} - d_{j-} lives in lane 2j; it is read back as a uniform
   // (SGPR) value below, no LDS staging
@@ -926,14 +693,13 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   double X[3];
   {
     double Y[3] = {0.0, 0.0, 0.0};
-#if PSP_DELTA_LDS
     // Delta_j staged in stg (free after the ori x ori sums) by lane 2j and read
     // back by every lane as a broadcast, one j at a time (a compiler memory
     // barrier per j keeps at most two j's loads in flight: hoisted all at once
     // they took 90 VGPRs); 45 LDS reads instead of 90 v_readlane
     // (PSP_LDS_ALIGN: 4 slots per j from slot 1, so each j's first pair is one
     // aligned ds_read_b128)
-    constexpr int DS = PSP_LDS_ALIGN ? 4 : 3, D0 = PSP_LDS_ALIGN ? 1 : 0;
+    constexpr int DS = 4, D0 = 1;
     static_assert(D0 + DS * K <= PG<DOF>::STG, "Delta (PG::STG)");
     if (LANE_IF(l, (l & 1) == 0 && l < 2 * K)) {
 #pragma unroll
@@ -944,7 +710,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #pragma unroll
     for (int i = 0; i < 3; i++) dn[i] = sm.stg[D0 + i];
 #pragma unroll
-    for (int j = 0; j < ((PSP_ABL & 4) ? 0 : K); j++) {
+    for (int j = 0; j < K; j++) {
       double dj[3] = {dn[0], dn[1], dn[2]};
       if (j + 1 < K) {
 #pragma unroll
@@ -956,21 +722,9 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       asm volatile("" : "+v"(Y[0]), "+v"(Y[1]), "+v"(Y[2])::"memory");
     }
     wsync();  // stg is rewritten by the next phase's users
-#else
-#pragma unroll
-    for (int j = 0; j < ((PSP_ABL & 4) ? 0 : K); j++)
-#pragma unroll
-      for (int i = 0; i < 3; i++) Y[i] += a[j] * readlane_d(dd[i], 2 * j);
-#endif
     const int cp = proc_couple(l);
     const int src = cp >= 0 ? cp : l;
-#if PSP_NT_TAN
     const double ar = 1.0 + dt * pc.nt_tan;  // proc_diag_sel's value (nt_tan = 0 off the scaled DOFs)
-#elif PSP_DIAG_SEL
-    const double ar = proc_diag_sel<DOF>(l, sh, dt);
-#else
-    const double ar = proc_diag<DOF>(l, sh, dt);
-#endif
 #pragma unroll
     for (int i = 0; i < 3; i++) {
       const double yc = shfl_d(Y[i], src);
@@ -984,15 +738,8 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   double nv[6];
   const int jl = l < DOF ? l : DOF - 1;
   const int jc = proc_couple(jl);
-#if PSP_NT_TAN
   const double aj = 1.0 + dt * pc.nt_tan;  // lanes >= DOF: 1 (their values are never stored)
-#elif PSP_DIAG_SEL
-  const double aj = proc_diag_sel<DOF>(jl, sh, dt);
-#else
-  const double aj = proc_diag<DOF>(jl, sh, dt);
-#endif
   const int Tl = (jl * (jl + 1)) >> 1;  // (unused without PSP_PIDX_SEL)
-#if PSP_PIDX_SEL
   // packed (p, j) for a compile-time row p < 12 and a lane column j as a select
   // between two sums (tri(j) once per lane): pidx's max / min / product per
   // access were 7 integer instructions; the coupled column is clamped so its
@@ -1000,7 +747,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   const int jcc = jc >= 0 ? jc : jl;
   const int Tc = (jcc * (jcc + 1)) >> 1;
   [[maybe_unused]] const double cf = LANE_IF(l, proc_couple(l < DOF ? l : DOF - 1) >= 0) ? dt : 0.0;
-  // (PSP_LMASK) pidx_sel's branch per row as lane masks: rows pv[q] and
+  // (r04) pidx_sel's branch per row as lane masks: rows pv[q] and
   // proc_couple(pv[q]), against the lane column jl and the coupled one jcc
   constexpr unsigned long long ml_r[6] = {col_ge_mask<DOF>(0, false), col_ge_mask<DOF>(1, false),
                                           col_ge_mask<DOF>(2, false), col_ge_mask<DOF>(6, false),
@@ -1017,11 +764,6 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 #pragma unroll
   for (int q = 0; q < 6; q++) {
     const int r = pv[q], rc = proc_couple(r);
-    if (PSP_ABL & 64) {
-      nv[q] = 0.0;
-      continue;
-    }
-#if PSP_CPL_FMA
     // (r04) the coupled column's term as an FMA with cf = dt (coupled lanes) or
     // 0: the conditional form was compiled to 12 exec-masked branches, each
     // waiting for its own LDS load (lgkmcnt(0)); S~ is finite, so cf = 0 adds 0
@@ -1029,31 +771,14 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
                           aj * (ds * sm.S[pidx_sel_b(r, jl, Tl, LANE_IN(ml_r[q]))]));
     const double t1 = fma(cf, sm.S[pidx_sel_b(rc, jcc, Tc, LANE_IN(mc_rc[q]))],
                           aj * (ds * sm.S[pidx_sel_b(rc, jl, Tl, LANE_IN(ml_rc[q]))]));
-#else
-    const double t0 = aj * (ds * sm.S[pidx_sel(r, jl, Tl)]) + (jc >= 0 ? dt * sm.S[pidx_sel(r, jcc, Tc)] : 0.0);
-    const double t1 = aj * (ds * sm.S[pidx_sel(rc, jl, Tl)]) + (jc >= 0 ? dt * sm.S[pidx_sel(rc, jcc, Tc)] : 0.0);
-#endif
     nv[q] = t0 + dt * t1;  // A_rr = 1 for pos/vel rows
   }
-#else
-#pragma unroll
-  for (int q = 0; q < 6; q++) {
-    const int r = pv[q], rc = proc_couple(r);
-    const double t0 = aj * (ds * sm.S[pidx(r, jl)]) + (jc >= 0 ? dt * sm.S[pidx(r, jc)] : 0.0);
-    const double t1 = aj * (ds * sm.S[pidx(rc, jl)]) + (jc >= 0 ? dt * sm.S[pidx(rc, jc)] : 0.0);
-    nv[q] = t0 + dt * t1;  // A_rr = 1 for pos/vel rows
-  }
-#endif
   // new time scale d' = A_ll d (A_ll = 1 on the unscaled DOFs)
   if (LANE_IF(l, l < DOF && scaled_dof(l))) {
     ds = aj * ds;
-#if PSP_FAST & 32
     double rc = __builtin_amdgcn_rcp(ds);  // d in (0, 1]: two Newton steps
     rc = fma(rc, fma(-ds, rc, 1.0), rc);
     ids = fma(rc, fma(-ds, rc, 1.0), rc);
-#else
-    ids = 1.0 / ds;
-#endif
   }
   psync();
   PSP_PHASE(24);
@@ -1065,29 +790,6 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   // was issued anyway and waited for on the critical path)
   auto rows_lt9 = [&](auto QS) {
     constexpr bool kQS = decltype(QS)::value;
-#if PSP_ROWS_SEL && PSP_PIDX_SEL
-    if constexpr (kQS) {
-      // branch-free: a lane whose entry is not written stores to its own slot
-      // of the staging area (free from the Delta broadcast to the next epoch)
-      const bool lane_ok = l < DOF && !(l >= 3 && l < 6);
-      const bool jpv = jc >= 0;
-      double* const dump = sm.stg + 16 + (l & 63);
-      static_assert(16 + 64 <= PG<DOF>::STG, "throw-away slots (PG::STG)");
-#pragma unroll
-      for (int q = 0; q < 6; q++) {
-        const int e = pidx_sel(pv[q], jl, Tl);
-        const double qq = (l == pv[q]) ? lq.q0 : 0.0;
-        double* d = (lane_ok && (!jpv || l <= pv[q])) ? sm.S + e : dump;
-        *d = (nv[q] + qq) * ids;
-      }
-#pragma unroll
-      for (int i = 0; i < 3; i++) {
-        double* d = lane_ok ? sm.S + pidx_sel(3 + i, jl, Tl) : dump;
-        *d = X[i] * ids;
-      }
-      return;
-    }
-#endif
     if (LANE_IF(l, l < DOF && !(l >= 3 && l < 6))) {
       const bool jpv = LANE_IF(l, proc_couple(l < DOF ? l : DOF - 1) >= 0);
       const double2* f2 = reinterpret_cast<const double2*>(fq);
@@ -1098,32 +800,30 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
                                                col_ge_mask<DOF>(2, false), col_ge_mask<DOF>(6, false),
                                                col_ge_mask<DOF>(7, false), col_ge_mask<DOF>(8, false)};
 #pragma unroll
-      for (int q = 0; q < ((PSP_ABL & 64) ? 0 : 6); q++)
+      for (int q = 0; q < 6; q++)
         if (LANE_IN(smask[q])) {  // !jpv || l <= pv[q]
-          const int e = PSP_PIDX_SEL ? pidx_sel_b(pv[q], l, Tl, LANE_IN(gmask[q])) : pidx(pv[q], l);  // l < DOF: jl == l
+          const int e = pidx_sel_b(pv[q], l, Tl, LANE_IN(gmask[q]));  // l < DOF: jl == l
           double qq;
-          if constexpr (kQS) qq = (PSP_QDIAG || l != pv[q]) ? 0.0 : lq.q0;
+          if constexpr (kQS) qq = 0.0;
           else qq = f2[e].y;
           sm.S[e] = (nv[q] + qq) * ids;
         }
-#if PSP_QDIAG
       // (r04) the lane-resident Q's diagonal on the pos / vel rows added by
       // their own lane afterwards, instead of a select per row: lane l in
       // {0, 1, 2, 6, 7, 8} (jpv) stored (l, l) above; d_l = 1 there (ids == 1),
       // so nv + q0 is bitwise the (nv + q0) * ids of the select form
-      if (kQS && jpv && !(PSP_ABL & 64)) sm.S[Tl + l] += lq.q0;
-#endif
+      if (kQS && jpv) sm.S[Tl + l] += lq.q0;
 #pragma unroll
       for (int i = 0; i < 3; i++) {
         constexpr unsigned long long omask[3] = {col_ge_mask<DOF>(3, false), col_ge_mask<DOF>(4, false),
                                                  col_ge_mask<DOF>(5, false)};
-        const int e = PSP_PIDX_SEL ? pidx_sel_b(3 + i, l, Tl, LANE_IN(omask[i])) : pidx(3 + i, l);
+        const int e = pidx_sel_b(3 + i, l, Tl, LANE_IN(omask[i]));
         if constexpr (kQS) sm.S[e] = X[i] * ids;
         else sm.S[e] = (X[i] + f2[e].y) * ids;
       }
     }
   };
-  if (qs || PSP_DIAG_HOT)
+  if (qs)
     rows_lt9(std::true_type{});
   else
     rows_lt9(std::false_type{});
@@ -1138,7 +838,6 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     constexpr int R0 = 9;
     const double2* f2 = reinterpret_cast<const double2*>(fq);
     const int bw = sh.q_bw;
-#if PSP_DIAG_SEL
     // the lane-resident band (qs) and the table band are separate uniform
     // branches: a per-lane select between them made the compiler issue the
     // table load anyway and wait for it (and for the IMU prefetch) every epoch.
@@ -1149,7 +848,6 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     for (int i = 0; i < 4; i++) asm volatile("" : "+s"(qw4[i]));
     auto band = [&](auto QS) {
       constexpr bool kQS = decltype(QS)::value;
-#if PSP_BAND_PRE
       if constexpr (kQS) {
         // (r04) the three entries (l, l - k) loaded unconditionally (clamped
         // into the triangle), then stored under the lane's mask: the masked
@@ -1161,9 +859,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
         int e[3];
         bool w[3];
         double idk = ids;  // 1 / d'_{l-k}
-#undef LMG
-#define LMG 8
-        // (PSP_LMASK) the band's lane conditions per k as constant masks
+        // (r04) the band's lane conditions per k as constant masks
         constexpr unsigned long long bandm[3] = {
             lane_mask([](int l) constexpr { return l >= R0 && l < DOF && l >= R0; }),
             lane_mask([](int l) constexpr { return l >= R0 && l < DOF && l - 1 >= R0; }),
@@ -1188,32 +884,11 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
           if (w[k]) sm.S[e[k]] = v[k] + f[k];
         return;
       }
-#endif
       double idk = ids;  // 1 / d'_{l-k}
 #pragma unroll
       for (int k = 0; k < 3; k++) {
         if (k > 0) idk = dpp_d<0x138, 0xf, 0xf>(idk);  // wave_shr:1 -> lane l - k
         const int j = l - k;
-#if PSP_ROWS_SEL
-        if constexpr (kQS) {
-          // branch-free read-modify-write: entry (l, j) clamped into the
-          // triangle for the load; a lane without a band entry (or with q == 0)
-          // stores to its own slot of the staging area
-          const bool w = l >= R0 && l < DOF && j >= R0 && k <= bw;
-          const int lc = l < DOF ? l : DOF - 1;
-          const int e = (lc * (lc + 1)) / 2 + (j >= 0 ? (j <= lc ? j : lc) : 0);
-          double q = k == 0 ? lq.q0 : (k == 1 ? lq.q1 : lq.q2);
-          if (k == 0 && l >= L::d_wv && l < L::d_wv + 4) {
-            const int iw = l - L::d_wv;
-            const double qw = iw == 0 ? qw4[0] : (iw == 1 ? qw4[1] : (iw == 2 ? qw4[2] : qw4[3]));
-            q = dt2 * (qw + wv_add);
-          }
-          const double v = sm.S[e] + q * (ids * idk);
-          double* d = (w && q != 0.0) ? sm.S + e : sm.stg + 16 + (l & 63);
-          *d = v;
-          continue;
-        }
-#endif
         if (l >= R0 && l < DOF && j >= R0 && k <= bw) {
           const int e = pidx(l, j);
           double q;
@@ -1228,31 +903,11 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
         }
       }
     };
-    if (PSP_ABL & 128)
-      ;
-    else if (qs || PSP_DIAG_HOT)
+    if (qs)
       band(std::true_type{});
     else
       band(std::false_type{});
-#else
-    double idk = ids;  // 1 / d'_{l-k}
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      if (k > 0) idk = dpp_d<0x138, 0xf, 0xf>(idk);  // wave_shr:1 -> lane l - k
-      const int j = l - k;
-      if (l >= R0 && l < DOF && j >= R0 && k <= bw) {
-        const int e = pidx(l, j);
-        double q;
-        if (qs)
-          q = k == 0 ? lq.q0 : (k == 1 ? lq.q1 : lq.q2);
-        else
-          q = f2[e].y;
-        if (k == 0 && l >= L::d_wv && l < L::d_wv + 4) q = dt2 * (sh.q_wv[l - L::d_wv] + wv_add);
-        if (q != 0.0) sm.S[e] += q * (ids * idk);
-      }
-    }
-#endif
-    for (int k = 3; k <= ((PSP_DIAG_HOT || QM == 1) ? 0 : bw); k++) {  // uniform bound: wide Q bands only
+    for (int k = 3; k <= (QM == 1 ? 0 : bw); k++) {  // uniform bound: wide Q bands only
       const double idj = shfl_d(ids, l - k >= 0 ? l - k : 0);
       const int j = l - k;
       if (l >= R0 && l < DOF && j >= R0) {
@@ -1263,19 +918,12 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     }
   }
   PSP_PHASE(25);
-#undef LMG
-#define LMG 16
   // new mean: vect parts f(mu), orientation the manifold mean
-#if PSP_BAND_PRE
   // every lane evaluates (reads past mu land in the staging area, never
   // stored): the loads need no exec branch and wait
   static_assert(Lay<DOF>::store + PG<DOF>::STG >= 64, "mu reads of lanes >= store stay in PspSmem");
-  double mv = proc_vect_lane(l & 63, sm.mu, pc);
+  double mv = proc_vect_lane(l & 63, flat(sm) + kFlatMu<DOF>, pc);
   asm volatile("" : "+v"(mv));
-#else
-  double mv = 0.0;
-  if (l < L::store && !(l >= 3 && l < 7)) mv = proc_vect_lane(l, sm.mu, pc);
-#endif
   psync();
   if (LANE_IF(l, l < L::store && !(l >= 3 && l < 7))) sm.mu[l] = mv;
   if (LANE_IF(l, l < 4)) sm.mu[3 + l] = mq[l];
@@ -1423,155 +1071,7 @@ struct PZ {  // measurementZPosition, PoseUKF.cpp:100-105: linear (k = 0)
   UWVK_DEV void jac(const double*, double (&H)[M][NC]) const { H[0][0] = 1; }
 };
 
-// Sigma~ -= C~ K~^T on rows [i0, i0 + R): lane l owns column l (entries
-// (i, l), i >= l).  The packed offset of (i0 + r, 0) is uniform (scalar ALU),
-// so a row costs one address add, the mask compare, M FMAs and the store;
-// C~_i is an LDS broadcast (stg[M i ..]).  Rows are loaded before any store.
-// Lanes l > i load a neighbouring entry of the same PspSmem (never stored).
-template <int R, int M>
-UWVK_DEV void rankm_rows(double* S, const double* stg, int i0, int c0, int l, const double (&Kt)[M]) {
-  const int tri = i0 * (i0 + 1) / 2;
-  double sv[R], cv[R][M];
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    sv[r] = S[tri + r * i0 + r * (r + 1) / 2 + l];
-#pragma unroll
-    for (int a = 0; a < M; a++) cv[r][a] = stg[M * (i0 - c0 + r) + a];
-  }
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-#if PSP_FAST & 4
-    double s2 = sv[r];
-#pragma unroll
-    for (int a = 0; a < M; a++) s2 = fma(-cv[r][a], Kt[a], s2);
-    if (l <= i0 + r) S[tri + r * i0 + r * (r + 1) / 2 + l] = s2;
-#else
-    double s2 = 0.0;
-#pragma unroll
-    for (int a = 0; a < M; a++) s2 += cv[r][a] * Kt[a];
-    if (l <= i0 + r) S[tri + r * i0 + r * (r + 1) / 2 + l] = sv[r] - s2;
-#endif
-  }
-}
-
-// The short rows 0 .. P-1 (P = min(32, DOF), at most 32 entries each) two to an
-// instruction: lanes 0-31 take row p, lanes 32-63 row P-1-p (column l & 31),
-// so rows [0, P) cost P/2 row steps instead of P.  The uniform row offsets and
-// C~ addresses are selected per half (two broadcast addresses, one per half);
-// Kx = K~ of column l & 31.
-template <int R, int M, int P>
-UWVK_DEV void rankm_pairs(double* S, const double* stg, int p0, int l, const double (&Kx)[M]) {
-  const int col = l & 31;
-#if PSP_PAIR_MASK
-  // the half's row and packed row offset as uniform (scalar) values blended
-  // with the lane mask hm = -(l >> 5) (bitwise and / add): written as
-  // `hi ? pb : pa` the compiler branched on the lane-divergent condition, two
-  // exec-masked paths per row with the offsets computed inside (r03 ISA)
-  const int hm = -(l >> 5);
-  double sv[R], cv[R][M];
-  int ad[R], row[R];
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const int pa = p0 + r, pb = P - 1 - pa;
-    const int ta = pa * (pa + 1) / 2, tb = pb * (pb + 1) / 2;
-    row[r] = pa + ((pb - pa) & hm);
-    ad[r] = ta + ((tb - ta) & hm) + col;
-    sv[r] = S[ad[r]];
-    const double* c = stg + M * row[r];
-#pragma unroll
-    for (int a = 0; a < M; a++) cv[r][a] = c[a];
-  }
-#else
-  const bool hi = l >= 32;
-  double sv[R], cv[R][M];
-  int ad[R], row[R];
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const int pa = p0 + r, pb = P - 1 - pa;
-    row[r] = hi ? pb : pa;
-    ad[r] = (hi ? pb * (pb + 1) / 2 : pa * (pa + 1) / 2) + col;
-    sv[r] = S[ad[r]];
-#pragma unroll
-    for (int a = 0; a < M; a++) cv[r][a] = stg[M * row[r] + a];
-  }
-#endif
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    double s2 = sv[r];
-#pragma unroll
-    for (int a = 0; a < M; a++) s2 = fma(-cv[r][a], Kx[a], s2);
-    if (col <= row[r]) S[ad[r]] = s2;
-  }
-}
-
-// Sigma~ -= C~ K~^T on v_mfma_f64_16x16x4_f64 (PSP_RANKM_MFMA): the packed
-// lower triangle as the 16 x 16 tiles (I, J), J <= I, of a 16 NT frame.  Tile
-// D = A B + acc with A[r][k] = -C~[16 I + r][k], B[k][c] = K~[16 J + c][k]
-// (k < M, zero padded to K = 4) and acc the tile of Sigma~ (lane l holds rows
-// (l >> 4) + 4 i, column l & 15: the f64 C/D map, uwvk_dev.hpp).  The
-// operands are transposed through stg one 16-row block at a time (the rows'
-// lanes write C~ / K~, every lane reads component l >> 4 of row l & 15).
-// Rows >= DOF are clamped on load and never stored; in diagonal tiles only
-// column <= row is stored.  The per-entry flops and their summation order
-// differ from the FMA-chain row sweep only in rounding.
-#undef LMG
-#define LMG 32
-template <int DOF, int M>
-UWVK_DEV void rankm_mfma(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
-  static_assert(M <= 3, "rank <= 3 (K = 4 with zero padding)");
-  constexpr int NT = (DOF + 15) / 16;
-  static_assert(2 * 16 * M <= PG<DOF>::STG, "operand blocks (PG::STG)");
-  // (the masks give the compiler the ranges: l is a laundered lane id)
-  const int q = (l >> 4) & 3, c = l & 15;
-  double Aop[NT], Bop[NT];
-#pragma unroll
-  for (int T = 0; T < NT; T++) {
-    if (q == T) {
-#pragma unroll
-      for (int k = 0; k < M; k++) {
-        stg[c * M + k] = Ct[k];
-        stg[16 * M + c * M + k] = Kt[k];
-      }
-    }
-    wsync();
-    const int qq = LANE_IF(l, ((l >> 4) & 3) < M) ? q : 0;
-    const double a = stg[c * M + qq], b = stg[16 * M + c * M + qq];
-    Aop[T] = LANE_IF(l, ((l >> 4) & 3) < M) ? -a : 0.0;
-    Bop[T] = LANE_IF(l, ((l >> 4) & 3) < M) ? b : 0.0;
-    wsync();  // the next block's writes after every lane's reads
-  }
-#pragma unroll
-  for (int I = 0; I < NT; I++) {
-    // packed offsets of this lane's rows 16 I + q + 4 i (clamped into the triangle)
-    int base[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      unsigned R = 16 * I + q + 4 * i;
-      if (16 * I + 4 * i + 3 >= DOF) R = R < DOF ? R : DOF - 1;  // only the last rows can pass DOF
-      base[i] = (int)((R * (R + 1)) >> 1) + c;
-    }
-#pragma unroll
-    for (int J = 0; J <= I; J++) {
-      d4_t acc;
-#pragma unroll
-      for (int i = 0; i < 4; i++) acc[i] = (16 * I + 4 * i < DOF) ? S[base[i] + 16 * J] : 0.0;
-      acc = mfma_f64(Aop[I], Bop[J], acc);
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        if (16 * I + 4 * i >= DOF) continue;  // no row of this register is in the triangle
-        const int R = 16 * I + q + 4 * i;
-        const bool row_ok = (16 * I + 4 * i + 3 < DOF) || R < DOF;  // compile-time true but for the last rows
-        const bool st = row_ok && (I > J || c <= q + 4 * i);
-        if (st) S[base[i] + 16 * J] = acc[i];
-      }
-    }
-  }
-}
-
 // one row block I of rankm_mfma_o (tiles (I, J), J <= I), then block I + 1
-#ifndef PSP_TQ_BASE  // r04: tile row offsets as T(x + q) = T(x) + q x + T(q) (x compile-time): one multiply-add
-#define PSP_TQ_BASE 1
-#endif
 template <int DOF, int I, int NT>
 UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop)[NT], int q, int c, int tq) {
   if constexpr (I < NT) {
@@ -1579,15 +1079,10 @@ UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop
     int base[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-#if PSP_TQ_BASE
       // row R = x + q, x = O + 16 I + 4 i: packed offset T(x) + q x + T(q) + O + c
       // (tq = T(q) + O + c, once per phase) instead of R (R + 1) / 2 per row
       const int x = O + 16 * I + 4 * i;  // a constant after unrolling
       base[i] = q * x + (x * (x + 1) / 2) + tq;
-#else
-      const unsigned R = O + 16 * I + q + 4 * i;
-      base[i] = (int)((R * (R + 1)) >> 1) + O + c;
-#endif
     }
     d4_t acc[I + 1];
 #pragma unroll
@@ -1602,7 +1097,7 @@ UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop
     else if constexpr (I == 1) asm volatile("" : "+v"(acc[0]), "+v"(acc[1]));
     else if constexpr (I == 2) asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]));
     else asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
-    // (PSP_LMASK) the diagonal tile's lower-triangle lanes per i as constant masks
+    // (r04) the diagonal tile's lower-triangle lanes per i as constant masks
     constexpr unsigned long long diagm[4] = {
         lane_mask([](int l) constexpr { return (l & 15) <= ((l >> 4) & 3) + 0; }),
         lane_mask([](int l) constexpr { return (l & 15) <= ((l >> 4) & 3) + 4; }),
@@ -1617,15 +1112,22 @@ UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop
   }
 }
 
-// The same product on a frame shifted by O = DOF mod 16 (PSP_RANKM_MFMA == 2):
-// the NT = DOF / 16 full row blocks [O + 16 I, O + 16 I + 16) make NT (NT + 1) / 2
-// tiles with every row inside the triangle (53: 6 tiles instead of 10, whose
-// last row block held 5 rows of 16); the strip of columns < O (rows 0..DOF-1)
-// is a lane-per-row FMA chain with K~ of those columns as uniform values.
-// Within a row block all tiles' loads are issued first, then the MFMAs
-// back to back (independent accumulators), then the stores: the r03 ISA of
-// rankm_mfma ran load -> MFMA -> s_nop 16 -> store per tile, ~1,900 cycles per
-// instance-epoch with its latencies exposed.
+// Sigma~ -= C~ K~^T on v_mfma_f64_16x16x4_f64.  Tile D = A B + acc with
+// A[r][k] = -C~[row r][k], B[k][c] = K~[col c][k] (k < M, zero padded to K = 4)
+// and acc the tile of Sigma~ (lane l holds rows (l >> 4) + 4 i, column l & 15:
+// the f64 C/D map, uwvk_dev.hpp).  The frame is shifted by O = DOF mod 16: the
+// NT = DOF / 16 full row blocks [O + 16 I, O + 16 I + 16) make NT (NT + 1) / 2
+// tiles with every row inside the triangle (53: 6 tiles instead of the 10 of
+// a 16-aligned frame, whose last row block held 5 rows of 16); in diagonal
+// tiles only column <= row is stored.  The strip of columns < O (rows
+// 0..DOF-1) is a lane-per-row FMA chain with K~ of those columns as uniform
+// values.  The operands are transposed through stg one 16-row block at a time.
+// Within a row block all tiles' loads are issued first, then the MFMAs back to
+// back (independent accumulators), then the stores (the r03 16-aligned form
+// ran load -> MFMA -> s_nop 16 -> store per tile, its latencies exposed; the
+// r03 all-tiles-in-flight form tied: profiles/EXPERIMENTS.md).  The per-entry
+// flops and their summation order differ from an FMA-chain row sweep only in
+// rounding.
 template <int DOF, int M>
 UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
   static_assert(M <= 3, "rank <= 3 (K = 4 with zero padding)");
@@ -1668,7 +1170,6 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
     for (int j = 0; j < O; j++)
 #pragma unroll
       for (int k = 0; k < M; k++) kc[j][k] = kStripLds ? stg[32 * M + j * M + k] : readlane_d(Kt[k], j);
-#if PSP_BAND_PRE
     {
       // (r04) every lane loads its row (clamped to the last one) outside any
       // branch; only the stores are masked to the rows of the triangle
@@ -1690,106 +1191,8 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
         for (int j = O - 1; j >= 0; j--) S[b0 + (j <= lc ? j : lc)] = nv[j];
       }
     }
-#else
-    if (l < DOF) {
-      const int b0 = (l * (l + 1)) >> 1;
-      double sv[O];
-#pragma unroll
-      for (int j = 0; j < O; j++) sv[j] = S[b0 + (j <= l ? j : l)];
-#pragma unroll
-      for (int j = O - 1; j >= 0; j--) {
-        double s2 = sv[j];
-#pragma unroll
-        for (int k = 0; k < M; k++) s2 = fma(-Ct[k], kc[j][k], s2);
-        S[b0 + (j <= l ? j : l)] = s2;
-      }
-    }
-#endif
   }
   rankm_block<DOF, 0, NT>(S, Aop, Bop, q, c, ((q * (q + 1)) >> 1) + O + c);
-}
-
-// rankm_mfma_o with every tile in flight at once (PSP_RANKM_MFMA == 3): all
-// tiles' loads, all MFMAs, the strip's FMA chains while they run, the stores
-template <int N>
-UWVK_DEV void pin_acc(d4_t (&a)[N]) {
-  if constexpr (N == 1) asm volatile("" : "+v"(a[0]));
-  else if constexpr (N == 3) asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]));
-  else if constexpr (N == 6) asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]));
-  else static_assert(N == 1 || N == 3 || N == 6, "tile count");
-}
-template <int DOF, int M>
-UWVK_DEV void rankm_mfma_all(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
-  static_assert(M <= 3, "rank <= 3 (K = 4 with zero padding)");
-  constexpr int NT = DOF / 16, O = DOF - 16 * NT, NTL = NT * (NT + 1) / 2;
-  static_assert(NT >= 1 && NT <= 3, "frame");
-  static_assert(2 * 16 * M <= PG<DOF>::STG, "operand blocks (PG::STG)");
-  const int q = (l >> 4) & 3, c = l & 15;
-  double Aop[NT], Bop[NT];
-#pragma unroll
-  for (int T = 0; T < NT; T++) {
-    const int src = l - O - 16 * T;
-    if (src >= 0 && src < 16) {
-#pragma unroll
-      for (int k = 0; k < M; k++) {
-        stg[src * M + k] = Ct[k];
-        stg[16 * M + src * M + k] = Kt[k];
-      }
-    }
-    wsync();
-    const int qq = LANE_IF(l, ((l >> 4) & 3) < M) ? q : 0;
-    const double a = stg[c * M + qq], b = stg[16 * M + c * M + qq];
-    Aop[T] = LANE_IF(l, ((l >> 4) & 3) < M) ? -a : 0.0;
-    Bop[T] = LANE_IF(l, ((l >> 4) & 3) < M) ? b : 0.0;
-    wsync();
-  }
-  int base[NT][4];
-#pragma unroll
-  for (int I = 0; I < NT; I++)
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const unsigned R = O + 16 * I + q + 4 * i;
-      base[I][i] = (int)((R * (R + 1)) >> 1) + O + c;
-    }
-  d4_t acc[NTL];
-#pragma unroll
-  for (int I = 0; I < NT; I++)
-#pragma unroll
-    for (int J = 0; J <= I; J++)
-#pragma unroll
-      for (int i = 0; i < 4; i++) acc[I * (I + 1) / 2 + J][i] = S[base[I][i] + 16 * J];
-#pragma unroll
-  for (int I = 0; I < NT; I++)
-#pragma unroll
-    for (int J = 0; J <= I; J++) acc[I * (I + 1) / 2 + J] = mfma_f64(Aop[I], Bop[J], acc[I * (I + 1) / 2 + J]);
-  if constexpr (O > 0) {  // the strip (columns < O) while the MFMAs run
-    double kc[O][M];
-#pragma unroll
-    for (int j = 0; j < O; j++)
-#pragma unroll
-      for (int k = 0; k < M; k++) kc[j][k] = readlane_d(Kt[k], j);
-    if (l < DOF) {
-      const int b0 = (l * (l + 1)) >> 1;
-      double sv[O];
-#pragma unroll
-      for (int j = 0; j < O; j++) sv[j] = S[b0 + (j <= l ? j : 0)];
-#pragma unroll
-      for (int j = 0; j < O; j++) {
-        double s2 = sv[j];
-#pragma unroll
-        for (int k = 0; k < M; k++) s2 = fma(-Ct[k], kc[j][k], s2);
-        if (j <= l) S[b0 + j] = s2;
-      }
-    }
-  }
-  pin_acc<NTL>(acc);
-#pragma unroll
-  for (int I = 0; I < NT; I++)
-#pragma unroll
-    for (int J = 0; J <= I; J++)
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        if (J < I || c <= q + 4 * i) S[base[I][i] + 16 * J] = acc[I * (I + 1) / 2 + J][i];
 }
 
 // acc + h x for an entry h of a measurement Jacobian: the structural zeros of
@@ -1807,8 +1210,6 @@ UWVK_DEV double hfma(double h, double x, double acc) {
 // ukf::update [EXT], PSP form.  gate: 0 accept any, 1 d2p95.  Returns the gate
 // decision; *ok = false on a non-positive pivot of the partial Cholesky.
 // ---------------------------------------------------------------------------
-#undef LMG
-#define LMG 64
 template <int DOF, int SR, class HM>
 UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const double (&Rm)[HM::M * HM::M], int gate,
                          const HM& hm, bool* ok, double ds, double ids, Stamper* st = nullptr) {
@@ -1819,11 +1220,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double a[KA];
   bool cok = true;
   if constexpr (K > 0) {
-#if PSP_ABL & 32
-    for (int c = 0; c < K; c++) a[c] = sm.S[pidx(l < DOF ? l : DOF - 1, c)];
-#else
     cok = pchol<DOF, K, HM>(sm.S, l, a, ds, sm.stg);
-#endif
   }
   PSP_PHASE(30);
   [[maybe_unused]] const bool pt = LANE_IF(l, l < 2 * K);  // the non-lds_sums path (PSP_FAST & 256 off)
@@ -1838,7 +1235,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   for (int i = 0; i < M; i++) zc[i] = readlane_d(zp[i], 2 * K);
   constexpr double wc = 1.0 + 2.0 * (DOF - K);
   double S[M * M];
-#if PSP_FAST & 256
   // H and P first: P reads the staged rows, after which stg holds the
   // transposed sums.  One round of M + M(M+1)/2 sums over the 2K point lanes:
   // u = z_p - z_0, s = sum u, m = s / N; sum dz dz^T = sum u u^T - m s^T - s m^T + 2K m m^T
@@ -1899,56 +1295,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double zd[M];
 #pragma unroll
   for (int i = 0; i < M; i++) zd[i] = K > 0 ? zp[i] - swap_pair_d(zp[i]) : 0.0;
-#else
-  // zbar = z_0 + (1/N) sum_{2K} (z_p - z_0)  (the linear pairs cancel)
-#pragma unroll
-  for (int i = 0; i < M; i++) {
-    const double s = K > 0 ? wave_sum_dpp<2 * K>(pt ? zp[i] - zc[i] : 0.0) : 0.0;
-#if PSP_FAST & 2
-    zb[i] = zc[i] + s * (1.0 / (double)G::N);
-#else
-    zb[i] = zc[i] + s / (double)G::N;
-#endif
-    e[i] = zc[i] - zb[i];
-  }
-  double dz[M];
-#pragma unroll
-  for (int i = 0; i < M; i++) dz[i] = zp[i] - zb[i];
-#pragma unroll
-  for (int i = 0; i < M; i++)
-#pragma unroll
-    for (int j = 0; j <= i; j++) {
-      const double s = K > 0 ? wave_sum_dpp<2 * K>(pt ? dz[i] * dz[j] : 0.0) : 0.0;
-      S[i * M + j] = 0.5 * (s + wc * e[i] * e[j]);
-    }
-  // Delta z_j = z_{j+} - z_{j-} lives in lane 2j (read back as uniform values)
-  double zd[M];
-#pragma unroll
-  for (int i = 0; i < M; i++) zd[i] = K > 0 ? zp[i] - swap_pair_d(zp[i]) : 0.0;
-  // affine part.  H at mu: every lane evaluates it, the values become uniform
-  // (SGPR) copies; P = H L_a lane-parallel (lane i*K + j); G = Sigma H^T (lane r).
-  double Hs[M][NC];
-  {
-    double H[M][NC];
-    hm.jac(sm.mu, H);
-#pragma unroll
-    for (int i = 0; i < M; i++)
-#pragma unroll
-      for (int t = 0; t < NC; t++) Hs[i][t] = readlane_d(H[i][t], 0);
-  }
-  double Pl = 0.0;
-  if constexpr (K > 0) {
-    const int q = LANE_IF(l, l < M * K) ? l : 0;
-    const int i = q / K, j = q - (q / K) * K;
-#pragma unroll
-    for (int t = 0; t < NC; t++) {
-      double h = Hs[0][t];
-#pragma unroll
-      for (int ii = 1; ii < M; ii++) h = (i == ii) ? Hs[ii][t] : h;
-      Pl += h * sm.stg[STG_ROWS + row_pos(HM::rows, HM::cols[t]) * K + j];
-    }
-  }
-#endif
   PSP_PHASE(31);
   const int rl = l < DOF ? l : DOF - 1;
   const int Trl = (rl * (rl + 1)) >> 1;
@@ -1957,7 +1303,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   for (int i = 0; i < M; i++) Gr[i] = 0.0;
 #pragma unroll
   for (int t = 0; t < NC; t++) {
-    double s = sm.S[PSP_PIDX_SEL ? pidx_sel(HM::cols[t], rl, Trl) : pidx(rl, HM::cols[t])];
+    double s = sm.S[pidx_sel(HM::cols[t], rl, Trl)];
     if (scaled_dof(HM::cols[t])) s = s * readlane_d(ds, HM::cols[t]);
 #pragma unroll
     for (int i = 0; i < M; i++) Gr[i] = hfma(Hs[i][t], s, Gr[i]);
@@ -1968,14 +1314,13 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   // Glin_r = G_r - sum_j L[r][j] P[:, j]: row r of (Sigma - L_a L_a^T) H^T;
   // C_r = Glin_r + 1/2 sum_j L[r][j] Dz_j; S += H Glin + R  (H Glin = H Sigma H^T - P P^T)
   double Gl[M], C[M];
-#if PSP_UPD_LDS
   if constexpr (K > 0) {
     // P (lane i K + j) and Dz_j (lane 2 j) staged in stg (free after the sums)
     // and read back as broadcasts one j at a time, as the predict's Delta
     // (PSP_DELTA_LDS): LDS reads instead of 4 M K v_readlane
     // (PSP_LDS_ALIGN: M = 3 rows padded to 4 from slot 1, so each j's first
     // pair is one aligned ds_read_b128)
-    constexpr int PS = (PSP_LDS_ALIGN && M == 3) ? 4 : M, P0 = (PSP_LDS_ALIGN && M >= 2) ? 1 : 0;
+    constexpr int PS = M == 3 ? 4 : M, P0 = M >= 2 ? 1 : 0;
     static_assert(P0 + 2 * PS * K <= PG<DOF>::STG, "P and Dz (PG::STG)");
     if (LANE_IF(l, l < M * K)) sm.stg[P0 + (l % K) * PS + l / K] = Pl;  // j-major: P[i][j] at j PS + i
     if (LANE_IF(l, (l & 1) == 0 && l < 2 * K)) {
@@ -2017,21 +1362,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       C[i] = Gr[i];
     }
   }
-#else
-#pragma unroll
-  for (int i = 0; i < M; i++) {
-    double g = Gr[i], c = 0.0;
-    if constexpr (K > 0) {
-#pragma unroll
-      for (int j = 0; j < K; j++) {
-        g -= a[j] * readlane_d(Pl, i * K + j);
-        c += a[j] * readlane_d(zd[i], 2 * j);
-      }
-    }
-    Gl[i] = g;
-    C[i] = g + 0.5 * c;
-  }
-#endif
 #pragma unroll
   for (int i = 0; i < M; i++)
 #pragma unroll
@@ -2081,89 +1411,10 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     Ct[i] = C[i] * ids;
     Kt[i] = Kg[i] * ids;
   }
-#if PSP_RANKM_MFMA
   psync();
-#if PSP_RANKM_MFMA == 3
-  if (!(PSP_ABL & 2)) rankm_mfma_all<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
-#elif PSP_RANKM_MFMA == 2
-  if (!(PSP_ABL & 2)) rankm_mfma_o<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
-#else
-  if (!(PSP_ABL & 2)) rankm_mfma<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
-#endif
-#elif PSP_FAST & 2048
-  {
-    // rows [0, P) paired (rankm_pairs), then rows [P, DOF) one per step; the
-    // C~ rows of each part are staged in stg in turn
-    constexpr int P = DOF < 32 ? DOF : 32, NPAIR = P / 2, RB = PSP_RB;
-    static_assert(P % 2 == 0 && M * P <= PG<DOF>::STG && M * (DOF - P) <= PG<DOF>::STG, "C~ parts (PG::STG)");
-    static_assert(63 < Lay<DOF>::store + PG<DOF>::STG, "row over-read (lanes l > i, last rows) stays inside PspSmem");
-    double Kx[M];
-#pragma unroll
-    for (int a2 = 0; a2 < M; a2++) Kx[a2] = shfl_d(Kt[a2], l & 31);
-    if (l < P) {
-#pragma unroll
-      for (int a2 = 0; a2 < M; a2++) sm.stg[M * l + a2] = Ct[a2];
-    }
-    psync();
-    if (!(PSP_ABL & 2)) {
-      constexpr int RBP = PSP_RBP < NPAIR ? PSP_RBP : NPAIR, NBP = NPAIR / RBP, REMP = NPAIR - NBP * RBP;
-#pragma unroll 1
-      for (int b = 0; b < NBP; b++) rankm_pairs<RBP, M, P>(sm.S, sm.stg, b * RBP, l, Kx);
-      if constexpr (REMP > 0) rankm_pairs<REMP, M, P>(sm.S, sm.stg, NBP * RBP, l, Kx);
-    }
-    if constexpr (DOF > P) {
-      psync();
-      if (l >= P && l < DOF) {
-#pragma unroll
-        for (int a2 = 0; a2 < M; a2++) sm.stg[M * (l - P) + a2] = Ct[a2];
-      }
-      psync();
-      if (!(PSP_ABL & 2)) {
-        constexpr int NR2 = DOF - P, NB2 = NR2 / RB, REM2 = NR2 - NB2 * RB;
-#pragma unroll 1
-        for (int b = 0; b < NB2; b++) rankm_rows<RB, M>(sm.S, sm.stg, P + b * RB, P, l, Kt);
-        if constexpr (REM2 > 0) rankm_rows<REM2, M>(sm.S, sm.stg, P + NB2 * RB, P, l, Kt);
-      }
-    }
-  }
-#else
-  {
-    // C~ rows for the broadcast reads (stg is free here), in two halves of
-    // rows [0, H) and [H, DOF) so that M * max(H, DOF - H) fits PG::STG
-    constexpr int RB = PSP_RB, NB = DOF / RB, REM = DOF - NB * RB;
-    constexpr int NB1 = (NB + 1) / 2, H = NB1 * RB;
-    static_assert(M * H <= PG<DOF>::STG && M * (DOF - H) <= PG<DOF>::STG, "C~ halves (PG::STG)");
-    static_assert(63 < Lay<DOF>::store + PG<DOF>::STG, "row over-read (lanes l > i, last rows) stays inside PspSmem");
-    if (l < H) {
-#pragma unroll
-      for (int a2 = 0; a2 < M; a2++) sm.stg[M * l + a2] = Ct[a2];
-    }
-    psync();
-    if (!(PSP_ABL & 2)) {
-#pragma unroll 1
-      for (int b = 0; b < NB1; b++) rankm_rows<RB, M>(sm.S, sm.stg, b * RB, 0, l, Kt);
-    }
-    psync();
-    if (l >= H && l < DOF) {
-#pragma unroll
-      for (int a2 = 0; a2 < M; a2++) sm.stg[M * (l - H) + a2] = Ct[a2];
-    }
-    psync();
-    if (!(PSP_ABL & 2)) {
-#pragma unroll 1
-      for (int b = NB1; b < NB; b++) rankm_rows<RB, M>(sm.S, sm.stg, b * RB, H, l, Kt);
-      if constexpr (REM > 0) rankm_rows<REM, M>(sm.S, sm.stg, NB * RB, H, l, Kt);
-    }
-  }
-#endif
+  rankm_mfma_o<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
   psync();
   PSP_PHASE(34);
-  if (PSP_ABL & 256) {
-    asm volatile("" ::"v"(dl));
-    return true;
-  }
-#undef LMG
-#define LMG 128
   // apply_delta, exact form: mu <- mu [+] delta, Sigma <- T Sigma T^T with T
   // the identity except on the orientation block.  ukfom re-spreads X_p =
   // mu [+] +-L_j, shifts every point by delta and takes the deviations from
@@ -2181,7 +1432,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       const double tq[4] = {eq[0], SR ? -eq[1] : eq[1], SR ? -eq[2] : eq[2], SR ? -eq[3] : eq[3]};
       qmatrix(tq, R);
     }
-#if PSP_BAND_PRE
     // (r04) rows 3..5 of every column j outside the block, and the ori x ori
     // block R B R^T: every lane loads and computes (its column clamped into
     // the triangle; the block's lanes 3..5 and lanes >= 9 compute values that
@@ -2220,44 +1470,10 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
         sm.S[e2] = n3[2];
       }
     }
-#else
-    // rows 3..5 of every column j outside the block
-    if (l < DOF && !(l >= 3 && l < 6)) {
-#if PSP_PIDX_SEL
-      const int Tl = (l * (l + 1)) >> 1;
-      const int e0 = pidx_sel(3, l, Tl), e1 = pidx_sel(4, l, Tl), e2 = pidx_sel(5, l, Tl);
-#else
-      const int e0 = pidx(3, l), e1 = pidx(4, l), e2 = pidx(5, l);
-#endif
-      const double s0 = sm.S[e0], s1 = sm.S[e1], s2 = sm.S[e2];
-      const int e[3] = {e0, e1, e2};
-#pragma unroll
-      for (int i = 0; i < 3; i++) sm.S[e[i]] = R[i * 3] * s0 + R[i * 3 + 1] * s1 + R[i * 3 + 2] * s2;
-    }
-    // ori x ori: R B R^T
-    double nb = 0.0;
-    if (l < 9) {
-      const int r = l / 3, c = l % 3;
-      double s = 0.0;
-#pragma unroll
-      for (int u = 0; u < 3; u++) {
-        double t = 0.0;
-#pragma unroll
-        for (int v = 0; v < 3; v++) t += sm.S[pidx(3 + u, 3 + v)] * sel3(R[v], R[3 + v], R[6 + v], c);
-        s += sel3(R[u], R[3 + u], R[6 + u], r) * t;
-      }
-      nb = s;
-    }
-#endif
     // storage s = l takes tangent delta_{l} (l < 3) or delta_{l-1} (l >= 7): DPP wave_shr:1
     const double dsh = dpp_d<0x138, 0xf, 0xf>(dl);
-#if PSP_BAND_PRE
-    double mnew = sm.mu[l & 63] + 1.0 * (LANE_IF(l, l < 3) ? dl : dsh);  // stored for the vector lanes only
+    double mnew = flat(sm)[kFlatMu<DOF> + (l & 63)] + 1.0 * (LANE_IF(l, l < 3) ? dl : dsh);  // stored for the vector lanes only
     asm volatile("" : "+v"(mnew));
-#else
-    double mnew = 0.0;
-    if (l < L::store && !(l >= 3 && l < 7)) mnew = sm.mu[l] + 1.0 * (l < 3 ? dl : dsh);
-#endif
     double qn[4];
     qplus_psp<SR>(eq, sm.mu + L::s_quat, qn);
     psync();

@@ -22,21 +22,12 @@
 #ifndef PSP_SIDE
 #define PSP_SIDE 0
 #endif
-#if PSP_SIDE != 0
-#undef UWVK_TIMELINE  // the per-wave timeline buffer is the side-0 object's
-#endif
 
 #define UWVK_POSE_KERNEL_BODIES
 #include "uwvk_pose_kernels.hpp"
 #include "uwvk_psp_dev.hpp"
 #include "uwvk_psp.hpp"
 
-#ifndef PSP_PAD_MOV
-#define PSP_PAD_MOV 0
-#endif
-#ifndef PSP_PAD_F64
-#define PSP_PAD_F64 0
-#endif
 
 namespace uwvk {
 namespace psp {
@@ -44,7 +35,7 @@ namespace psp {
 #ifdef UWVK_TIMELINE
 // diagnostic build only (tools/timeline.py): per-wave wall-clock marks of the
 // epoch kernel (entry, Sigma loaded, epochs done, stored) and the CU it ran on
-__device__ unsigned long long uwvk_timeline[8 * 131072];
+static __device__ unsigned long long uwvk_timeline[8 * 131072];  // per side's translation unit
 UWVK_DEV void tl_mark(int64_t w, int k) {
   const unsigned long long t = wall_clock64();
   if (lane_id() == 0 && w < 131072) uwvk_timeline[w * 8 + k] = t;
@@ -114,9 +105,6 @@ UWVK_DEV void tail_signal(const EpochArgs& ea, int64_t t, int chunk) {
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-#ifndef PSP_FLAG_VGPR
-#define PSP_FLAG_VGPR 0  // r02 A/B: no measurable gain, one more VGPR (168)
-#endif
 
 template <int DOF>
 UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst, int l = lane_id()) {
@@ -166,14 +154,10 @@ UWVK_DEV void lane_proc(const PoseBufs& b, const PoseShared& sh, int64_t inst, i
   if (s < DOF && scaled_dof(s)) pc.nt_tan = tan_ntau_sel<DOF>(s, sh);
 }
 
-#ifndef PSP_STORE_PRE  // r04: the epilogue's LDS reads issued before the masked HBM stores
-#define PSP_STORE_PRE 1
-#endif
 template <int DOF>
 UWVK_DEV void store_psp(const PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst, int l = lane_id()) {
   using G = PG<DOF>;
   double* gs = b.sigma + inst * (int64_t)G::NP;
-#if PSP_STORE_PRE
   // (r04) every slot's LDS read first (the last, partial slot's lanes past the
   // triangle read the mean / staging area behind it, never stored), then the
   // coalesced stores: the masked form waited for each read inside its branch
@@ -186,23 +170,15 @@ UWVK_DEV void store_psp(const PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst,
     double v[SG];
 #pragma unroll
     for (int u = 0; u < SG; u++)
-      if (t0 + u < G::NSLOT) v[u] = sm.S[l + 64 * (t0 + u)];
+      if (t0 + u < G::NSLOT) v[u] = flat(sm)[l + 64 * (t0 + u)];  // S at offset 0
 #pragma unroll
     for (int u = 0; u < SG; u++) {
       const int t = t0 + u, e = l + 64 * t;
       if (t < G::NSLOT && (t + 1 < G::NSLOT || e < G::NP)) gs[e] = v[u];
     }
   }
-  const double m = sm.mu[l & 63];
+  const double m = flat(sm)[kFlatMu<DOF> + (l & 63)];
   if (l < Lay<DOF>::store) b.mu[inst * Lay<DOF>::store + l] = m;
-#else
-#pragma unroll 4
-  for (int t = 0; t < G::NSLOT; t++) {
-    const int e = l + 64 * t;
-    if (e < G::NP) gs[e] = sm.S[e];
-  }
-  if (l < Lay<DOF>::store) b.mu[inst * Lay<DOF>::store + l] = sm.mu[l];
-#endif
 }
 
 template <int M>
@@ -317,20 +293,11 @@ __global__ __launch_bounds__(64) void k_psp_update(PoseBufs b, PoseShared sh, Me
 // s_waitcnt vmcnt(0) lgkmcnt(0) (a memory round trip on the epoch's critical
 // path, which also drained the input prefetch); as a constant-space pointer
 // the reads are scalar loads through the scalar cache.
-#ifndef PSP_SHARED_CONST
-#define PSP_SHARED_CONST 1
-#endif
 UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
-#if PSP_SHARED_CONST
   using CP = const __attribute__((address_space(4))) PoseShared*;
   CP p = (CP)b.shared;
   asm volatile("" : "+s"(p));
   return *(const PoseShared*)p;
-#else
-  const PoseShared* p = b.shared;
-  asm volatile("" : "+s"(p));
-  return *p;
-#endif
 }
 
 // Needs <= 168 VGPRs (3 waves per SIMD: with 12 instances per CU from the LDS
@@ -338,11 +305,6 @@ UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
 // resident waves).  amdgpu_waves_per_eu(3) also gives 156 but schedules the
 // epoch loop worse: 145.0M against 148.5M steps/s (r02 A/B), so it is not set;
 // a fully unrolled Sigma store once took the kernel to 188 (2 waves per SIMD).
-#ifdef PSP_WPE  // A/B builds only: amdgpu_waves_per_eu(PSP_WPE)
-#define PSP_EPOCH_ATTR __attribute__((amdgpu_waves_per_eu(PSP_WPE)))
-#else
-#define PSP_EPOCH_ATTR
-#endif
 UWVK_DEV TailUnit ticket_unit(const EpochArgs& ea, uint32_t u) {
   TailUnit t{(int64_t)u, ea.first, ea.first + ea.count, 0, -1};
   if (ea.chunks > 1 && (int64_t)u >= ea.tail0) {
@@ -374,9 +336,6 @@ UWVK_DEV uint32_t ticket_value(const EpochArgs& ea, uint32_t v) {
 // the next unit's Sigma~ and mean, loaded into registers before this unit's
 // stores (persistent kernel): gfx950's vmcnt counts loads and stores in one
 // ordered counter, so a load issued after the stores waits for them as well
-#ifndef PSP_PREFETCH
-#define PSP_PREFETCH 1
-#endif
 template <int DOF>
 struct PspPre {
   double v[PG<DOF>::NSLOT];
@@ -407,10 +366,6 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
 #else
   (void)tlw;
 #endif
-#ifndef PSP_EARLY_INPUTS
-#define PSP_EARLY_INPUTS 1
-#endif
-#if PSP_EARLY_INPUTS
   // (r04) the unit's independent input loads (rotation rate, per-lane process
   // constants, the first epoch's IMU) issued before Sigma~'s load is waited
   // for: one HBM round trip at the unit's start instead of three in a row
@@ -422,10 +377,6 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
   // second copy for the final store was a second set of loop-carried VGPRs)
   ProcCtx pc;
   for (int k = 0; k < 3; k++) pc.w[k] = b.rot[inst * 3 + k];
-#ifndef PSP_DT_VGPR
-#define PSP_DT_VGPR 1
-#endif
-#if PSP_DT_VGPR
   // dt as a VGPR: a uniform kernel argument is an SGPR pair live across the
   // whole epoch loop, which the allocator spilled to a VGPR lane and reloaded
   // (four v_readlane, the whole 16-byte kernarg group) at each of its ~23
@@ -435,9 +386,6 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     asm volatile("" : "+v"(dtv));
     pc.dt = dtv;
   }
-#else
-  pc.dt = ea.dt;
-#endif
   pc.off = nullptr;
   lane_proc<DOF>(b, *b.shared, inst, lp, pc);
   // the next epoch's IMU inputs are prefetched one epoch ahead (their load
@@ -445,15 +393,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
   uint32_t fl_n = 0;
   double g_n[3] = {0, 0, 0}, a_n[3] = {0, 0, 0};
   auto fetch = [&](int64_t e) {
-#if PSP_FLAG_VGPR
-    // a lane-dependent (always zero) offset keeps the prefetched flag word in a
-    // VGPR until the next epoch reads it: from a uniform address the compiler
-    // moved it to an SGPR at once (readfirstlane + a spill-lane write), waiting
-    // out the load's latency at the top of every epoch
-    fl_n = ea.flags[e + (olane() >> 6)];
-#else
     fl_n = ea.flags[e];
-#endif
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       g_n[k] = ea.gyro[(e * B + inst) * 3 + k];
@@ -461,8 +401,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     }
   };
   if (e_end > e_begin) fetch(e_begin);
-#endif
-  if (PERSIST && PSP_PREFETCH && pre->have) {
+  if (PERSIST && pre->have) {
     using G = PG<DOF>;
     const int l = olane();
 #pragma unroll
@@ -486,73 +425,15 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     ds = c.x;
     ids = c.y;
   }
-#if !PSP_EARLY_INPUTS
-  bool ok = true, nan = false;
-  uint32_t cnt[4] = {0, 0, 0, 0};
-  MeasArgs ma{};
-  ma.v3[0] = ea.p_sens[0]; ma.v3[1] = ea.p_sens[1]; ma.v3[2] = ea.p_sens[2];
-  // the stored rotation rate (PoseUKF.cpp:492-496) lives in pc.w only (a
-  // second copy for the final store was a second set of loop-carried VGPRs)
-  ProcCtx pc;
-  for (int k = 0; k < 3; k++) pc.w[k] = b.rot[inst * 3 + k];
-#ifndef PSP_DT_VGPR
-#define PSP_DT_VGPR 1
-#endif
-#if PSP_DT_VGPR
-  // dt as a VGPR: a uniform kernel argument is an SGPR pair live across the
-  // whole epoch loop, which the allocator spilled to a VGPR lane and reloaded
-  // (four v_readlane, the whole 16-byte kernarg group) at each of its ~23
-  // uses per epoch (tools/isa_hot.py); as a VGPR each use is an operand
-  {
-    double dtv = ea.dt;
-    asm volatile("" : "+v"(dtv));
-    pc.dt = dtv;
-  }
-#else
-  pc.dt = ea.dt;
-#endif
-  pc.off = nullptr;
-  lane_proc<DOF>(b, *b.shared, inst, lp, pc);
-  // the next epoch's IMU inputs are prefetched one epoch ahead (their load
-  // latency overlaps this epoch's arithmetic)
-  uint32_t fl_n = 0;
-  double g_n[3] = {0, 0, 0}, a_n[3] = {0, 0, 0};
-  auto fetch = [&](int64_t e) {
-#if PSP_FLAG_VGPR
-    // a lane-dependent (always zero) offset keeps the prefetched flag word in a
-    // VGPR until the next epoch reads it: from a uniform address the compiler
-    // moved it to an SGPR at once (readfirstlane + a spill-lane write), waiting
-    // out the load's latency at the top of every epoch
-    fl_n = ea.flags[e + (olane() >> 6)];
-#else
-    fl_n = ea.flags[e];
-#endif
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      g_n[k] = ea.gyro[(e * B + inst) * 3 + k];
-      a_n[k] = ea.acc[(e * B + inst) * 3 + k];
-    }
-  };
-  if (e_end > e_begin) fetch(e_begin);
-#endif
   // persistent: the next unit's ticket, claimed behind the first inputs' loads
   // (a wait for those does not wait for the atomic; it has long returned when
   // the next epoch's loads are waited for)
   if constexpr (PERSIST) *next = ticket_issue(ea);
 #pragma unroll 1
   for (int64_t e = e_begin; e < e_end; e++) {
-#if PSP_FLAG_VGPR
-    const uint32_t fl = __builtin_amdgcn_readfirstlane(fl_n);
-#else
     const uint32_t fl = fl_n;
-#endif
     const double g[3] = {g_n[0], g_n[1], g_n[2]}, za[3] = {a_n[0], a_n[1], a_n[2]};
-#ifndef PSP_FETCH_LATE
-#define PSP_FETCH_LATE 0
-#endif
-#if !PSP_FETCH_LATE
     if (e + 1 < e_end) fetch(e + 1);
-#endif
     if (all_finite(g, 3)) {  // integrateMeasurement(RotationRate): checkMeasurment, then store
       for (int k = 0; k < 3; k++) pc.w[k] = g[k];
     } else {
@@ -560,28 +441,9 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     }
     const PoseShared& sh = shared_for_epoch(b);
     UWVK_STAMP(41);
-#if PSP_PAD_MOV > 0 || PSP_PAD_F64 > 0
-    {  // diagnostic (A/B only): N independent VALU instructions per epoch, to
-       // measure what one more 32-bit / fp64 instruction costs the loop
-      double pz[4];
-      int pi[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        pz[i] = (double)(lane_id() + i);
-        pi[i] = lane_id() + i;
-      }
-#pragma unroll
-      for (int i = 0; i < PSP_PAD_MOV; i++) asm volatile("v_mov_b32 %0, %0" : "+v"(pi[i & 3]));
-#pragma unroll
-      for (int i = 0; i < PSP_PAD_F64; i++) asm volatile("v_add_f64 %0, %0, 0" : "+v"(pz[i & 3]));
-    }
-#endif
-    if (!PSP_DIAG_HOT && ((e - ea.first) & 1023) == 1023) psp_fold<DOF>(sm, ds, ids);  // keep d in range
+    if (((e - ea.first) & 1023) == 1023) psp_fold<DOF>(sm, ds, ids);  // keep d in range
     bool sok = psp_predict<DOF, QM, SR>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, st);
     ok = ok && sok;
-#if PSP_FETCH_LATE  // the next epoch's inputs issued after the predict: a shorter live range
-    if (e + 1 < e_end) fetch(e + 1);
-#endif
     if (fl & UWVK_EV_ACC) {
       if (all_finite(za, 3)) {
         do_update<DOF, MK_ACC, SR>(sm, sh, inst, za, sh.log_acc_cov, ma, &sok, ds, ids, st);
@@ -590,7 +452,6 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
         nan = true;
       }
     }
-#ifndef PSP_HOT_ONLY  // diagnostic builds (tools/isa_hot.py): the C3 epoch's predict + acceleration update only
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + inst) * 3;
       if (all_finite(z, 3)) {
@@ -625,7 +486,6 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
       }
     }
     }
-#endif
   }
   if constexpr (PERSIST) {
     // the next unit (its ticket has long returned); a whole instance or a
@@ -634,7 +494,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     const uint32_t un = gridDim.x + ticket_value(ea, *next);
     *next = un;
     const TailUnit tn = ticket_unit(ea, un < ea.units ? un : 0u);
-    pre->have = PSP_PREFETCH && un < ea.units && tn.chunk <= 0;
+    pre->have = un < ea.units && tn.chunk <= 0;
     // every path defines the registers here (zeros when nothing is
     // prefetched), so they are dead through the next unit's epochs
     using G = PG<DOF>;
@@ -679,7 +539,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
 }
 
 template <int DOF, int QM, int EVS, int SR>
-__global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
+__global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const int64_t B = b.batch;
   const TailUnit tu = tail_unit(ea, B);
@@ -701,7 +561,7 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
 // moves to its next unit without a new workgroup dispatch.  The next ticket is
 // taken while the current unit runs (its atomic latency hidden).
 template <int DOF, int QM, int EVS, int SR>
-__global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, PoseShared sh0, EpochArgs ea) {
+__global__ __launch_bounds__(64) void k_psp_epoch_p(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
   // the first unit is the block's own index (no atomic: 3,072 blocks claiming
@@ -785,17 +645,9 @@ static void launch_epoch_dof(hipStream_t st, const PoseBufs& b, const PoseShared
   // QM) and the launch's event kinds (EVS 1: no pressure / ADCP epoch in the
   // range, the C3 workload); a general Q runs the one kernel with everything
   const bool pa = (ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP)) != 0;
-#ifndef PSP_QM_SPLIT
-#define PSP_QM_SPLIT 1
-#endif
-#if !PSP_QM_SPLIT  // A/B: one kernel for every shape and event set (the r03k build)
-  launch_epoch_q<DOF, 0, 0, SR>(st, b, sh, ea, g);
-  (void)pa;
-#else
   if (!sh.q_simple) launch_epoch_q<DOF, 2, 0, SR>(st, b, sh, ea, g);
   else if (pa) launch_epoch_q<DOF, 1, 0, SR>(st, b, sh, ea, g);
   else launch_epoch_q<DOF, 1, 1, SR>(st, b, sh, ea, g);
-#endif
 }
 
 template <int SR>
@@ -914,9 +766,7 @@ int64_t psp_epoch_slots(int dof, int device, bool persist) {
 // epoch each, r02 timeline).  C minimises
 // count / (2 C) + 0.3 C (C - 1) epochs; none below a 10 % gain or when the
 // XCD has under (C + 1) s instances.
-#ifndef PSP_TAIL_OVH
-#define PSP_TAIL_OVH 0.75
-#endif
+constexpr double kTailChunkOverhead = 0.75;  // epochs per extra chunk (r02 timeline)
 int plan_tail(int64_t n, int64_t s, int64_t count) {
   if (s <= 0 || count < 4) return 1;
   const double base = 0.5 * (double)count;
@@ -924,7 +774,7 @@ int plan_tail(int64_t n, int64_t s, int64_t count) {
   int chunks = 1;
   for (int c = 2; c <= 8 && 2 * c <= count; c++) {
     if (n < (c + 1) * s) break;
-    const double cost = (double)count / (2.0 * c) + PSP_TAIL_OVH * c * (c - 1);
+    const double cost = (double)count / (2.0 * c) + kTailChunkOverhead * c * (c - 1);
     if (cost < best) {
       best = cost;
       chunks = c;
@@ -937,16 +787,23 @@ int plan_tail(int64_t n, int64_t s, int64_t count) {
 
 }  // namespace uwvk
 
-#if defined(UWVK_TIMELINE) && PSP_SIDE == 0
-extern "C" int uwvk_debug_read_timeline(unsigned long long* out, long long n) {
+// diagnostic builds only: each side's translation unit keeps its own device
+// symbols, so each exports its own reader (the _r suffix: the right side, SR = 1)
+#if PSP_SIDE == 0
+#define UWVK_PSP_DBG(name) name
+#else
+#define UWVK_PSP_DBG(name) name##_r
+#endif
+
+#if defined(UWVK_TIMELINE)
+extern "C" int UWVK_PSP_DBG(uwvk_debug_read_timeline)(unsigned long long* out, long long n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(uwvk::psp::uwvk_timeline), (size_t)n * 8) != hipSuccess;
 }
 #endif
 
-#if defined(UWVK_STAMPS) && PSP_SIDE == 0
-// diagnostic build only: per-phase cycle sums of the PSP epoch kernel (the
-// left-side kernels; the right side's translation unit keeps its own sums)
-extern "C" int uwvk_debug_read_stamps_psp(unsigned long long* sum, unsigned long long* cnt, int reset) {
+#if defined(UWVK_STAMPS)
+// per-phase cycle sums of this side's PSP kernels
+extern "C" int UWVK_PSP_DBG(uwvk_debug_read_stamps_psp)(unsigned long long* sum, unsigned long long* cnt, int reset) {
   if (hipMemcpyFromSymbol(sum, HIP_SYMBOL(uwvk::uwvk_stamp_sum), 64 * 8) != hipSuccess) return 1;
   if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(uwvk::uwvk_stamp_cnt), 64 * 8) != hipSuccess) return 1;
   if (reset) {

@@ -21,11 +21,19 @@ using namespace uwvk::aug;
 namespace {
 
 using BottomM = Manifold<Seg<SEG_V, 1>, Seg<SEG_S2>>;                        // BottomUKF.hpp:18-21
-using IPoseM = Manifold<Seg<SEG_V, 3>, Seg<SEG_SO3>>;                        // IndirectPoseUKF.hpp:19-22
-using IPoseMarkerM = Manifold<Seg<SEG_V, 3>, Seg<SEG_SO3>, Seg<SEG_V, 3>, Seg<SEG_SO3>>;  // IndirectPoseUKF.cpp:25-29
+// IndirectPoseUKF's orientation_error is an MTK::SO3 like PoseUKF's orientation:
+// SR = 1 the body-frame [+] q exp(d) (MTK's SO3::boxplus, the default), 0 nav-frame
+template <int SR>
+using SO3Seg = Seg<SR ? SEG_SO3R : SEG_SO3>;
+template <int SR>
+using IPoseM = Manifold<Seg<SEG_V, 3>, SO3Seg<SR>>;                          // IndirectPoseUKF.hpp:19-22
+template <int SR>
+using IPoseMarkerM = Manifold<Seg<SEG_V, 3>, SO3Seg<SR>, Seg<SEG_V, 3>, SO3Seg<SR>>;  // IndirectPoseUKF.cpp:25-29
 using BE = Engine<BottomM>;
-using IE = Engine<IPoseM>;
-using IAE = Engine<IPoseMarkerM>;
+template <int SR>
+using IE = Engine<IPoseM<SR>>;
+template <int SR>
+using IAE = Engine<IPoseMarkerM<SR>>;
 
 struct SmallBufs {
   int64_t batch;
@@ -139,15 +147,17 @@ __global__ __launch_bounds__(BE::BLOCK) void k_bottom_normal(SmallBufs b, const 
 
 // ---- IndirectPoseUKF -------------------------------------------------------
 // predictionStepImpl (IndirectPoseUKF.cpp:80-92) + processModel (:7-20)
-__global__ __launch_bounds__(IE::BLOCK) void k_ipose_predict(SmallBufs b, M36 Q, double tau, double dt) {
-  __shared__ double smem[IE::IPB * IE::words];
+template <int SR>
+__global__ __launch_bounds__(IE<SR>::BLOCK) void k_ipose_predict(SmallBufs b, M36 Q, double tau, double dt) {
+  using E = IE<SR>;
+  __shared__ double smem[E::IPB * E::words];
   int64_t inst;
-  IE e = make_engine<IE>(smem, b, nullptr, &inst);
+  E e = make_engine<E>(smem, b, nullptr, &inst);
   load(e, b, inst);
   // Q' = dt^2 (Q with the orientation block R (2/(tau dt) Q_o) R^T), R = mu's rotation
   double Rm[9];
   {
-    const double q[4] = {e.sm[IE::o_mu + 3], e.sm[IE::o_mu + 4], e.sm[IE::o_mu + 5], e.sm[IE::o_mu + 6]};
+    const double q[4] = {e.sm[E::o_mu + 3], e.sm[E::o_mu + 4], e.sm[E::o_mu + 5], e.sm[E::o_mu + 6]};
     qmatrix(q, Rm);
   }
   const double s = 2.0 / (tau * dt), dt2 = dt * dt;
@@ -175,7 +185,10 @@ __global__ __launch_bounds__(IE::BLOCK) void k_ipose_predict(SmallBufs b, M36 Q,
 #pragma unroll
         for (int k = 0; k < 3; k++) d[k] = ntau * l[k] * dt;
         so3_exp(d, ex);
-        qmul(ex, x + 3, r);
+        // orientation_error.boxplus(d, dt) (:17); d is a multiple of log(q), so
+        // exp(d) commutes with q and both sides give the same product
+        if constexpr (SR) qmul(x + 3, ex, r);
+        else qmul(ex, x + 3, r);
 #pragma unroll
         for (int k = 0; k < 4; k++) x[3 + k] = r[k];
       },
@@ -185,26 +198,28 @@ __global__ __launch_bounds__(IE::BLOCK) void k_ipose_predict(SmallBufs b, M36 Q,
 
 // integrateMeasurement(marker features, ...) (IndirectPoseUKF.cpp:94-135):
 // augment with the marker pose, one S2 update per feature, keep the filter block
-__global__ __launch_bounds__(IAE::BLOCK) void k_ipose_visual(SmallBufs b, VisArgs va) {
-  __shared__ double smem[IAE::IPB * IAE::words];
+template <int SR>
+__global__ __launch_bounds__(IAE<SR>::BLOCK) void k_ipose_visual(SmallBufs b, VisArgs va) {
+  using E = IAE<SR>;
+  __shared__ double smem[E::IPB * E::words];
   int64_t inst;
-  IAE e = make_engine<IAE>(smem, b, va.mask, &inst);
+  E e = make_engine<E>(smem, b, va.mask, &inst);
   if (e.live) {
-    for (int i = e.g; i < 144; i += IAE::G) {
+    for (int i = e.g; i < 144; i += E::G) {
       const int r = i / 12, c = i % 12;
       double v = 0.0;
       if (r < 6 && c < 6) v = b.sigma[inst * 36 + r * 6 + c];
       else if (r >= 6 && c >= 6) v = va.cov_marker[(r - 6) * 6 + (c - 6)];
-      e.sm[IAE::o_sig + i] = v;
+      e.sm[E::o_sig + i] = v;
     }
-    for (int k = e.g; k < 14; k += IAE::G)
-      e.sm[IAE::o_mu + k] = k < 7 ? b.mu[inst * 7 + k] : va.marker[inst * va.marker_stride + (k - 7)];
+    for (int k = e.g; k < 14; k += E::G)
+      e.sm[E::o_mu + k] = k < 7 ? b.mu[inst * 7 + k] : va.marker[inst * va.marker_stride + (k - 7)];
   }
   __syncthreads();
-  const bool ok = visual_loop<IAE, 7, true>(e, va, inst);
+  const bool ok = visual_loop<E, 7, true>(e, va, inst);
   if (e.live && ok) {
-    for (int i = e.g; i < 36; i += IAE::G) b.sigma[inst * 36 + i] = e.sm[IAE::o_sig + (i / 6) * 12 + (i % 6)];
-    for (int k = e.g; k < 7; k += IAE::G) b.mu[inst * 7 + k] = e.sm[IAE::o_mu + k];
+    for (int i = e.g; i < 36; i += E::G) b.sigma[inst * 36 + i] = e.sm[E::o_sig + (i / 6) * 12 + (i % 6)];
+    for (int k = e.g; k < 7; k += E::G) b.mu[inst * 7 + k] = e.sm[E::o_mu + k];
   }
   if (e.live && !ok && e.g == 0) b.status[inst] |= UWVK_ST_NOTPD;
 }
@@ -246,6 +261,7 @@ struct uwvk_bottom : SmallHandle {
 struct uwvk_ipose : SmallHandle {
   M36 Q{};
   double tau = 1.0;
+  int so3_right = 1;  // UWVK_OPT_SO3_RIGHT (uwvk_ipose_set_option), default body frame
 };
 
 static void small_destroy(SmallHandle* h) {
@@ -477,6 +493,15 @@ void uwvk_ipose_destroy(uwvk_ipose* h) {
 
 void* uwvk_ipose_stream(const uwvk_ipose* h) { return h ? (void*)h->stream : nullptr; }
 
+uwvk_status uwvk_ipose_set_option(uwvk_ipose* h, int option, int value) {
+  if (!h) return UWVK_EINVAL;
+  if (option == UWVK_OPT_SO3_RIGHT) {
+    h->so3_right = value ? 1 : 0;
+    return UWVK_OK;
+  }
+  return UWVK_EINVAL;
+}
+
 uwvk_status uwvk_ipose_init(uwvk_ipose* h, const double position_error_std[3], const double orientation_error_std[3],
                             double orientation_error_tau, const double* initial_position_error,
                             const double initial_position_error_std[3]) {
@@ -530,8 +555,12 @@ uwvk_status uwvk_ipose_predict(uwvk_ipose* h, double dt) {
   UWVK_DEVICE_GUARD(h);
   if (!h || !(dt > 0.0)) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
-  hipLaunchKernelGGL(k_ipose_predict, dim3(grid_of(h->batch, IE::IPB)), dim3(IE::BLOCK), 0, h->stream, h->bufs(),
-                     h->Q, h->tau, dt);
+  if (h->so3_right)
+    hipLaunchKernelGGL(k_ipose_predict<1>, dim3(grid_of(h->batch, IE<1>::IPB)), dim3(IE<1>::BLOCK), 0, h->stream,
+                       h->bufs(), h->Q, h->tau, dt);
+  else
+    hipLaunchKernelGGL(k_ipose_predict<0>, dim3(grid_of(h->batch, IE<0>::IPB)), dim3(IE<0>::BLOCK), 0, h->stream,
+                       h->bufs(), h->Q, h->tau, dt);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(h->stream));
   return UWVK_OK;
@@ -554,8 +583,12 @@ uwvk_status uwvk_ipose_update_visual(uwvk_ipose* h, int32_t n_features, const do
     return (uwvk_status)st;
   }
   va.ref = h->d_aux;
-  hipLaunchKernelGGL(k_ipose_visual, dim3(grid_of(h->batch, IAE::IPB)), dim3(IAE::BLOCK), 0, h->stream, h->bufs(),
-                     va);
+  if (h->so3_right)
+    hipLaunchKernelGGL(k_ipose_visual<1>, dim3(grid_of(h->batch, IAE<1>::IPB)), dim3(IAE<1>::BLOCK), 0, h->stream,
+                       h->bufs(), va);
+  else
+    hipLaunchKernelGGL(k_ipose_visual<0>, dim3(grid_of(h->batch, IAE<0>::IPB)), dim3(IAE<0>::BLOCK), 0, h->stream,
+                       h->bufs(), va);
   const hipError_t e = hipGetLastError();
   if (hipStreamSynchronize(h->stream) != hipSuccess || e != hipSuccess) return UWVK_EDEVICE;
   return UWVK_OK;

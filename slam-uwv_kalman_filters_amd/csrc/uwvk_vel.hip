@@ -21,7 +21,7 @@ struct VelShared {  // batch-shared model parameters (by value)
   double M[36], Dl[36], Dq[36], Minv[36];
   double weight, buoyancy, cog[3], cob[3];
   double Q0[16];  // process_noise_cov (VelocityUKF.cpp:54-55)
-  double gk, gm[3];  // weight - buoyancy, weight cog - buoyancy cob (VEL_GLIN)
+  double gk, gm[3];  // weight - buoyancy, weight cog - buoyancy cob (restoring forces, v_deriv)
 };
 
 struct VelBufs {
@@ -49,20 +49,13 @@ struct VelEpochArgs {
   int64_t first, count;
 };
 
-// The model parameters reach the RK4 code either by value (kernel argument:
-// SGPRs) or, in k_vel_epoch_g (VEL_LDS), from an LDS copy read through a
-// pointer laundered before every derivative, so that each derivative loads
-// the rows it uses next to their use instead of the whole set being hoisted
-// out of the epoch loop (the by-value matrices were 370 spilled SGPR slots
-// and ~1,250 v_readlane per epoch).
-using LVS = __attribute__((address_space(3))) const VelShared;
+// The model parameters reach the RK4 code through a pointer laundered before
+// every derivative, so that each derivative loads the rows it uses next to
+// their use instead of the whole set being hoisted out of the epoch loop (the
+// by-value matrices were 370 spilled SGPR slots and ~1,250 v_readlane per
+// epoch).
 UWVK_DEV const VelShared& vlaunder(const VelShared& p) { return p; }
-UWVK_DEV LVS& vlaunder(LVS& p) {
-  LVS* q = &p;
-  asm volatile("" : "+v"(q));
-  return *q;
-}
-// (r04) VEL_SMEM: the device copy in the constant address space, its pointer
+// (r04) the device copy in the constant address space, its pointer
 // re-laundered (an SGPR pair) before every derivative, so that the matrices
 // arrive by scalar loads (s_load, the scalar data cache) next to their use
 using GVS = __attribute__((address_space(4))) const VelShared;
@@ -73,20 +66,11 @@ UWVK_DEV GVS& vlaunder(GVS& p) {
 }
 
 // ---- [EXT] ModelSimulation: M nu_dot + C(nu) nu + D(nu) nu + g(q) = tau, RK4 --
-#ifndef VEL_GLIN
-#define VEL_GLIN 1
-#endif
-// (r04) VEL_FASTDIV: fp64 sqrt and division are ~10-15 VALU sequences each on
+// (r04) fp64 sqrt and division are ~10-15 VALU sequences each on
 // gfx950; the Cholesky, the quaternion normalisation and the means' 1/N use
 // 1/sqrt (hardware seed + one Halley step, < 1 ulp) and products instead, the
 // means' x / N as x (1/N) with one FMA correction (correctly rounded quotient).
 // Rounding-level differences from the literal forms, inside the tolerances.
-#ifndef VEL_LAUNDER_MAT
-#define VEL_LAUNDER_MAT 0  // r04 A/B: 892.7-897.6 against 878.0-892.6 M steps/s (profiles/r04/lm/), a tie, not kept
-#endif
-#ifndef VEL_FASTDIV
-#define VEL_FASTDIV 1
-#endif
 UWVK_DEV double v_rsqrt(double x) {
   const double r = __builtin_amdgcn_rsq(x);
   const double e = fma(-(x * r), r, 1.0);
@@ -94,13 +78,9 @@ UWVK_DEV double v_rsqrt(double x) {
 }
 template <int N>
 UWVK_DEV double v_divn(double x) {
-#if VEL_FASTDIV
   constexpr double y = 1.0 / N;
   const double q = x * y;
   return fma(fma(-q, (double)N, x), y, q);
-#else
-  return x / (double)N;
-#endif
 }
 template <class PS>
 UWVK_DEV void v_coriolis(const PS& P, const double nu[6], double c[6]) {
@@ -135,13 +115,7 @@ UWVK_DEV void v_deriv(const PS& P, const double tau[6], const double s[13], doub
   for (int i = 0; i < 4; i++) ds[3 + i] = 0.5 * qd[i];
   double c[6], d[6], g[6], r[6];
   v_coriolis(P, nu, c);
-#if VEL_LAUNDER_MAT
-  // (r04) each matrix's scalar loads after its own launder point: fewer
-  // matrices live in SGPRs at once (spilled to VGPR lanes otherwise)
-  const auto& PD = vlaunder(P);
-#else
   const auto& PD = P;
-#endif
 #pragma unroll
   for (int i = 0; i < 6; i++) {
     double sl = 0, sq = 0;
@@ -152,7 +126,6 @@ UWVK_DEV void v_deriv(const PS& P, const double tau[6], const double s[13], doub
     }
     d[i] = sl + sq;
   }
-#if VEL_GLIN
   // (r04) the restoring forces through one rotation: qrot_inv is linear in its
   // vector and both forces lie along the nav z axis, so with r = R^T e_z
   //   -(fg + fb) = (W - B) r,   -(cog x fg + cob x fb) = (W cog - B cob) x r
@@ -166,24 +139,9 @@ UWVK_DEV void v_deriv(const PS& P, const double tau[6], const double s[13], doub
 #pragma unroll
     for (int i = 0; i < 3; i++) { g[i] = P.gk * r[i]; g[3 + i] = m3[i]; }
   }
-#else
-  const double fw[3] = {0, 0, -P.weight}, fb[3] = {0, 0, P.buoyancy};
-  const double cog[3] = {P.cog[0], P.cog[1], P.cog[2]}, cob[3] = {P.cob[0], P.cob[1], P.cob[2]};
-  double fg[3], fbb[3], mg[3], mb[3];
-  qrot_inv(q, fw, fg);
-  qrot_inv(q, fb, fbb);
-  cross3(cog, fg, mg);
-  cross3(cob, fbb, mb);
-#pragma unroll
-  for (int i = 0; i < 3; i++) { g[i] = -(fg[i] + fbb[i]); g[3 + i] = -(mg[i] + mb[i]); }
-#endif
 #pragma unroll
   for (int i = 0; i < 6; i++) r[i] = tau[i] - c[i] - d[i] - g[i];
-#if VEL_LAUNDER_MAT
-  const auto& PI = vlaunder(P);
-#else
   const auto& PI = P;
-#endif
 #pragma unroll
   for (int i = 0; i < 6; i++) {
     double a = 0;
@@ -219,15 +177,9 @@ UWVK_DEV void v_rk4(const PS& P, const double tau[6], double dt, const double s[
   v_deriv(vlaunder(P), tau, t, k);
 #pragma unroll
   for (int i = 0; i < 13; i++) o[i] = s[i] + (dt / 6.0) * (acc[i] + k[i]);
-#if VEL_FASTDIV
   const double in = v_rsqrt(o[3] * o[3] + o[4] * o[4] + o[5] * o[5] + o[6] * o[6]);
 #pragma unroll
   for (int i = 3; i < 7; i++) o[i] *= in;
-#else
-  const double n = sqrt(o[3] * o[3] + o[4] * o[4] + o[5] * o[5] + o[6] * o[6]);
-#pragma unroll
-  for (int i = 3; i < 7; i++) o[i] /= n;
-#endif
 }
 
 // ---- 4-DOF vector-manifold UKF core in registers [EXT ukfom] -----------------
@@ -243,7 +195,6 @@ UWVK_DEV bool v_chol(const double A[16], double L[16]) {
       double s = A[i * 4 + j];
 #pragma unroll
       for (int k = 0; k < j; k++) s -= L[i * 4 + k] * L[j * 4 + k];
-#if VEL_FASTDIV
       if (i == j) {
         ok = ok && (s > 0.0);
         inv[i] = v_rsqrt(s);
@@ -251,14 +202,6 @@ UWVK_DEV bool v_chol(const double A[16], double L[16]) {
       } else {
         L[i * 4 + j] = s * inv[j];
       }
-#else
-      if (i == j) {
-        ok = ok && (s > 0.0);
-        L[i * 4 + i] = sqrt(s);
-      } else {
-        L[i * 4 + j] = s / L[j * 4 + j];
-      }
-#endif
     }
   }
   return ok;
@@ -299,12 +242,7 @@ UWVK_DEV void v_mean(const double (&X)[N][M], double ref[M]) {
     }
 #pragma unroll
     for (int k = 0; k < M; k++) ref[k] = ref[k] + 1.0 * d[k];
-#if VEL_FASTDIV
   } while (nrm > 1e-12 && ++it < 10000);  // |delta|^2 against (1e-6)^2: no sqrt
-#else
-    nrm = sqrt(nrm);
-  } while (nrm > 1e-6 && ++it < 10000);
-#endif
 }
 
 UWVK_DEV void v_cov(const double (&X)[9][4], const double mean[4], double S[16]) {
@@ -470,18 +408,11 @@ UWVK_DEV void v_store(const VelBufs& b, int64_t i, const double mu[4], const dou
 }
 
 // (r04) the model parameters by scalar loads from the handle's device copy
-// (VEL_SMEM, vlaunder above): the by-value kernel argument (144 doubles of
+// (vlaunder above): the by-value kernel argument (144 doubles of
 // matrices) did not fit the SGPRs, was spilled to VGPR lanes and read back by
 // ~1,000 v_readlane per epoch; C2 534.6-542.1 -> 620.3-620.9 M steps/s
 // (profiles/r04/c2smem/)
-#ifndef VEL_SMEM
-#define VEL_SMEM 1
-#endif
-#if VEL_SMEM
 #define VEL_PARAMS(b, P0) GVS& P = *(GVS*)(b).shared; (void)(P0)
-#else
-#define VEL_PARAMS(b, P0) const VelShared& P = (P0)
-#endif
 
 __global__ __launch_bounds__(64) void k_vel_predict(VelBufs b, VelShared P0, double dt) {
   VEL_PARAMS(b, P0);
@@ -577,22 +508,14 @@ __global__ __launch_bounds__(64) void k_vel_epoch(VelBufs b, VelShared P0, VelEp
 // lane.  4 filters per wave: batch 4096 fills 1024 waves, one per SIMD,
 // where the lane-per-filter kernel occupies 64.
 // ---------------------------------------------------------------------------
-#ifndef VEL_DPP_NOOLD
-#define VEL_DPP_NOOLD 1
-#endif
-// (r04, VEL_DPP_NOOLD) every lane has a source lane under the controls used here
+// (r04) every lane has a source lane under the controls used here
 // (quad_perm, row_half_mirror, row_mirror, all rows and banks), so the old value
 // is never read: mov_dpp leaves it undefined, where update_dpp's explicit 0 cost
 // a v_mov_b32 before every DPP move (~490 per wave-epoch pass of the C2 kernel)
 template <int CTRL>
 UWVK_DEV double vdpp(double v) {
-#if VEL_DPP_NOOLD
   const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
-#else
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
-#endif
   return __hiloint2double(hi, lo);
 }
 // sum over the 16 lanes of this lane's DPP row, identical in every lane
@@ -603,25 +526,15 @@ UWVK_DEV double row_sum16(double v) {
   v = v + vdpp<0x140>(v);  // row_mirror
   return v;
 }
-// (r04) VEL_ROW_DPP: the row broadcast as DPP row_newbcast (lane SRC of each
-// 16-lane row to the whole row, two v_mov_b32_dpp) instead of two ds_bpermute
-// round trips through the LDS crossbar
-#ifndef VEL_ROW_DPP
-#define VEL_ROW_DPP 0  // r04 A/B: 883.7-891.3 against 880.5-885.8 M steps/s (profiles/r04/rb/), a tie, not kept
-#endif
+// lane SRC of each 16-lane row to the whole row (two ds_bpermute; the DPP
+// row_newbcast form was not kept, profiles/EXPERIMENTS.md)
 template <int SRC>
 UWVK_DEV double row_bcast_c(double v) {
   static_assert(SRC >= 0 && SRC < 16, "row lane");
-#if VEL_ROW_DPP
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x150 + SRC, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x150 + SRC, 0xf, 0xf, false);
-  return __hiloint2double(hi, lo);
-#else
   const int ba = (((int)threadIdx.x & ~15) + SRC) * 4;
   const int lo = __builtin_amdgcn_ds_bpermute(ba, __double2loint(v));
   const int hi = __builtin_amdgcn_ds_bpermute(ba, __double2hiint(v));
   return __hiloint2double(hi, lo);
-#endif
 }
 // value of row lane src (0..15) in every lane of the row
 UWVK_DEV double row_bcast(double v, int src) {
@@ -631,9 +544,6 @@ UWVK_DEV double row_bcast(double v, int src) {
   return __hiloint2double(hi, lo);
 }
 
-#ifndef VEL_PT_SEL
-#define VEL_PT_SEL 1
-#endif
 // sigma point g of (mu, L) [EXT ukfom]: 0 = mu, 2j+1 = mu + L_j, 2j+2 = mu - L_j
 UWVK_DEV void vg_point(const double mu[4], const double L[16], int g, double x[4]) {
   const int j = g >= 1 && g < 9 ? (g - 1) >> 1 : 0;
@@ -644,9 +554,7 @@ UWVK_DEV void vg_point(const double mu[4], const double L[16], int g, double x[4
 #pragma unroll
     for (int jj = 1; jj < 4; jj++) {
       c = (j == jj) ? L[k * 4 + jj] : c;
-#if VEL_PT_SEL
       asm volatile("" : "+v"(c));  // keep the selects: as one lane-indexed L[k][j] the compiler put L in scratch
-#endif
     }
     x[k] = sg == 0.0 ? mu[k] : mu[k] + sg * c;
   }
@@ -669,12 +577,7 @@ UWVK_DEV void vg_mean(const double x[M], bool pt, double ref[M]) {
     }
 #pragma unroll
     for (int k = 0; k < M; k++) ref[k] = ref[k] + 1.0 * d[k];
-#if VEL_FASTDIV
   } while (nrm > 1e-12 && ++it < 10000);
-#else
-    nrm = sqrt(nrm);
-  } while (nrm > 1e-6 && ++it < 10000);
-#endif
 }
 
 // Sigma = 1/2 sum_p d_p d_p^T over the point lanes (+ add)
@@ -782,33 +685,12 @@ UWVK_DEV bool vg_update(double mu[4], double S[16], const double z[M], const dou
 
 constexpr int VG = 16;  // lanes per filter
 
-#ifndef VEL_NOHOIST
 // (r04) loop-invariant scalar data (Q0, the DVL covariance) loaded where it is
 // used: hoisted out of the epoch loop it held 50 SGPRs, which the register
 // allocator spilled to VGPR lanes and restored with v_readlane every epoch
-#define VEL_NOHOIST 1
-#endif
 
-#ifndef VEL_LDS
-#define VEL_LDS 0  // r04 A/B: 474.5 against 546.8 M steps/s on C2 (profiles/r04/c2ab/), not kept
-#endif
 __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, VelEpochArgs ea) {
-#if VEL_SMEM
   VEL_PARAMS(b, P0);
-#elif VEL_LDS
-  // the model parameters in LDS (one copy per workgroup), read per derivative
-  __shared__ VelShared sp;
-  {
-    constexpr int NW = (int)(sizeof(VelShared) / 8);
-    const double* src = reinterpret_cast<const double*>(b.shared);
-    double* dst = reinterpret_cast<double*>(&sp);
-    for (int k = (int)threadIdx.x; k < NW; k += 64) dst[k] = src[k];
-    __syncthreads();
-  }
-  LVS& P = *(LVS*)&sp;
-#else
-  const VelShared& P = P0;
-#endif
   const int g = (int)threadIdx.x & (VG - 1);
   const int64_t B = b.batch, inst = (int64_t)blockIdx.x * (64 / VG) + (int)threadIdx.x / VG;
   const bool live = inst < B;
@@ -820,10 +702,6 @@ __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, Vel
   for (int k = 0; k < 13; k++) m[k] = b.model[i * 13 + k];
   double q[4] = {m[3], m[4], m[5], m[6]};
   bool ok = true;
-#ifndef VEL_PREFETCH
-#define VEL_PREFETCH 1
-#endif
-#if VEL_PREFETCH
   // (r04) the next epoch's gyro / efforts / flag word issued one epoch ahead:
   // at one wave per SIMD the loads' latency was exposed at the top of every epoch
   double w_n[3] = {0, 0, 0}, tau_n[6] = {0, 0, 0, 0, 0, 0};
@@ -836,21 +714,13 @@ __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, Vel
     fl_n = ea.flags[e + (g >> 4)];  // a lane-dependent (zero) offset: a VGPR until used
   };
   if (ea.count > 0) fetch(ea.first);
-#endif
   for (int64_t e = ea.first; e < ea.first + ea.count; e++) {
-#if VEL_PREFETCH
     const uint32_t fl = __builtin_amdgcn_readfirstlane(fl_n);
 #pragma unroll
     for (int k = 0; k < 3; k++) { w[k] = w_n[k]; m[10 + k] = w[k]; }
 #pragma unroll
     for (int k = 0; k < 6; k++) tau[k] = tau_n[k];
     if (e + 1 < ea.first + ea.count) fetch(e + 1);
-#else
-#pragma unroll
-    for (int k = 0; k < 3; k++) { w[k] = ea.gyro[(e * B + i) * 3 + k]; m[10 + k] = w[k]; }
-#pragma unroll
-    for (int k = 0; k < 6; k++) tau[k] = ea.efforts[(e * B + i) * 6 + k];
-#endif
     // predict (VelocityUKF.cpp:115-128): point lanes integrate their sigma
     // point, lane 9 the side model, in one RK4 pass
     double L[16], x[4];
@@ -877,35 +747,23 @@ __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, Vel
     }
     vg_mean<4>(x, pt, mu);
     vg_cov(x, mu, pt, S);
-#if VEL_NOHOIST
     {  // Q0 by scalar loads here, not hoisted out of the loop into 32 SGPRs held across it
       const auto& PQ = vlaunder(P);
 #pragma unroll
       for (int k = 0; k < 16; k++) S[k] += ea.dt * PQ.Q0[k];
     }
-#else
-#pragma unroll
-    for (int k = 0; k < 16; k++) S[k] += ea.dt * P.Q0[k];
-#endif
     if (side) {
 #pragma unroll
       for (int k = 0; k < 13; k++) m[k] = n13[k];
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) q[k] = row_bcast_c<9>(side ? m[3 + k] : 0.0);
-#if !VEL_PREFETCH
-    const uint32_t fl = ea.flags[e];
-#endif
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + i) * 3;
       const double zz[3] = {z[0], z[1], z[2]};
-#if VEL_NOHOIST
       const double* Rd = ea.dvl_cov;
       asm volatile("" : "+s"(Rd));  // R loaded in the branch, not held in SGPRs across the loop
       ok = vg_update<3, 0>(mu, S, zz, Rd, g) && ok;
-#else
-      ok = vg_update<3, 0>(mu, S, zz, ea.dvl_cov, g) && ok;
-#endif
     }
     if (fl & UWVK_EV_PRESSURE) {
       const double zz[1] = {ea.pressure[(int64_t)ea.p_index[e] * B + i]};

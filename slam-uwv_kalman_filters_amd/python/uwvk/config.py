@@ -255,7 +255,16 @@ def from_dict(d, base_pose=None, base_uwv=None):
         if k in ("so3_right", "dense_sigma", "literal_apply_delta"):
             if not isinstance(v, bool):
                 raise ConfigError("engine.%s: expected true / false, got %r" % (k, v))
-        elif isinstance(v, bool) or not isinstance(v, int) or v < (-1 if k == "persist" else 0):
+        elif k == "persist":
+            # UWVK_OPT_PERSIST is 0 / 1 (a boolean in YAML reads the same)
+            if not (isinstance(v, bool) or (isinstance(v, int) and v in (0, 1))):
+                raise ConfigError("engine.persist: expected 0 / 1 or true / false, got %r" % (v,))
+            eng[k] = int(v)
+        elif k == "tail_slots":
+            # UWVK_OPT_TAIL_SLOTS: 0 runtime occupancy, > 0 blocks per XCD, < 0 (-1) no tail spreading
+            if isinstance(v, bool) or not isinstance(v, int) or v < -1:
+                raise ConfigError("engine.tail_slots: expected an integer >= -1, got %r" % (v,))
+        elif isinstance(v, bool) or not isinstance(v, int) or v < 0:
             raise ConfigError("engine.%s: expected a non-negative integer, got %r" % (k, v))
     return FilterConfig(pose, uwv, eng, VisualLandmarks(vis) if vis is not None else None)
 
@@ -287,7 +296,10 @@ def dump(cfg, path):
 
 
 def apply_engine_options(batch, opts):
-    """Engine options on a PoseUKFBatch (each maps to a uwvk_pose_set_option)."""
+    """Engine options on a PoseUKFBatch (each maps to a uwvk_pose_set_option).
+    Applied after the caller's own settings, so an option the file sets wins
+    over the same option set on the command line (bench.py warns when both
+    are given and differ)."""
     for k, v in opts.items():
         if k == "so3_right":
             batch.set_so3_right(v)
@@ -300,7 +312,6 @@ def apply_engine_options(batch, opts):
         elif k == "tail_chunks":
             batch.set_tail_chunks(v)
         elif k == "persist":
-            if v >= 0:
-                batch.set_persist(v)
+            batch.set_persist(int(v))
         else:
             raise ConfigError("engine.%s: unknown option" % k)

@@ -40,11 +40,11 @@ SYMBOLS = [
     "uwvk_bottom_create", "uwvk_bottom_destroy", "uwvk_bottom_stream", "uwvk_bottom_init",
     "uwvk_bottom_set_process_noise", "uwvk_bottom_set_velocity", "uwvk_bottom_predict", "uwvk_bottom_update_range",
     "uwvk_bottom_update_normal", "uwvk_bottom_get_state", "uwvk_bottom_get_status",
-    "uwvk_ipose_create", "uwvk_ipose_destroy", "uwvk_ipose_stream", "uwvk_ipose_init",
+    "uwvk_ipose_create", "uwvk_ipose_destroy", "uwvk_ipose_stream", "uwvk_ipose_init", "uwvk_ipose_set_option",
     "uwvk_ipose_set_pose_reference", "uwvk_ipose_predict", "uwvk_ipose_update_visual",
     "uwvk_ipose_get_corrected_pose", "uwvk_ipose_get_state", "uwvk_ipose_get_status",
     "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots", "uwvk_pose_epoch_qshape", "uwvk_pose_timer_mark", "uwvk_pose_timer_elapsed",
-    "uwvk_xcd_round_robin", "uwvk_synth_normal",
+    "uwvk_xcd_round_robin", "uwvk_synth_normal", "uwvk_synth_normal_at",
 ]
 
 _LIB = None
@@ -172,7 +172,9 @@ class PoseUKFBatch:
         _chk(self.L.uwvk_pose_set_option(self.h, 3, int(slots)), "set_option")
 
     def set_so3_right(self, on=True):
-        """UWVK_OPT_SO3_RIGHT: body-frame SO3 boxplus q exp(d) on every path (PSP, dense, literal), like the oracle's or_set_so3_right."""
+        """UWVK_OPT_SO3_RIGHT: body-frame SO3 boxplus q exp(d) (the default, MTK's
+        SO3::boxplus) or, with on=False, the nav-frame exp(d) q, on every path
+        (PSP, dense, literal), like the oracle's or_set_so3_right."""
         _chk(self.L.uwvk_pose_set_option(self.h, 5, int(bool(on))), "set_option")
 
     def set_tail_chunks(self, chunks):

@@ -16,9 +16,9 @@ def shard_range(rank, world, global_batch):
     return lo, hi
 
 
-def _qlog_delta(q, t, right=False):
-    """log(q * conj(t)) (nav frame, the left SO3 side) or, right=True,
-    log(conj(t) * q) (body frame, UWVK_OPT_SO3_RIGHT) for arrays of unit
+def _qlog_delta(q, t, right=True):
+    """log(conj(t) * q) (body frame, the right SO3 side: the default,
+    UWVK_OPT_SO3_RIGHT) or, right=False, log(q * conj(t)) (nav frame) for arrays of unit
     quaternions (w, x, y, z): the orientation error in the frame the filter's
     covariance is expressed in.  The two products differ only in the sign of
     the cross term."""
@@ -32,9 +32,10 @@ def _qlog_delta(q, t, right=False):
     return k[..., None] * v
 
 
-def ensemble_stats_host(x, P, truth, right=False):
+def ensemble_stats_host(x, P, truth, right=True):
     """Host reference of uwvk_pose_ensemble_stats (same layout of `out`);
-    right: the handle's SO3 side (the orientation error log(t^-1 q))."""
+    right: the handle's SO3 side (True, the default: the orientation error
+    log(t^-1 q); False: log(q t^-1))."""
     store = x.shape[1]
     out = np.zeros(3 * store + 2)
     out[:store] = x.sum(0)

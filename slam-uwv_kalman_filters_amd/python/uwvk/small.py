@@ -109,6 +109,11 @@ class IndirectPoseUKFBatch(_Small):
         Q = _f64(Q)
         _chk(self._fn("set_process_noise")(self.h, _p(Q)), "ipose_set_process_noise")
 
+    def set_so3_right(self, on=True):
+        """UWVK_OPT_SO3_RIGHT of the orientation_error: body frame q exp(d) (the
+        default, MTK's SO3::boxplus) or, on=False, nav frame exp(d) q."""
+        _chk(self._fn("set_option")(self.h, 5, int(bool(on))), "ipose_set_option")
+
     def set_pose_reference(self, pose):
         pose = _per(pose, self.batch, (7,))
         _chk(self._fn("set_pose_reference")(self.h, _p(pose)), "ipose_set_pose_reference")

@@ -239,58 +239,101 @@ def normals(seed, first, batch, stream, shape_tail):
     return out.reshape((batch,) + tuple(shape_tail))
 
 
+def _normal_rec_lib(seed, first, batch, stream, offset, records, group):
+    """uwvk_synth_normal_at (record-major) through the C ABI, or None."""
+    import ctypes as C
+    try:
+        from . import engine
+        L = engine.lib()
+        fn = L.uwvk_synth_normal_at
+    except (OSError, AttributeError):
+        return None
+    out = np.empty((records, batch, group))
+    rc = fn(C.c_uint64(seed), C.c_int64(first), C.c_int64(batch), C.c_uint32(stream), C.c_int64(offset),
+            C.c_int64(records * group), C.c_int32(group), out.ctypes.data_as(C.c_void_p))
+    if rc != 0:
+        raise ValueError("uwvk_synth_normal_at: status %d" % rc)
+    return out
+
+
+def normals_rec(seed, first, batch, stream, offset, records, group):
+    """[records, batch, group]: variates offset .. offset + records * group of
+    each instance's stream, record-major (the logs' [epoch][instance][component]
+    layout): normals(...)[j, offset + r * group + g] = out[r, j, g]."""
+    if records == 0 or batch == 0:
+        return np.zeros((records, batch, group))
+    out = _normal_rec_lib(seed, first, batch, stream, offset, records, group)
+    if out is None:
+        full = _normal_np(seed, np.arange(first, first + batch), stream, offset + records * group)[:, offset:]
+        out = np.ascontiguousarray(full.reshape(batch, records, group).transpose(1, 0, 2))
+    return out
+
+
 def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_instance=0, cfg=None,
-                  dropout_on=30.0, dropout_off=10.0, adcp_every=1000, efforts_velocity_only=False):
+                  dropout_on=30.0, dropout_off=10.0, adcp_every=1000, efforts_velocity_only=False, epoch0=0):
     """Per-instance noisy measurement log.  Returns a dict of numpy arrays.
 
     mode C1/C3: 1 kHz IMU + 5 Hz DVL.
     mode C4: C3 + 10 Hz pressure + 1 Hz ADCP x 4 cells (weights 0, 1/3, 2/3, 1,
              d2p95 gate) + DVL drop-outs (30 s on / 10 s off) with 10 Hz
              BodyEfforts updates during the drop-out.
+    epoch0: the log's epochs [epoch0, epoch0 + epochs) of the mission that
+             starts at epoch 0 -- bitwise the same rows (flags by absolute time,
+             the noise streams' same variates) as a slice of the whole log, with
+             the sensor index arrays counted from the segment's first sample;
+             `truth` is the whole mission's (absolute epoch index).
     """
     cfg = cfg or default_pose_config()
     uwv = default_uwv()
-    tr = Truth(epochs, dt)
-    k = np.arange(1, epochs + 1)  # measurement sample index (t = k dt)
-    flags = np.full(epochs, abi.EV_ACC, np.uint32)
-    t_meas = k * dt
-    dropout = np.zeros(epochs, bool)
+    total = epoch0 + epochs
+    tr = Truth(total, dt)
+    kall = np.arange(1, total + 1)  # measurement sample index (t = k dt)
+    flags_all = np.full(total, abi.EV_ACC, np.uint32)
+    t_meas = kall * dt
+    dropout = np.zeros(total, bool)
     if mode == "C4":
         dropout = np.mod(t_meas, dropout_on + dropout_off) >= dropout_on - 1e-12
-    dvl_due = (k % 200 == 0) & ~dropout
-    flags[dvl_due] |= abi.EV_DVL
+    dvl_due = (kall % 200 == 0) & ~dropout
+    flags_all[dvl_due] |= abi.EV_DVL
     if mode == "C4":
-        flags[k % 100 == 0] |= abi.EV_PRESSURE
-        flags[k % adcp_every == 0] |= abi.EV_ADCP
-        flags[(k % 100 == 0) & dropout] |= abi.EV_EFFORTS
+        flags_all[kall % 100 == 0] |= abi.EV_PRESSURE
+        flags_all[kall % adcp_every == 0] |= abi.EV_ADCP
+        flags_all[(kall % 100 == 0) & dropout] |= abi.EV_EFFORTS
         if efforts_velocity_only:
-            flags[(flags & abi.EV_EFFORTS) != 0] |= abi.EV_EFFORTS_VELOCITY_ONLY
+            flags_all[(flags_all & abi.EV_EFFORTS) != 0] |= abi.EV_EFFORTS_VELOCITY_ONLY
+    flags = np.ascontiguousarray(flags_all[epoch0:])
+    k = kall[epoch0:]
 
     def idx_of(bit):
         sel = (flags & bit) != 0
         ix = np.full(epochs, -1, np.int32)
         ix[sel] = np.arange(sel.sum(), dtype=np.int32)
-        return ix, k[sel]
+        before = int(((flags_all[:epoch0] & bit) != 0).sum())  # samples of this sensor before the segment
+        return ix, k[sel], before
 
-    dvl_index, dvl_k = idx_of(abi.EV_DVL)
-    p_index, p_k = idx_of(abi.EV_PRESSURE)
-    a_index, a_k = idx_of(abi.EV_ADCP)
-    e_index, e_k = idx_of(abi.EV_EFFORTS)
+    dvl_index, dvl_k, dvl_0 = idx_of(abi.EV_DVL)
+    p_index, p_k, p_0 = idx_of(abi.EV_PRESSURE)
+    a_index, a_k, a_0 = idx_of(abi.EV_ADCP)
+    e_index, e_k, e_0 = idx_of(abi.EV_EFFORTS)
 
-    def normal(stream, shape_tail):
-        # counter-based: one stream per (instance, measurement kind)
-        return normals(seed, first_instance, batch, stream, shape_tail)
+    def rec(stream, first_record, records, group):
+        # counter-based: one stream per (instance, measurement kind), record-major
+        return normals_rec(seed, first_instance, batch, stream, first_record * group, records, group)
 
     sg = 1e-4 / np.sqrt(dt)
     sa = 1e-3 / np.sqrt(dt)
-    gyro = tr.gyro[k][None] + sg * normal(0, (epochs, 3))
-    acc = tr.acc[k][None] + sa * normal(1, (epochs, 3))
-    gyro = np.ascontiguousarray(gyro.transpose(1, 0, 2))
-    acc = np.ascontiguousarray(acc.transpose(1, 0, 2))
-    dvl = tr.dvl[dvl_k][None] + 0.01 * normal(2, (len(dvl_k), 3))
-    dvl = np.ascontiguousarray(dvl.transpose(1, 0, 2))
-    pressure = tr.pressure[p_k][None] + 100.0 * normal(3, (len(p_k),))
-    pressure = np.ascontiguousarray(pressure.T)
+    gyro = rec(0, epoch0, epochs, 3)  # [epochs][batch][3]
+    gyro *= sg
+    gyro += tr.gyro[k][:, None, :]
+    acc = rec(1, epoch0, epochs, 3)
+    acc *= sa
+    acc += tr.acc[k][:, None, :]
+    dvl = rec(2, dvl_0, len(dvl_k), 3)
+    dvl *= 0.01
+    dvl += tr.dvl[dvl_k][:, None, :]
+    pressure = np.ascontiguousarray(rec(3, p_0, len(p_k), 1)[..., 0])  # [n][batch]
+    pressure *= 100.0
+    pressure += tr.pressure[p_k][:, None]
     weights = np.array([0.0, 1.0 / 3.0, 2.0 / 3.0, 1.0])
     cells = len(weights)
     vn = tr.v_nav[a_k]
@@ -299,21 +342,22 @@ def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_in
     rb = _rotz_T(tr.psi[a_k], vn - wvb3)[:, None, :2]
     rw = _rotz_T(tr.psi[a_k], vn - wv3)[:, None, :2]
     adcp_true = weights[None, :, None] * rb + (1 - weights)[None, :, None] * rw  # [n, cells, 2]
-    adcp = adcp_true[None] + 0.05 * normal(4, (len(a_k), cells, 2))
-    adcp = np.ascontiguousarray(adcp.transpose(1, 2, 0, 3))  # [n][cells][batch][2]
+    adcp = rec(4, a_0, len(a_k), cells * 2).reshape(len(a_k), batch, cells, 2).transpose(0, 2, 1, 3)
+    adcp = np.ascontiguousarray(adcp_true[:, :, None, :] + 0.05 * adcp)  # [n][cells][batch][2]
     M, Dl, Dq = uwv_arrays(uwv)
     vel6 = np.concatenate([_rotz_T(tr.psi[e_k], tr.v_nav[e_k] - wv3), np.zeros((len(e_k), 2)),
                            tr.r[e_k][:, None]], -1)
     acc6 = np.concatenate([_rotz_T(tr.psi[e_k], tr.a_nav[e_k]), np.zeros((len(e_k), 3))], -1)
     tau_true = calc_efforts_np(M, Dl, Dq, acc6, vel6)
     std = np.array(cfg.model_noise_parameters.body_efforts_std[:])
-    efforts = tau_true[None] + std * normal(5, (len(e_k), 6))
-    efforts = np.ascontiguousarray(efforts.transpose(1, 0, 2))
+    efforts = rec(5, e_0, len(e_k), 6)  # [n][batch][6]
+    efforts *= std
+    efforts += tau_true[:, None, :]
 
     # initial pose estimate, perturbed per instance
     pos_cov = np.diag([1.0, 1.0, 0.25])
     rot_cov = np.diag([1e-4, 1e-4, 2.5e-3])
-    n0 = normal(6, (6,))
+    n0 = normals(seed, first_instance, batch, 6, (6,))
     pos0 = tr.pos[0][None] + n0[:, :3] * np.sqrt(np.diag(pos_cov))
     rv = n0[:, 3:] * np.sqrt(np.diag(rot_cov))
     th = np.linalg.norm(rv, axis=1)
@@ -321,7 +365,7 @@ def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_in
     dq = np.concatenate([np.cos(th / 2)[:, None], s[:, None] * rv], 1)
     q0 = _qmul(dq, np.broadcast_to(tr.q[0], dq.shape))
     return dict(
-        mode=mode, dof=dof, batch=batch, epochs=epochs, dt=dt, flags=flags,
+        mode=mode, dof=dof, batch=batch, epochs=epochs, epoch0=epoch0, dt=dt, flags=flags,
         gyro=gyro, acc=acc, acc_cov=np.eye(3) * sa ** 2,
         dvl_index=dvl_index, dvl=dvl, dvl_cov=np.eye(3) * 0.01 ** 2,
         pressure_index=p_index, pressure=pressure, pressure_cov=100.0 ** 2, pressure_sensor_in_imu=np.zeros(3),

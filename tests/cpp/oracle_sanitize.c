@@ -113,7 +113,7 @@ static int pose_run(int dof, int right) {
   for (int i = 0; i < dof * dof; i++)
     if (!isfinite(P[i])) bad |= 1;
   free(f);
-  or_set_so3_right(0);
+  or_set_so3_right(1); /* back to the default side */
   return bad;
 }
 

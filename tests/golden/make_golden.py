@@ -9,6 +9,10 @@ known-answer tests.  Each .npz holds the INPUTS (the full measurement log and
 initial state) and checkpointed OUTPUTS (mean every `mu_every` epochs,
 covariance every `cov_every` epochs), so a fixture is self-contained.
 
+SO3 side: pose_*.npz run the default right side (q exp(d),
+MTK's SO3::boxplus); pose_*_left.npz the same logs on the left side (exp(d) q,
+the option).  Each file records its side in `so3_right`.
+
     python tests/golden/make_golden.py
 """
 import os
@@ -39,28 +43,30 @@ CASES = {
 }
 
 
-def make_pose(name, c):
+def make_pose(name, c, right=True):
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     log = synth.make_pose_log(c["batch"], c["epochs"], mode=c["mode"], dof=c["dof"], **c.get("kw", {}))
     o = O.OraclePoseBatch(c["batch"], c["dof"])
-    o.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
-    o.set_process_noise_from_config(cfg, log["dt"])
     mus, covs, mu_ep, cov_ep = [], [], [], []
     counts = np.zeros((c["batch"], 4), np.uint32)
-    for e0 in range(0, c["epochs"], c["mu_every"]):
-        counts += o.run_log(log, e0, c["mu_every"])
-        x, P = o.get_state()
-        e = e0 + c["mu_every"]
-        mus.append(x)
-        mu_ep.append(e)
-        if e % c["cov_every"] == 0:
-            covs.append(P)
-            cov_ep.append(e)
+    with O.so3_side(right):
+        o.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+        o.set_process_noise_from_config(cfg, log["dt"])
+        for e0 in range(0, c["epochs"], c["mu_every"]):
+            counts += o.run_log(log, e0, c["mu_every"])
+            x, P = o.get_state()
+            e = e0 + c["mu_every"]
+            mus.append(x)
+            mu_ep.append(e)
+            if e % c["cov_every"] == 0:
+                covs.append(P)
+                cov_ep.append(e)
     out = {k: np.asarray(log[k]) for k in LOG_KEYS}
     out.update(dof=c["dof"], epochs=c["epochs"], dt=log["dt"], mu=np.stack(mus), mu_epochs=np.array(mu_ep),
-               cov=np.stack(covs), cov_epochs=np.array(cov_ep), accept_counts=counts)
-    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
-    print(name, "mu", out["mu"].shape, "cov", out["cov"].shape, "accepts", counts.tolist())
+               cov=np.stack(covs), cov_epochs=np.array(cov_ep), accept_counts=counts, so3_right=int(right))
+    fn = name + ("" if right else "_left")
+    np.savez_compressed(os.path.join(HERE, fn + ".npz"), **out)
+    print(fn, "mu", out["mu"].shape, "cov", out["cov"].shape, "accepts", counts.tolist())
 
 
 def make_vel():
@@ -87,6 +93,7 @@ def make_vel():
 
 
 if __name__ == "__main__":
-    for name, c in CASES.items():
-        make_pose(name, c)
+    for right in (True, False):
+        for name, c in CASES.items():
+            make_pose(name, c, right)
     make_vel()

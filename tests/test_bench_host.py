@@ -12,9 +12,14 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
+# committed counter passes: the default (right SO3 side) kernel and the left option's
+PMC_WORKLOADS = ["C3-dof53-b65536", "C3-dof53-b65536-left"]
+
+
+@pytest.mark.parametrize("workload", PMC_WORKLOADS)
 @pytest.mark.parametrize("steps", [20, 200])
-def test_committed_counter_passes_give_executed_roofline(steps):
-    e = bench.pmc_entry("C3-dof53-b65536", steps)
+def test_committed_counter_passes_give_executed_roofline(steps, workload):
+    e = bench.pmc_entry(workload, steps)
     assert e.get("epochs_per_launch") == steps, "no counter pass of the %d-epoch launch committed" % steps
     pw = e["per_wave_epoch"]
     # the counters come from the timed launch of 65,536 instances (normalised per
@@ -59,7 +64,7 @@ def test_bench_line_fields_documented():
                 '"effective_tflops"', '"counters"', '"timing"'):
         assert key in src
     d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
-    assert "C3-dof53-b65536-e20" in d
+    assert "C3-dof53-b65536-e20" in d and "C3-dof53-b65536-left-e20" in d
 
 
 # ---- multi-GPU launch logic (no GPU: spawned scripts stand in for the ranks) ----

@@ -48,8 +48,9 @@ uwv:
                    [0, 0, 0, 20, 0, 0], [0, 0, 0, 0, 30, 0], [0, 0, 0, 0, 0, 30]]
   weight: 2000
 engine:
-  so3_right: true
-  tail_slots: 0
+  so3_right: false
+  tail_slots: -1
+  persist: false
 """
 
 
@@ -65,7 +66,7 @@ def test_yaml_fields_and_defaults():
     assert (c.pose.location.latitude, c.pose.location.altitude) == (0.9, 5.0)
     assert c.uwv.inertia_matrix[0] == 210.0 and c.uwv.inertia_matrix[7] == 250.0
     assert list(c.uwv.damping_matrices[0]) == list(synth.default_uwv().damping_matrices[0])
-    assert c.engine == {"so3_right": True, "tail_slots": 0}
+    assert c.engine == {"so3_right": False, "tail_slots": -1, "persist": 0}
 
 
 @pytest.mark.parametrize("doc,where", [
@@ -76,7 +77,9 @@ def test_yaml_fields_and_defaults():
     ("uwv: {damping_matrices: [[1, 2]]}", "uwv.damping_matrices: expected 2 entries"),
     ("uwv: {inertia_matrix: [[1, 2, 3]]}", "uwv.inertia_matrix: expected 36 values, got 3"),
     ("engine: {so3_right: 1}", "engine.so3_right: expected true / false"),
-    ("engine: {tail_slots: -2}", "engine.tail_slots: expected a non-negative integer"),
+    ("engine: {tail_slots: -2}", "engine.tail_slots: expected an integer >= -1"),
+    ("engine: {persist: -1}", "engine.persist: expected 0 / 1"),
+    ("engine: {tail_chunks: -1}", "engine.tail_chunks: expected a non-negative integer"),
     ("engine: {warp_speed: 9}", "engine.warp_speed: unknown option"),
     ("filters: {}", "filters: unknown section"),
     ("pose_config: {location: {latitude: .nan}}", "pose_config.location.latitude: NaN"),
@@ -165,15 +168,18 @@ def test_apply_engine_options_calls():
     class Fake:
         def __getattr__(self, n):
             return lambda *a: calls.append((n,) + a)
-    config.apply_engine_options(Fake(), {"so3_right": True, "dense_sigma": False, "persist": -1, "tail_chunks": 2})
-    assert calls == [("set_so3_right", True), ("set_dense_sigma", False), ("set_tail_chunks", 2)]
+    config.apply_engine_options(Fake(), {"so3_right": True, "dense_sigma": False, "persist": 1, "tail_chunks": 2,
+                                         "tail_slots": -1})
+    assert calls == [("set_so3_right", True), ("set_dense_sigma", False), ("set_persist", 1), ("set_tail_chunks", 2),
+                     ("set_tail_slots", -1)]
 
 
 @pytest.mark.gpu
 def test_gpu_filter_from_file_matches_oracle(tmp_path):
     """A filter configured from a file (non-default noise, location, hydrostatics,
-    right SO3 side) through the HIP engine against the oracle given the same
-    parsed structs, over a 40-epoch C3 log."""
+    left SO3 side) through the HIP engine against the oracle given the same
+    parsed structs, over a 40-epoch C3 log.  The file selects the left SO3
+    side (the non-default option) and turns tail spreading off."""
     from uwvk import engine
     import oracle_ctypes as O
     from helpers import cov_err, state_err
@@ -187,7 +193,7 @@ def test_gpu_filter_from_file_matches_oracle(tmp_path):
     g = engine.PoseUKFBatch(B, dof)
     config.apply_engine_options(g, c.engine)
     o = O.OraclePoseBatch(B, dof)
-    with O.so3_right():
+    with O.so3_left():
         for f in (o, g):
             f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], c.pose, c.uwv)
             f.set_process_noise_from_config(c.pose, log["dt"])
@@ -199,7 +205,7 @@ def test_gpu_filter_from_file_matches_oracle(tmp_path):
     assert se < TOL_LOG and ce < TOL_LOG, (se, ce)
     # and the file's values mattered: the default config gives a different state
     d = engine.PoseUKFBatch(B, dof)
-    d.set_so3_right(True)
+    d.set_so3_right(False)
     d.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], synth.default_pose_config(),
                        synth.default_uwv())
     d.set_process_noise_from_config(synth.default_pose_config(), log["dt"])

@@ -2,7 +2,9 @@
 
 CPU: the oracle reproduces its committed fixtures (regression pin of the
 oracle).  GPU (-m gpu): the HIP engine, through the C ABI, reproduces the
-same checkpoints within the fp64 log tolerance."""
+same checkpoints within the fp64 log tolerance.  Each pose fixture records
+its SO3 side (`so3_right`: pose_*.npz the default right side, pose_*_left.npz
+the left option); oracle and engine run on that side."""
 import glob
 import os
 
@@ -39,6 +41,15 @@ def _run(f, g, chunk, runner):
     return np.stack(mus), np.stack(covs)
 
 
+def test_fixture_sides():
+    """Both sides are pinned: every default-side fixture has its left twin."""
+    right = [p for p in POSE if not p.endswith("_left.npz")]
+    assert right and all(int(np.load(p)["so3_right"]) == 1 for p in right)
+    for p in right:
+        left = p[:-4] + "_left.npz"
+        assert left in POSE and int(np.load(left)["so3_right"]) == 0
+
+
 @pytest.mark.parametrize("path", POSE, ids=[os.path.basename(p) for p in POSE])
 def test_oracle_reproduces_fixture(path):
     g = np.load(path, allow_pickle=False)
@@ -46,10 +57,11 @@ def test_oracle_reproduces_fixture(path):
     dof, B = int(g["dof"]), g["mu"].shape[1]
     o = O.OraclePoseBatch(B, dof)
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
-    o.init_from_config(g["pos0"], g["pos_cov"], g["rot0"], g["rot_cov"], cfg, uwv)
-    o.set_process_noise_from_config(cfg, log["dt"])
     chunk = int(g["mu_epochs"][0])
-    mus, covs = _run(o, g, chunk, lambda e0, n: o.run_log(log, e0, n))
+    with O.so3_side(bool(g["so3_right"])):
+        o.init_from_config(g["pos0"], g["pos_cov"], g["rot0"], g["rot_cov"], cfg, uwv)
+        o.set_process_noise_from_config(cfg, log["dt"])
+        mus, covs = _run(o, g, chunk, lambda e0, n: o.run_log(log, e0, n))
     for k in range(len(mus)):
         P = g["cov"][-1]
         assert state_err(mus[k], g["mu"][k], P, dof).max() < 1e-11
@@ -85,6 +97,7 @@ def test_engine_reproduces_fixture(path, engine_path):
     log = _log(g)
     dof, B = int(g["dof"]), g["mu"].shape[1]
     f = engine.PoseUKFBatch(B, dof)
+    f.set_so3_right(bool(g["so3_right"]))
     f.set_dense_sigma(engine_path == "dense")
     f.set_literal_apply_delta(engine_path == "literal")
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()

@@ -1,12 +1,13 @@
-"""GPU parity with the body-frame (right) SO3 boxplus, the largest unpinned
-semantic (PoseUKF.cpp:31-32, :451): the engine under
-UWVK_OPT_SO3_RIGHT against the oracle under or_set_so3_right(1), for the
-predict, every update kind and multi-epoch logs, on all three engine paths:
-psp (the default: the SR = 1 instantiations of the PSP kernels, with
-apply_delta's T = R(exp d)^T), dense (the literal kernels)
-and literal (the literal kernels with ukfom's literal apply_delta re-spread).
-Whichever side the real MTK uses, the fast path reproduces it.  Tolerances as
-in test_gpu_parity.py."""
+"""GPU parity on both sides of the SO3 boxplus, the largest unpinned semantic
+(SURVEY 8(c) item 5): right, q exp(d) -- MTK's SO3::boxplus and the default
+since r05 (PoseState.hpp:15, PoseUKF.cpp:32) -- and left, exp(d) q, the
+option.  The engine with UWVK_OPT_SO3_RIGHT = side against the oracle under
+or_set_so3_right(side), for the predict, every update kind and multi-epoch
+logs, on all three engine paths: psp (the default: the SR instantiations of
+the PSP kernels, with apply_delta's T = R(exp d)^T on the right, R(exp d) on
+the left), dense (the literal kernels) and literal (the
+literal kernels with ukfom's literal apply_delta re-spread).  Tolerances as in
+test_gpu_parity.py."""
 import numpy as np
 import pytest
 
@@ -27,30 +28,33 @@ def eng():
     return engine
 
 
-class RightOracle:
-    """OraclePoseBatch whose every call runs with the right boxplus (the
+class SideOracle:
+    """OraclePoseBatch whose every call runs with the given boxplus side (the
     oracle's switch is process-wide: set for the call, restored after)."""
 
-    def __init__(self, *a):
+    def __init__(self, right, *a):
+        self.right = right
         self.o = O.OraclePoseBatch(*a)
 
     def __getattr__(self, name):
         fn = getattr(self.o, name)
 
         def call(*a, **k):
-            with O.so3_right():
+            with O.so3_side(self.right):
                 return fn(*a, **k)
         return call
 
 
 PATHS = ["psp", "dense", "literal"]
+SIDES = ["right", "left"]
 
 
-def _pair(eng, batch, dof, mode="C3", epochs=10, path="psp"):
+def _pair(eng, batch, dof, mode="C3", epochs=10, path="psp", side="right"):
     cfg, uwv, log = pose_setup(batch, dof, mode, epochs)
-    o = RightOracle(batch, dof)
+    right = side == "right"
+    o = SideOracle(right, batch, dof)
     g = eng.PoseUKFBatch(batch, dof)
-    g.set_so3_right(True)
+    g.set_so3_right(right)
     if path == "dense":
         g.set_dense_sigma(True)
     elif path == "literal":
@@ -68,10 +72,11 @@ def _check(o, g, dof, tol):
     assert se < tol and ce < tol, (se, ce)
 
 
+@pytest.mark.parametrize("side", SIDES)
 @pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("dof", [53, 26])
-def test_predict_right(eng, dof, path):
-    cfg, uwv, log, o, g = _pair(eng, 6, dof, path=path)
+def test_predict_side(eng, dof, path, side):
+    cfg, uwv, log, o, g = _pair(eng, 6, dof, path=path, side=side)
     for k in range(3):
         for f in (o, g):
             f.set_rotation_rate(log["gyro"][k])
@@ -79,12 +84,13 @@ def test_predict_right(eng, dof, path):
     _check(o, g, dof, TOL_STEP)
 
 
+@pytest.mark.parametrize("side", SIDES)
 @pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("kind", ["acceleration", "velocity", "pressure", "water_velocity", "xy", "z", "efforts",
                                   "efforts_vel", "geographic", "delayed_xy"])
-def test_single_update_right(eng, kind, path):
+def test_single_update_side(eng, kind, path, side):
     dof, B = 53, 5
-    cfg, uwv, log, o, g = _pair(eng, B, dof, path=path)
+    cfg, uwv, log, o, g = _pair(eng, B, dof, path=path, side=side)
     for f in (o, g):
         f.set_rotation_rate(log["gyro"][0])
         f.predict(1e-3)
@@ -122,12 +128,13 @@ def test_single_update_right(eng, kind, path):
     _check(o, g, dof, TOL_STEP)
 
 
+@pytest.mark.parametrize("side", SIDES)
 @pytest.mark.parametrize("dof,mode,epochs,path", [(53, "C3", 400, "psp"), (26, "C3", 400, "psp"),
                                                   (53, "C4", 1000, "psp"), (26, "C4", 1000, "psp"),
                                                   (53, "C3", 400, "dense"), (26, "C3", 400, "dense"),
                                                   (53, "C4", 1000, "dense"), (53, "C3", 400, "literal")])
-def test_run_log_right(eng, dof, mode, epochs, path):
-    cfg, uwv, log, o, g = _pair(eng, 4, dof, mode, epochs, path=path)
+def test_run_log_side(eng, dof, mode, epochs, path, side):
+    cfg, uwv, log, o, g = _pair(eng, 4, dof, mode, epochs, path=path, side=side)
     counts_o = o.run_log(log)
     acc = eng.DeviceBuffer(np.zeros((4, 4), np.uint32))
     g.run_log(g.upload_log(log), accept_counts=acc)
@@ -139,7 +146,8 @@ def test_run_log_right(eng, dof, mode, epochs, path):
 @pytest.mark.parametrize("dense", [False, True])
 def test_right_differs_from_left(eng, dense):
     """The switch reaches the kernels: the same 400-epoch C3 log on the left
-    and right engine paths differs by far more than the parity tolerance."""
+    and right engine paths differs by far more than the parity tolerance, and
+    a fresh handle runs the right side (the default)."""
     cfg, uwv, log = pose_setup(2, 53, "C3", 400)
     xs = []
     for right in (False, True):
@@ -151,16 +159,23 @@ def test_right_differs_from_left(eng, dense):
         g.run_log(g.upload_log(log))
         xs.append(g.get_state())
     assert state_err(xs[1][0], xs[0][0], xs[0][1], 53).max() > 0.1
+    d = eng.PoseUKFBatch(2, 53)  # no set_so3_right: the default side
+    d.set_dense_sigma(dense)
+    d.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    d.set_process_noise_from_config(cfg, 1e-3)
+    d.run_log(d.upload_log(log))
+    np.testing.assert_array_equal(d.get_state()[0], xs[1][0])
 
 
+@pytest.mark.parametrize("side", SIDES)
 @pytest.mark.parametrize("dof", [53, 26])
-def test_visual_landmark_right(eng, dof):
+def test_visual_landmark_side(eng, dof, side):
     """The marker-augmented visual update (PoseUKF.cpp:613-654) with both SO3
-    segments (filter and marker orientation) on the right side, against the
-    oracle's right side (aug SEG_SO3R / sm SEG_SO3R)."""
+    segments (filter and marker orientation) on the given side, against the
+    oracle's same side (aug / sm SEG_SO3R on the right, SEG_SO3 on the left)."""
     from test_small_filters import pose_scene, visual_common
     B = 5
-    cfg, uwv, log, o, g = _pair(eng, B, dof, "C3", 60)
+    cfg, uwv, log, o, g = _pair(eng, B, dof, "C3", 60, side=side)
     o.run_log(log)
     g.run_log(g.upload_log(log))
     x0 = o.get_state()[0]
@@ -172,12 +187,14 @@ def test_visual_landmark_right(eng, dof):
     assert not g.get_status().any()
 
 
-def test_ensemble_stats_right(eng):
-    """uwvk_pose_ensemble_stats on a right-side handle measures the orientation
-    error in the body frame, log(t^-1 q), like the host reference."""
+@pytest.mark.parametrize("side", SIDES)
+def test_ensemble_stats_side(eng, side):
+    """uwvk_pose_ensemble_stats measures the orientation error on the handle's
+    side, log(t^-1 q) (right) or log(q t^-1) (left), like the host reference."""
     from uwvk import ensemble
     B = 130  # two partial rows of 64 plus a remainder
-    cfg, uwv, log, o, g = _pair(eng, B, 53, "C3", 50)
+    right = side == "right"
+    cfg, uwv, log, o, g = _pair(eng, B, 53, "C3", 50, side=side)
     g.run_log(g.upload_log(log))
     x, P = g.get_state()
     truth = np.array(log["truth"].state(50, 53), dtype=np.float64)
@@ -186,6 +203,6 @@ def test_ensemble_stats_right(eng):
     ax = np.array([0.6, -0.3, 0.74]) / np.linalg.norm([0.6, -0.3, 0.74])
     truth[3:7] = np.r_[np.cos(0.6), np.sin(0.6) * ax]
     got = g.ensemble_stats(truth)
-    np.testing.assert_allclose(got, ensemble.ensemble_stats_host(x, P, truth, right=True), rtol=1e-9, atol=1e-12)
-    left = ensemble.ensemble_stats_host(x, P, truth, right=False)
-    assert not np.allclose(got[2 * 54 + 3:2 * 54 + 6], left[2 * 54 + 3:2 * 54 + 6], rtol=1e-3)
+    np.testing.assert_allclose(got, ensemble.ensemble_stats_host(x, P, truth, right=right), rtol=1e-9, atol=1e-12)
+    other = ensemble.ensemble_stats_host(x, P, truth, right=not right)
+    assert not np.allclose(got[2 * 54 + 3:2 * 54 + 6], other[2 * 54 + 3:2 * 54 + 6], rtol=1e-3)

@@ -75,8 +75,8 @@ def test_psp_epoch_kernels_keep_three_waves_per_simd(src, side):
 # had 272 B/lane until r04: vg_point's select chain over L[k][0..3] by the
 # lane's column was turned into one lane-indexed load from a private copy of L,
 # i.e. L stored to scratch and reloaded in every predict and update
-# (VEL_PT_SEL keeps the selects; C2 633-635 -> 741-745 M steps/s,
-# profiles/r04/vpt/).  Since VEL_NOHOIST (+3%, profiles/r04/nh/) the kernel
+# (the r04 point selection keeps the selects; C2 633-635 -> 741-745 M steps/s,
+# profiles/r04/vpt/).  Since the r04 no-hoist change (+3%, profiles/r04/nh/) the kernel
 # keeps 168 B/lane of loop-invariant values written once before the epoch
 # loop and only read inside it; a scratch store inside the loop fails here.
 @pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
@@ -132,12 +132,19 @@ def test_sext32_literal_scan_catches_the_hazard():
     assert not sext32_literals("  s_mov_b64 s[4:5], -2\n  s_mov_b64 vcc, 0x3fffffff\n  s_movk_i32 s2, 0xffe0\n")
 
 
+ALL_TUS = sorted(os.path.join("csrc", f) for f in os.listdir(os.path.join(PKG, "csrc")) if f.endswith(".hip"))
+
+
 @pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
-@pytest.mark.parametrize("src", ["csrc/uwvk_psp_k.hip", "csrc/uwvk_psp_k_r.hip"])
-def test_psp_isa_has_no_zero_extended_64bit_literal(src, tmp_path):
-    out = str(tmp_path / "psp.s")
+@pytest.mark.parametrize("src", ALL_TUS)
+def test_isa_has_no_zero_extended_64bit_literal(src, tmp_path):
+    """The hazard comes from the compiler, not from the PSP code: every
+    translation unit of libuwvk.so, each with its Makefile flags."""
+    name = os.path.basename(src)[:-4]
+    flags = psp_flags() if name in ("uwvk_psp_k", "uwvk_psp_k_r") else []
+    out = str(tmp_path / (name + ".s"))
     cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-           *psp_flags(), "-S", src, "-o", out]
+           *flags, "-S", src, "-o", out]
     r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-2000:]
     bad = sext32_literals(open(out).read())

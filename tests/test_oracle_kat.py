@@ -64,9 +64,9 @@ def _quat_mul(a, b):
 
 
 def test_so3_side_switch_identities():
-    """Right [+] (q * exp(d), classic MTK) vs the default left [+] (exp(d) * q):
-    each satisfies the manifold identities, and they differ exactly by the side
-    the increment multiplies on."""
+    """The default right [+] (q * exp(d), MTK's SO3::boxplus) vs the left [+]
+    option (exp(d) * q): each satisfies the manifold identities, and they differ
+    exactly by the side the increment multiplies on."""
     lay = C.create_string_buffer(32 * 4)
     L.or_layout_init(lay, 53)
     rng = np.random.default_rng(11)
@@ -74,17 +74,19 @@ def test_so3_side_switch_identities():
     x[3:7] = so3_exp(rng.standard_normal(3) * 0.8)
     delta = rng.standard_normal(53) * 0.3
     out_l, out_r, d = np.zeros(54), np.zeros(54), np.zeros(53)
-    assert L.or_get_so3_right() == 0
-    L.or_boxplus(lay, p(x), p(delta), C.c_double(1.0), out_l.ctypes.data_as(DP))
-    with O.so3_right():
-        assert L.or_get_so3_right() == 1
-        L.or_boxplus(lay, p(x), p(delta), C.c_double(1.0), out_r.ctypes.data_as(DP))
-        L.or_boxminus(lay, p(out_r), p(x), d.ctypes.data_as(DP))
+    assert L.or_get_so3_right() == 1
+    with O.so3_left():
+        assert L.or_get_so3_right() == 0
+        L.or_boxplus(lay, p(x), p(delta), C.c_double(1.0), out_l.ctypes.data_as(DP))
+        L.or_boxminus(lay, p(out_l), p(x), d.ctypes.data_as(DP))
         np.testing.assert_allclose(d, delta, rtol=0, atol=1e-13)   # (x [+] d) [-] x = d
-        L.or_boxplus(lay, p(x), p(np.zeros(53)), C.c_double(1.0), out_r.ctypes.data_as(DP))
-        np.testing.assert_array_equal(out_r, x)                     # x [+] 0 = x
-        L.or_boxplus(lay, p(x), p(delta), C.c_double(1.0), out_r.ctypes.data_as(DP))
-    assert L.or_get_so3_right() == 0
+    assert L.or_get_so3_right() == 1
+    L.or_boxplus(lay, p(x), p(delta), C.c_double(1.0), out_r.ctypes.data_as(DP))
+    L.or_boxminus(lay, p(out_r), p(x), d.ctypes.data_as(DP))
+    np.testing.assert_allclose(d, delta, rtol=0, atol=1e-13)   # (x [+] d) [-] x = d
+    L.or_boxplus(lay, p(x), p(np.zeros(53)), C.c_double(1.0), out_r.ctypes.data_as(DP))
+    np.testing.assert_array_equal(out_r, x)                     # x [+] 0 = x
+    L.or_boxplus(lay, p(x), p(delta), C.c_double(1.0), out_r.ctypes.data_as(DP))
     e = so3_exp(delta[3:6])
     np.testing.assert_allclose(out_l[3:7], _quat_mul(e, x[3:7]), atol=1e-15)
     np.testing.assert_allclose(out_r[3:7], _quat_mul(x[3:7], e), atol=1e-15)
@@ -94,20 +96,15 @@ def test_so3_side_switch_identities():
 
 def test_so3_side_changes_c3_trajectory():
     """The two [+] conventions give materially different C3 filters (400 epochs,
-    2 DVL updates): the left (nav-frame) default is an unpinned choice, not a
-    rounding detail.  Both runs stay finite and positive definite."""
+    2 DVL updates): the side (right by default, MTK's SO3::boxplus) is an
+    unpinned choice, not a rounding detail.  Both runs stay finite and positive definite."""
     from helpers import state_err
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     log = synth.make_pose_log(2, 400, "C3")
     res = []
     for right in (False, True):
         o = O.OraclePoseBatch(2, 53)
-        if right:
-            with O.so3_right():
-                o.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
-                o.set_process_noise_from_config(cfg, log["dt"])
-                o.run_log(log)
-        else:
+        with O.so3_side(right):
             o.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
             o.set_process_noise_from_config(cfg, log["dt"])
             o.run_log(log)
@@ -119,7 +116,7 @@ def test_so3_side_changes_c3_trajectory():
     # after 0.4 s the trajectories differ by ~0.3-0.6 standard deviations: 10^6 x the
     # 1e-7 parity tolerance, so the choice of side is never hidden by the tests
     assert state_err(xr, xl, Pl, 53).max() > 0.1
-    assert L.or_get_so3_right() == 0
+    assert L.or_get_so3_right() == 1
 
 
 def test_cholesky():

@@ -13,6 +13,18 @@ from uwvk import synth
 TOL = 1e-10
 
 
+@pytest.fixture(params=["right", "left"])
+def side(request):
+    """Both SO3 [+] sides (right, MTK's q exp(d), is the default; left is the
+    option): the oracle's process-wide switch and the twin's module switch."""
+    right = request.param == "right"
+    prev = T.SO3_RIGHT
+    T.SO3_RIGHT = right
+    with O.so3_side(right):
+        yield request.param
+    T.SO3_RIGHT = prev
+
+
 def _pair(dof, mode="C3", epochs=50, seed=synth.SEED):
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     log = synth.make_pose_log(1, epochs, mode=mode, seed=seed, dof=dof)
@@ -41,7 +53,7 @@ def test_init_and_noise_identical(dof):
 
 
 @pytest.mark.parametrize("dof", [53, 26])
-def test_predict_and_updates(dof):
+def test_predict_and_updates(dof, side):
     log, o, t = _pair(dof)
     for e in range(40):
         o.set_rotation_rate(log["gyro"][e])
@@ -68,7 +80,7 @@ def test_predict_and_updates(dof):
 
 
 @pytest.mark.parametrize("dof", [53])
-def test_constrain_velocity_after_efforts(dof):
+def test_constrain_velocity_after_efforts(dof, side):
     log, o, t = _pair(dof)
     rng = np.random.default_rng(3)
     for e in range(5):
@@ -87,7 +99,7 @@ def test_constrain_velocity_after_efforts(dof):
         _cmp(o, t, dof)
 
 
-def test_geographic_and_gate():
+def test_geographic_and_gate(side):
     log, o, t = _pair(53)
     x, _ = o.get_state()
     lat, lon = T.nav_to_world(t.loc, x[0, 0] + 0.3, x[0, 1] - 0.4)
@@ -104,7 +116,7 @@ def test_geographic_and_gate():
 
 
 @pytest.mark.parametrize("mode", ["C3", "C4"])
-def test_run_log_matches_twin(mode):
+def test_run_log_matches_twin(mode, side):
     epochs = 300 if mode == "C3" else 1100
     log, o, t = _pair(53, mode, epochs)
     o.run_log(log)

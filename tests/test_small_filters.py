@@ -194,12 +194,12 @@ def pose_scene(x, seed=21):
     return true_t, true_q, marker, px + V.pixel_noise(B, seed + 1, 0.3)
 
 
-@pytest.mark.parametrize("right", [False, True])
+@pytest.mark.parametrize("right", [True, False])
 @pytest.mark.parametrize("dof", [53, 26])
 def test_pose_visual_update_reduces_error(dof, right):
-    """right: both SO3 segments of PoseStateWithMarker on the body-frame side
-    (or_set_so3_right, sm SEG_SO3R)"""
-    import contextlib
+    """Both SO3 segments of PoseStateWithMarker on the filter's side
+    (or_set_so3_right: sm SEG_SO3R on the default right side, SEG_SO3 on the
+    left); the side reaches the augmented update."""
     B = 3
     cfg, uwv, log = pose_setup(B, dof=dof, epochs=5)
     o = O.OraclePoseBatch(B, dof)
@@ -208,15 +208,15 @@ def test_pose_visual_update_reduces_error(dof, right):
     x0, P0 = o.get_state()
     true_t, true_q, marker, px = pose_scene(x0)
     fcov, fpos, cm, cam, cib = visual_common(B)
-    with (O.so3_right() if right else contextlib.nullcontext()):
+    with O.so3_side(right):
         o.update_visual(px, fcov, fpos, marker, cm, cam, cib)
     x1, P1 = o.get_state()
-    if right:  # the side reaches the augmented update: it differs from the left one
-        o2 = O.OraclePoseBatch(B, dof)
-        o2.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
-        o2.set_process_noise_from_config(cfg, log["dt"])
+    o2 = O.OraclePoseBatch(B, dof)  # the other side differs
+    o2.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    o2.set_process_noise_from_config(cfg, log["dt"])
+    with O.so3_side(not right):
         o2.update_visual(px, fcov, fpos, marker, cm, cam, cib)
-        assert np.abs(o2.get_state()[1] - P1).max() > 1e-9
+    assert np.abs(o2.get_state()[1] - P1).max() > 1e-9
     e0 = np.linalg.norm(x0[:, :3] - true_t, axis=1)
     e1 = np.linalg.norm(x1[:, :3] - true_t, axis=1)
     assert (e1 < e0).all(), (e0, e1)
@@ -293,20 +293,26 @@ def test_gpu_bottom_mask_and_errors():
 
 
 @pytest.mark.gpu
-def test_gpu_ipose_predict_and_visual():
+@pytest.mark.parametrize("right", [True, False])
+def test_gpu_ipose_predict_and_visual(right):
+    """Both sides of the orientation_error's SO3 [+] (right, the default; left
+    via uwvk_ipose_set_option) against the oracle's same side."""
     B = 13  # not a multiple of 2 / 4 instances per wave
     ref, p_err, q_err, marker, px = ipose_scene(B)
     g, o = IndirectPoseUKFBatch(B), O.OracleIndirectPoseBatch(B)
+    if not right:
+        g.set_so3_right(False)
     ipe = np.random.default_rng(2).normal(0, 0.1, (B, 3))
-    for f in (g, o):
-        f.init([0.1, 0.1, 0.2], [0.01, 0.01, 0.02], 20.0, ipe, [0.5, 0.5, 0.5])
-        f.set_pose_reference(ref)
     fcov, fpos, cm, cam, cib = visual_common(B)
-    for step in range(4):
+    with O.so3_side(right):
         for f in (g, o):
-            f.predict(0.1)
-        for f in (g, o):
-            f.update_visual(px, fcov, fpos, marker, cm, cam, cib)
+            f.init([0.1, 0.1, 0.2], [0.01, 0.01, 0.02], 20.0, ipe, [0.5, 0.5, 0.5])
+            f.set_pose_reference(ref)
+        for step in range(4):
+            for f in (g, o):
+                f.predict(0.1)
+            for f in (g, o):
+                f.update_visual(px, fcov, fpos, marker, cm, cam, cib)
     (xg, Pg), (xo, Po) = g.get_state(), o.get_state()
     assert _vec_err(xg[:, :3], xo[:, :3], np.diagonal(Po, axis1=1, axis2=2)[:, :3]) < TOL
     assert float(np.max(qlog_err(xg[:, 3:], xo[:, 3:]) / np.sqrt(np.min(np.diagonal(Po, axis1=1, axis2=2)[:, 3:],

@@ -15,8 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 out = "/tmp/psp_branch.s"
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-                "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", "-DPSP_HOT_ONLY",
-                "-DPSP_DIAG_HOT=1", *sys.argv[1:], "-S", "-o", out, os.path.join(PKG, "csrc", "uwvk_psp_k.hip")],
+                "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form",
+                *sys.argv[1:], "-S", "-o", out, os.path.join(PKG, "csrc", "uwvk_psp_k.hip")],
                check=True, stderr=subprocess.DEVNULL)
 s = open(out).read().split("\n")
 name = "_ZN4uwvk3psp11k_psp_epochILi53ELi1ELi1ELi0EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE"

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Static instruction mix of the C3 epoch loop of k_psp_epoch<53> (diagnostic):
-compiles the PSP translation unit with -DPSP_HOT_ONLY (the epoch loop keeps the
+compiles the PSP translation unit (r05: PSP_HOT_ONLY is gone; the epoch loop keeps the
 predict and the acceleration update only) plus any extra flags, finds the epoch
 loop (the outermost loop of the kernel) and counts its instructions by class.
 Inner loops (rank-M blocks, manifold-mean iterations) are counted once.
@@ -19,7 +19,7 @@ PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 def mix(extra=(), dof=53):
     out = "/tmp/psp_hot_%d.s" % os.getpid()
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-                    "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", "-DPSP_HOT_ONLY", *extra, "-S", "-o", out,
+                    "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", *extra, "-S", "-o", out,
                     os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
     s = open(out).read().split("\n")
     os.unlink(out)

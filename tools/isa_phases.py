@@ -17,7 +17,7 @@ dof = sys.argv[1] if len(sys.argv) > 1 else "53"
 extra = sys.argv[2:]
 out = "/tmp/psp_phases.s"
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-                "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", "-DUWVK_STAMPS", "-DPSP_HOT_ONLY", "-DPSP_DIAG_HOT=1", *extra, "-S", "-o", out,
+                "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", "-DUWVK_STAMPS", *extra, "-S", "-o", out,
                 os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
 s = open(out).read().split("\n")
 name = "_ZN4uwvk3psp11k_psp_epochILi%sELi1ELi1ELi0EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % dof

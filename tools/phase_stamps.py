@@ -32,6 +32,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=65536)
 ap.add_argument("--epochs", type=int, default=20)
 ap.add_argument("--dense", action="store_true", help="literal kernels (k_pose_epoch) instead of PSP")
+ap.add_argument("--so3-left", action="store_true", help="the left SO3 side (SR = 0 kernels; default right)")
 a = ap.parse_args()
 L = engine.lib(os.path.join(ROOT, "slam-uwv_kalman_filters_amd", "libuwvk_stamps.so"))
 cfg, uwv = synth.default_pose_config(), synth.default_uwv()
@@ -39,7 +40,10 @@ log = synth.make_pose_log(a.batch, a.epochs + 1, "C3")
 f = engine.PoseUKFBatch(a.batch)
 if a.dense:
     f.set_dense_sigma(True)
-read = L.uwvk_debug_read_stamps if a.dense else L.uwvk_debug_read_stamps_psp
+f.set_so3_right(not a.so3_left)
+# each side's PSP translation unit has its own stamp sums (the _r reader: SR = 1)
+read = L.uwvk_debug_read_stamps if a.dense else (L.uwvk_debug_read_stamps_psp if a.so3_left
+                                                 else L.uwvk_debug_read_stamps_psp_r)
 f.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
 f.set_process_noise_from_config(cfg, log["dt"])
 d = f.upload_log(log)

@@ -15,7 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag, steps = sys.argv[1], int(sys.argv[2])
 workload = sys.argv[3] if len(sys.argv) > 3 else "C3-dof53-b65536"
-rdir = sys.argv[4] if len(sys.argv) > 4 else "r03"
+rdir = sys.argv[4] if len(sys.argv) > 4 else "r05"
 base = os.path.join(ROOT, "gpurun_out", tag, "s%d" % steps)
 KERNEL = "k_psp_epoch<53"  # k_psp_epoch<53, QM> (r03: instantiated per process-noise shape)
 N_SIMD = 1024
@@ -45,7 +45,7 @@ waves = mix["SQ_WAVES"]
 instances = int(workload.rsplit("-b", 1)[1])
 we = instances * steps
 e = {
-    "kernel": "k_psp_epoch<53, 1, 1, 0>", "epochs_per_launch": steps, "waves": waves, "instances": instances,
+    "kernel": "k_psp_epoch<53, 1, 1, %d>" % (0 if workload.endswith("-left") else 1), "epochs_per_launch": steps, "waves": waves, "instances": instances,
     "fetch_size_kib_raw": fetch["FETCH_SIZE"], "write_size_kib_raw": write["WRITE_SIZE"],
     "fetch_bytes": fetch["FETCH_SIZE"] * 1024 * 2, "write_bytes": write["WRITE_SIZE"] * 1024,
 }

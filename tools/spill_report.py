@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """SGPR spill traffic of the C3 epoch loop of k_psp_epoch<53> (diagnostic):
-compiles with -DPSP_HOT_ONLY -DPSP_DIAG_HOT=1 (+ extra flags), finds the VGPRs
+compiles the PSP translation unit (+ extra flags; r05: the hot-path-only diagnostic defines are gone, the whole kernel is analysed), finds the VGPRs
 used as SGPR spill lanes, and lists the spill slots by the number of reloads
 (v_readlane from a spill VGPR) inside the epoch loop, with the instruction that
 defined the spilled SGPR before the loop (a kernarg s_load offset names the
@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 out = "/tmp/spill_%d.s" % os.getpid()
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-                "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", *([] if os.environ.get("FULL") == "1" else ["-DPSP_HOT_ONLY", "-DPSP_DIAG_HOT=1"]), *sys.argv[1:], "-S", "-o", out,
+                "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", *sys.argv[1:], "-S", "-o", out,
                 os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
 s = open(out).read().split("\n")
 os.unlink(out)

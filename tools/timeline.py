@@ -44,7 +44,8 @@ def main():
     L = engine.lib()
     n = min(B + 8 * (ch - 1) * ch * (a.tail_slots or s_x), 131072)  # spread launches: 8 (c - 1) r_x more blocks
     buf = np.zeros(n * 8, np.uint64)
-    assert L.uwvk_debug_read_timeline(buf.ctypes.data_as(C.c_void_p), C.c_longlong(n * 8)) == 0
+    # the default (right) side's kernels record into the SR = 1 object's buffer
+    assert L.uwvk_debug_read_timeline_r(buf.ctypes.data_as(C.c_void_p), C.c_longlong(n * 8)) == 0
     t = buf.reshape(n, 8)
     t = t[t[:, 3] != 0]  # blocks that ran
     n = len(t)
