@@ -149,3 +149,45 @@ def test_isa_has_no_zero_extended_64bit_literal(src, tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     bad = sext32_literals(open(out).read())
     assert not bad, bad[:10]
+
+
+# Address-space casts into the constant address space (scalar loads through the
+# scalar cache): valid only for a pointer whose value is a global address.  The
+# r04o PSP_EA_LAUNDER variant cast the address of the by-value EpochArgs
+# kernel parameter: the escaping address made clang copy the parameter into a
+# private alloca (addrspace 5), and `addrspacecast addrspace(5) -> addrspace(4)`
+# (private -> constant, disjoint non-flat spaces) is lowered to an undefined
+# SGPR pair: the first scalar load through it, s_load_dword s0, s[64:65], 0x298
+# (ea.first), read a garbage address and the kernel faulted (UWVK_EDEVICE,
+# profiles/EXPERIMENTS.md "r05: the r04o device fault"; tools/eal_variant.py
+# rebuilds the variant).  The shipped casts (PoseShared, Qp) start from global
+# pointer values loaded from PoseBufs.  This scan keeps private -> constant /
+# global casts and private copies of the kernel-argument structs out of the IR.
+def ir_cast_findings(ir):
+    bad = []
+    for line in ir.splitlines():
+        if re.search(r"addrspacecast ptr addrspace\(5\) \S+ to ptr addrspace\((1|4)\)", line):
+            bad.append(line.strip())
+        if re.search(r'alloca %"struct\.uwvk::(EpochArgs|PoseShared|PoseBufs|MeasArgs)"', line):
+            bad.append(line.strip())
+    return bad
+
+
+def test_ir_cast_scan_catches_the_r04o_pattern():
+    assert ir_cast_findings('  %6 = alloca %"struct.uwvk::EpochArgs", align 8, addrspace(5)\n')
+    assert ir_cast_findings("  %467 = addrspacecast ptr addrspace(5) %6 to ptr addrspace(4)\n")
+    assert not ir_cast_findings("  %717 = addrspacecast ptr %24 to ptr addrspace(4)\n")
+
+
+@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
+@pytest.mark.parametrize("src", ALL_TUS)
+def test_no_private_to_constant_address_space_cast(src, tmp_path):
+    name = os.path.basename(src)[:-4]
+    flags = psp_flags() if name in ("uwvk_psp_k", "uwvk_psp_k_r") else []
+    out = str(tmp_path / (name + ".ll"))
+    cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
+           *flags, "-S", "-emit-llvm", src, "-o", out]
+    r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    bad = ir_cast_findings(open(out).read())
+    assert not bad, bad[:10]
