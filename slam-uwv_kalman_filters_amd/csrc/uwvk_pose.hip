@@ -440,7 +440,9 @@ static uwvk_status launch_update(uwvk_pose* h, int m, const double* mu, const do
   ma.only_vel = only_vel;
   ma.accepted = h->d_accepted;
   PoseBufs b = bufs(h);
-  if (K == MK_EFFORTS || use_dense(h))
+  // the full BodyEfforts model is non-affine in 48 of 53 DOFs: the literal kernel;
+  // its velocity-only form (constrainVelocity, k = 9) runs on PSP
+  if ((K == MK_EFFORTS && !only_vel) || use_dense(h))
     HIPCHK(launch_pose_update(h->dof, K, h->stream, b, h->sh, ma, m));
   else {
     HIPCHK(upload_shared(h, h->qp_dt));
@@ -730,7 +732,8 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   }
   // PSP: one launch per run of epochs up to and including the next BodyEfforts
   // epoch (its predict and other updates); that epoch's efforts update alone
-  // then goes through the literal efforts kernel (same HBM state layout).  Efforts is
+  // then goes through the literal efforts kernel, or, in its velocity-only form,
+  // the PSP constrainVelocity kernel (same HBM state layout).  Efforts is
   // the last update of an epoch (the fused literal order), so the split is exact.
   std::vector<uint32_t> fl;
   const uint32_t* hf = log->host_flags ? log->host_flags + first : nullptr;
@@ -769,8 +772,10 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     if (r < first + count) {
       ea.first = r;
       ea.count = 1;
-      HIPCHK(launch_pose_efforts_epoch(h->dof, h->stream, b, sh, ea,
-                                       (hf[r - first] & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0));
+      if (hf[r - first] & UWVK_EV_EFFORTS_VELOCITY_ONLY)  // constrainVelocity: PSP (PEffVO)
+        HIPCHK(launch_psp_efforts_vo(h->dof, h->stream, b, sh, ea));
+      else  // measurementEfforts: the literal kernel
+        HIPCHK(launch_pose_efforts_epoch(h->dof, h->stream, b, sh, ea, 0));
     }
     e = last;
   }

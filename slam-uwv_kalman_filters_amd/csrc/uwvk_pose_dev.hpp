@@ -1247,6 +1247,19 @@ struct HJmax<HConstrain<DOF>, DOF> {
 
 // getRotationRate (PoseUKF.cpp:693-699) at the current mean
 template <int DOF>
+UWVK_DEV void rotation_rate_body_mu(const double* mu, const PoseShared& sh, const double w[3], double out[3]) {
+  using L = Lay<DOF>;
+  const double lat = sh.lat0 + mu[L::s_pos] * sh.inv_rm;
+  double sl, cl;
+  sincos(lat, &sl, &cl);
+  const double er[3] = {kEarthW * cl, 0.0, kEarthW * sl};
+  const double q[4] = {mu[L::s_quat], mu[L::s_quat + 1], mu[L::s_quat + 2], mu[L::s_quat + 3]};
+  double r[3];
+  qrot_inv(q, er, r);
+#pragma unroll
+  for (int i = 0; i < 3; i++) out[i] = (w[i] - mu[L::s_bg + i]) - r[i];
+}
+template <int DOF>
 UWVK_DEV void rotation_rate_body(const Smem<DOF>& sm, const PoseShared& sh, const double w[3], double out[3]) {
   using L = Lay<DOF>;
   const double lat = sh.lat0 + sm.mu[L::s_pos] * sh.inv_rm;

@@ -1071,6 +1071,39 @@ struct PZ {  // measurementZPosition, PoseUKF.cpp:100-105: linear (k = 0)
   UWVK_DEV void jac(const double*, double (&H)[M][NC]) const { H[0][0] = 1; }
 };
 
+template <int DOF>
+struct PEffVO {  // constrainVelocity, PoseUKF.cpp:199-219, 585-591 (only_affect_velocity)
+  // The model reads the state's velocity only: orientation, water velocity and
+  // body acceleration are frozen at mu (HConstrain), the dynamic model's
+  // parameters are the shared model's (the handle's model blocks, A9).  It is
+  // nonlinear in the velocity (Coriolis, quadratic damping) and independent of
+  // every other DOF, so the nonlinear prefix is the velocity block's end, k = 9
+  // (19 model evaluations), and there is no affine part (H = 0, NC = 0).
+  static constexpr int M = 6, K = 9, NR = 3, NC = 0, ZMODE = 0, GATE = 0;
+  static constexpr int rows[NR] = {6, 7, 8};
+  static constexpr int cols[1] = {6};  // placeholder: NC = 0 columns are used
+  HConstrain<DOF> h;
+  UWVK_DEV void eval(const double* x, double (&z)[M]) const { h(x, z); }
+  UWVK_DEV void jac(const double*, double (&)[M][1]) const {}
+};
+
+// R sums (R > what one staging round holds) over NL contributors: chunks of
+// lds_sums, the staging area reused between rounds
+template <int R, int NL, int STRIDE, int C0 = 0>
+UWVK_DEV void lds_sums_chunked(const double (&v)[R], double* buf, int l, double (&out)[R]) {
+  if constexpr (C0 < R) {
+    constexpr int CH0 = 115 / NL, CH = (R - C0) < CH0 ? (R - C0) : CH0;
+    double vc[CH], oc[CH];
+#pragma unroll
+    for (int i = 0; i < CH; i++) vc[i] = v[C0 + i];
+    lds_sums<CH, NL, STRIDE>(vc, buf, l, oc);
+#pragma unroll
+    for (int i = 0; i < CH; i++) out[C0 + i] = oc[i];
+    wsync();  // every lane's reads of this round before the next round's writes
+    lds_sums_chunked<R, NL, STRIDE, C0 + CH>(v, buf, l, out);
+  }
+}
+
 // one row block I of rankm_mfma_o (tiles (I, J), J <= I), then block I + 1
 template <int DOF, int I, int NT>
 UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop)[NT], int q, int c, int tq) {
@@ -1215,7 +1248,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
                          const HM& hm, bool* ok, double ds, double ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   using G = PG<DOF>;
-  constexpr int M = HM::M, K = HM::K, NC = HM::NC, KA = K > 0 ? K : 1;
+  constexpr int M = HM::M, K = HM::K, NC = HM::NC, KA = K > 0 ? K : 1, NCA = NC > 0 ? NC : 1;
   int l = olane();  // re-laundered per phase (PSP_PHASE)
   double a[KA];
   bool cok = true;
@@ -1238,9 +1271,9 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   // H and P first: P reads the staged rows, after which stg holds the
   // transposed sums.  One round of M + M(M+1)/2 sums over the 2K point lanes:
   // u = z_p - z_0, s = sum u, m = s / N; sum dz dz^T = sum u u^T - m s^T - s m^T + 2K m m^T
-  double Hs[M][NC];
+  double Hs[M][NCA];
   {
-    double H[M][NC];
+    double H[M][NCA];
     hm.jac(sm.mu, H);
 #pragma unroll
     for (int i = 0; i < M; i++)
@@ -1267,7 +1300,8 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     for (int i2 = 0; i2 < M; i2++)
 #pragma unroll
       for (int j2 = 0; j2 <= i2; j2++) v[k++] = v[i2] * v[j2];
-    lds_sums<R, 2 * K, 1>(v, sm.stg, l, sums);
+    if constexpr (R * 2 * K <= 115) lds_sums<R, 2 * K, 1>(v, sm.stg, l, sums);
+    else lds_sums_chunked<R, 2 * K, 1>(v, sm.stg, l, sums);  // M = 6 (constrainVelocity)
     double m[M];
 #pragma unroll
     for (int i2 = 0; i2 < M; i2++) {
@@ -1412,7 +1446,18 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     Kt[i] = Kg[i] * ids;
   }
   psync();
-  rankm_mfma_o<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
+  if constexpr (M <= 3) {
+    rankm_mfma_o<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
+  } else {  // rank M > 3 (constrainVelocity, M = 6): two passes of rank 3 and M - 3
+    double c0[3], k0[3], c1[M - 3], k1[M - 3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) { c0[i] = Ct[i]; k0[i] = Kt[i]; }
+#pragma unroll
+    for (int i = 0; i < M - 3; i++) { c1[i] = Ct[3 + i]; k1[i] = Kt[3 + i]; }
+    rankm_mfma_o<DOF, 3>(sm.S, sm.stg, c0, k0, l);
+    psync();
+    rankm_mfma_o<DOF, M - 3>(sm.S, sm.stg, c1, k1, l);
+  }
   psync();
   PSP_PHASE(34);
   // apply_delta, exact form: mu <- mu [+] delta, Sigma <- T Sigma T^T with T

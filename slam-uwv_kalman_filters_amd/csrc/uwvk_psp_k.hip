@@ -241,6 +241,37 @@ UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, co
   }
 }
 
+// constrainVelocity (PoseUKF.cpp:199-219, the only_affect_velocity branch of
+// :581-602) in PSP form (PEffVO, k = 9): the frozen inputs at mu exactly as the
+// literal kernel's do_update_efforts<DOF, 1> builds them
+template <int DOF, int SR>
+UWVK_DEV bool do_update_vo(PspSmem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, int64_t inst,
+                           const double* zin, const double* Rin, bool* ok, double ds, double ids) {
+  using L = Lay<DOF>;
+  double z[6], R[36];
+  copy_zr<6>(zin, Rin, z, R);
+  PEffVO<DOF> hm;
+  HConstrain<DOF>& h = hm.h;
+  h.ef.base = b.uwv;
+  h.ef.weight = sh.uwv_weight;
+  h.ef.buoyancy = sh.uwv_buoyancy;
+  for (int k = 0; k < 3; k++) { h.ef.cog[k] = sh.cog[k]; h.ef.cob[k] = sh.cob[k]; }
+  const double w[3] = {b.rot[inst * 3], b.rot[inst * 3 + 1], b.rot[inst * 3 + 2]};
+  double wb[3];
+  rotation_rate_body_mu<DOF>(sm.mu, sh, w, wb);  // getRotationRate() at mu (PoseUKF.cpp:588)
+  h.blk.has = true;
+  h.blk.v = b.model + inst * 27;  // the shared model's current blocks (A9)
+  for (int k = 0; k < 3; k++) { h.wb[k] = wb[k]; h.imu[k] = sh.p.imu_in_body[k]; }
+  h.w3[0] = sm.mu[L::s_wv]; h.w3[1] = sm.mu[L::s_wv + 1]; h.w3[2] = 0.0;
+  for (int k = 0; k < 4; k++) h.q[k] = sm.mu[L::s_quat + k];
+  double ra[3], cr[3], cc[3];
+  qrot_inv(h.q, sm.mu + L::s_acc, ra);
+  cross3(wb, h.imu, cr);
+  cross3(wb, cr, cc);
+  for (int k = 0; k < 3; k++) h.ab[k] = ra[k] - cc[k];
+  return psp_update<DOF, SR>(sm, z, R, 0, hm, ok, ds, ids);
+}
+
 template <int DOF, int SR>
 __global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, double dt) {
   __shared__ PspSmem<DOF> sm;
@@ -278,7 +309,9 @@ __global__ __launch_bounds__(64) void k_psp_update(PoseBufs b, PoseShared sh, Me
   }
   load_psp<DOF>(sm, b, inst);
   bool ok = true;
-  const bool acc = do_update<DOF, KIND, SR>(sm, sh, inst, z, R, ma, &ok, 1.0, 1.0);
+  bool acc;
+  if constexpr (KIND == MK_EFFORTS) acc = do_update_vo<DOF, SR>(sm, sh, b, inst, z, R, &ok, 1.0, 1.0);  // only_vel
+  else acc = do_update<DOF, KIND, SR>(sm, sh, inst, z, R, ma, &ok, 1.0, 1.0);
   if (lane_id() == 0) {
     if (!ok) b.status[inst] |= UWVK_ST_NOTPD;
     if (ma.accepted) ma.accepted[inst] = acc ? 1 : 0;
@@ -595,6 +628,30 @@ __global__ __launch_bounds__(64) void k_psp_epoch_p(PoseBufs b, PoseShared sh0, 
   }
 }
 
+// run_log's velocity-only BodyEfforts epoch (UWVK_EV_EFFORTS_VELOCITY_ONLY):
+// after the k_psp_epoch launch that ran the epoch's predict and other updates,
+// the constrainVelocity update alone (the last update of the epoch), the same
+// bookkeeping as k_pose_efforts_epoch
+template <int DOF, int SR>
+__global__ __launch_bounds__(64) void k_psp_efforts_vo(PoseBufs b, PoseShared sh, EpochArgs ea) {
+  __shared__ PspSmem<DOF> sm;
+  const int64_t B = b.batch, inst = xcd_instance(B), e = ea.first;
+  if (!(ea.flags[e] & UWVK_EV_EFFORTS)) return;
+  const double* z = ea.efforts + ((int64_t)ea.e_index[e] * B + inst) * 6;
+  if (!all_finite(z, 6)) {
+    if (lane_id() == 0) b.status[inst] |= UWVK_ST_NAN;
+    return;
+  }
+  load_psp<DOF>(sm, b, inst);
+  bool ok = true;
+  const bool acc = do_update_vo<DOF, SR>(sm, sh, b, inst, z, ea.e_cov, &ok, 1.0, 1.0);
+  if (lane_id() == 0) {
+    if (!ok) b.status[inst] |= UWVK_ST_NOTPD;
+    if (ea.accept_counts) ea.accept_counts[inst * 4 + 3] += acc ? 1u : 0u;
+  }
+  store_psp<DOF>(sm, b, inst);
+}
+
 }  // namespace psp
 
 template <int DOF, int SR>
@@ -610,6 +667,10 @@ static hipError_t psp_update_dof(int kind, hipStream_t st, const PoseBufs& b, co
     case MK_Z: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_Z, SR>), g, t, 0, st, b, sh, ma, m); break;
     case MK_GEO: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_GEO, SR>), g, t, 0, st, b, sh, ma, m); break;
     case MK_DELAYED: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_DELAYED, SR>), g, t, 0, st, b, sh, ma, m); break;
+    case MK_EFFORTS:  // PSP covers the velocity-only form (constrainVelocity) alone
+      if (!ma.only_vel) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_EFFORTS, SR>), g, t, 0, st, b, sh, ma, m);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -628,6 +689,16 @@ template <int SR>
 hipError_t launch_psp_update_sr(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                                 const MeasArgs& ma, int m) {
   return dof == 53 ? psp_update_dof<53, SR>(kind, st, b, sh, ma, m) : psp_update_dof<26, SR>(kind, st, b, sh, ma, m);
+}
+
+template <int SR>
+hipError_t launch_psp_efforts_vo_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                                    const EpochArgs& ea) {
+  if (dof == 53)
+    hipLaunchKernelGGL((psp::k_psp_efforts_vo<53, SR>), dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, ea);
+  else
+    hipLaunchKernelGGL((psp::k_psp_efforts_vo<26, SR>), dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, ea);
+  return hipGetLastError();
 }
 
 template <int DOF, int QM, int EVS, int SR>
@@ -667,6 +738,8 @@ template hipError_t launch_psp_update_sr<PSP_SIDE>(int, int, hipStream_t, const 
                                                    const MeasArgs&, int);
 template hipError_t launch_psp_epoch_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&,
                                                   const EpochArgs&, int64_t, uint32_t);
+template hipError_t launch_psp_efforts_vo_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&,
+                                                       const EpochArgs&);
 
 #if PSP_SIDE == 0
 // the handle's side picks the instantiation set (a template parameter of every
@@ -685,6 +758,11 @@ hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const Po
                             int64_t grid, uint32_t ev_any) {
   return sh.so3_right ? launch_psp_epoch_sr<1>(dof, st, b, sh, ea, grid, ev_any)
                       : launch_psp_epoch_sr<0>(dof, st, b, sh, ea, grid, ev_any);
+}
+
+hipError_t launch_psp_efforts_vo(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                                 const EpochArgs& ea) {
+  return sh.so3_right ? launch_psp_efforts_vo_sr<1>(dof, st, b, sh, ea) : launch_psp_efforts_vo_sr<0>(dof, st, b, sh, ea);
 }
 
 // XCC placement probe: block b writes the XCC it runs on (hardware XCC_ID).

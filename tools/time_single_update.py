@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Times the single-call literal updates (uwvk_pose_update_efforts, and the
-acceleration update on the dense path) at batch 65,536: HIP events on the
-handle's stream around 5 calls each.  UWVK_LIB selects a variant library."""
+"""Times single-call updates at batch 65,536: the literal BodyEfforts update
+(uwvk_pose_update_efforts), its velocity-only form (constrainVelocity) on PSP
+(r05) and on the literal kernel, and the acceleration update on the dense path:
+HIP events on the handle's stream around 5 calls each (each call includes its
+measurement upload).  UWVK_LIB selects a variant library."""
 import os
 import sys
 
@@ -24,9 +26,10 @@ acc = np.tile([0.0, 0.0, 9.81], (B, 1)) + rng.normal(0, 1e-3, (B, 3))
 acov = np.eye(3) * 1e-4
 out = {}
 for name, call in (("efforts", lambda: f.update("efforts", eff, ecov, only_vel=0)),
+                   ("efforts_vo_psp", lambda: f.update("efforts", eff, ecov, only_vel=1)),
+                   ("efforts_vo_dense", lambda: f.update("efforts", eff, ecov, only_vel=1)),
                    ("acceleration_dense", lambda: f.update("acceleration", acc, acov))):
-    if name.endswith("_dense"):
-        f.set_dense_sigma(True)
+    f.set_dense_sigma(name.endswith("_dense"))
     call()
     f.synchronize()
     f.timer_start()
