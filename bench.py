@@ -150,6 +150,9 @@ def parse():
                          "0 one workgroup per instance, -1 the engine default")
     ap.add_argument("--tail-slots", type=int, default=0,
                     help="UWVK_OPT_TAIL_SLOTS: 0 runtime occupancy, > 0 blocks per XCD, < 0 no tail spreading")
+    ap.add_argument("--lds-pad", type=int, default=0,
+                    help="UWVK_OPT_LDS_PAD (diagnostic): unused dynamic LDS bytes per PSP epoch workgroup, lowering "
+                         "its occupancy (use with --tail-slots -1)")
     ap.add_argument("--config", default="",
                     help="YAML / JSON filter configuration (uwvk.config: PoseUKFConfig, UWVParameters, engine "
                          "options) instead of the synthetic defaults; the line names it in config.config_file")
@@ -525,6 +528,8 @@ def main():
                              cfg=cfg, epochs=seg_bounds[0][1])
     f = engine.PoseUKFBatch(B, a.dof, device=local)
     f.set_tail_slots(a.tail_slots)
+    if a.lds_pad:
+        f.set_lds_pad(a.lds_pad)
     if a.persist >= 0:
         f.set_persist(a.persist)
     if a.tail_chunks:

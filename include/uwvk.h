@@ -449,6 +449,12 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   bitwise those of 0.  (MI355X, C3 batch 65,536: 0.2-0.5% faster over 200
  *   epochs, 0.5-0.9% slower over 20) */
 #define UWVK_OPT_PERSIST 6
+/* UWVK_OPT_LDS_PAD (diagnostic, r05): bytes of dynamic LDS requested per PSP
+ *   epoch workgroup on top of its static 12.8 KB, unused by the kernel: it only
+ *   lowers the resident workgroups per CU (12 -> 9 / 6 / 4 ...), to measure the
+ *   epoch kernel's rate against occupancy.  0 default;
+ *   use with UWVK_OPT_TAIL_SLOTS < 0 (the tail planner assumes no pad). */
+#define UWVK_OPT_LDS_PAD 7
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
 /* Host-only query (no device work): the chunks per tail instance the
  * UWVK_OPT_TAIL_SLOTS planner picks for one XCD's instances over its resident

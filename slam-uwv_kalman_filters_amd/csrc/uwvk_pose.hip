@@ -66,6 +66,7 @@ struct uwvk_pose {
   // persistent epoch kernel (UWVK_OPT_PERSIST): ticket counter and the value
   // it holds when the next launch starts (every launch takes units + grid)
   int persist = 0;
+  uint32_t lds_pad = 0;  // UWVK_OPT_LDS_PAD (diagnostic occupancy sweep)
   uint32_t* d_ticket = nullptr;
   uint32_t ticket_next = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -759,7 +760,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     uint32_t ev_any = 0;  // the event kinds of this launch's epochs (kernel choice)
     for (int64_t k = e; k < last; k++) ev_any |= hf[k - first];
     HIPCHK(prepare_tail(h, ea, grid));
-    if (launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid, ev_any) != hipSuccess) {
+    if (launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid, ev_any, h->lds_pad) != hipSuccess) {
       // a persistent launch that did not run took no tickets: restart the
       // counter from zero (stream-ordered, before any later launch)
       if (ea.ticket) {
@@ -836,6 +837,11 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
   }
   if (option == UWVK_OPT_PERSIST) {
     h->persist = value ? 1 : 0;
+    return UWVK_OK;
+  }
+  if (option == UWVK_OPT_LDS_PAD) {  // diagnostic: occupancy sweep of the epoch kernel
+    if (value < 0 || value > 150 * 1024) return UWVK_EINVAL;
+    h->lds_pad = (uint32_t)value;
     return UWVK_OK;
   }
   return UWVK_EINVAL;

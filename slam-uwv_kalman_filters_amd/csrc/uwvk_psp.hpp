@@ -12,7 +12,7 @@ hipError_t launch_psp_update_sr(int dof, int kind, hipStream_t st, const PoseBuf
                                 const MeasArgs& ma, int m);
 template <int SR>
 hipError_t launch_psp_epoch_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                               int64_t grid, uint32_t ev_any);
+                               int64_t grid, uint32_t ev_any, uint32_t lds_pad);
 template <int SR>
 hipError_t launch_psp_efforts_vo_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                                     const EpochArgs& ea);
@@ -27,9 +27,9 @@ extern template hipError_t launch_psp_update_sr<0>(int, int, hipStream_t, const 
 extern template hipError_t launch_psp_update_sr<1>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
                                                    const MeasArgs&, int);
 extern template hipError_t launch_psp_epoch_sr<0>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                  const EpochArgs&, int64_t, uint32_t);
+                                                  const EpochArgs&, int64_t, uint32_t, uint32_t);
 extern template hipError_t launch_psp_epoch_sr<1>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                  const EpochArgs&, int64_t, uint32_t);
+                                                  const EpochArgs&, int64_t, uint32_t, uint32_t);
 // the handle's side (sh.so3_right) picks the launcher
 hipError_t launch_psp_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt);
 hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
@@ -41,8 +41,9 @@ hipError_t launch_psp_efforts_vo(int dof, hipStream_t st, const PoseBufs& b, con
 // grid 0: one block per instance; otherwise 8 (n_x + (chunks - 1) r_x)
 // ev_any: the OR of the launch's epoch flags (selects the kernel instantiation;
 // all bits set is always correct)
+// lds_pad: UWVK_OPT_LDS_PAD's dynamic LDS bytes per workgroup (diagnostic)
 hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                            int64_t grid = 0, uint32_t ev_any = 0xffffffffu);
+                            int64_t grid = 0, uint32_t ev_any = 0xffffffffu, uint32_t lds_pad = 0);
 // resident k_psp_epoch blocks per XCD (occupancy x CUs / 8), 0 if unknown
 int64_t psp_epoch_slots_per_xcd(int dof, int device);
 // resident blocks of the static (k_psp_epoch) or persistent (k_psp_epoch_p)

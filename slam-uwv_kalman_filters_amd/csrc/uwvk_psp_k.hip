@@ -702,33 +702,34 @@ hipError_t launch_psp_efforts_vo_sr(int dof, hipStream_t st, const PoseBufs& b, 
 }
 
 template <int DOF, int QM, int EVS, int SR>
-static void launch_epoch_q(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea, dim3 g) {
+static void launch_epoch_q(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea, dim3 g,
+                           uint32_t pad) {
   if (ea.ticket)
-    hipLaunchKernelGGL((psp::k_psp_epoch_p<DOF, QM, EVS, SR>), g, dim3(64), 0, st, b, sh, ea);
+    hipLaunchKernelGGL((psp::k_psp_epoch_p<DOF, QM, EVS, SR>), g, dim3(64), pad, st, b, sh, ea);
   else
-    hipLaunchKernelGGL((psp::k_psp_epoch<DOF, QM, EVS, SR>), g, dim3(64), 0, st, b, sh, ea);
+    hipLaunchKernelGGL((psp::k_psp_epoch<DOF, QM, EVS, SR>), g, dim3(64), pad, st, b, sh, ea);
 }
 
 template <int DOF, int SR>
 static void launch_epoch_dof(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea, dim3 g,
-                             uint32_t ev_any) {
+                             uint32_t ev_any, uint32_t pad) {
   // the kernel instantiated for the handle's process-noise shape (psp_predict
   // QM) and the launch's event kinds (EVS 1: no pressure / ADCP epoch in the
   // range, the C3 workload); a general Q runs the one kernel with everything
   const bool pa = (ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP)) != 0;
-  if (!sh.q_simple) launch_epoch_q<DOF, 2, 0, SR>(st, b, sh, ea, g);
-  else if (pa) launch_epoch_q<DOF, 1, 0, SR>(st, b, sh, ea, g);
-  else launch_epoch_q<DOF, 1, 1, SR>(st, b, sh, ea, g);
+  if (!sh.q_simple) launch_epoch_q<DOF, 2, 0, SR>(st, b, sh, ea, g, pad);
+  else if (pa) launch_epoch_q<DOF, 1, 0, SR>(st, b, sh, ea, g, pad);
+  else launch_epoch_q<DOF, 1, 1, SR>(st, b, sh, ea, g, pad);
 }
 
 template <int SR>
 hipError_t launch_psp_epoch_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                               int64_t grid, uint32_t ev_any) {
+                               int64_t grid, uint32_t ev_any, uint32_t lds_pad) {
   const dim3 g((unsigned)(grid > 0 ? grid : b.batch));
   if (dof == 53)
-    launch_epoch_dof<53, SR>(st, b, sh, ea, g, ev_any);
+    launch_epoch_dof<53, SR>(st, b, sh, ea, g, ev_any, lds_pad);
   else
-    launch_epoch_dof<26, SR>(st, b, sh, ea, g, ev_any);
+    launch_epoch_dof<26, SR>(st, b, sh, ea, g, ev_any, lds_pad);
   return hipGetLastError();
 }
 
@@ -737,7 +738,7 @@ template hipError_t launch_psp_predict_sr<PSP_SIDE>(int, hipStream_t, const Pose
 template hipError_t launch_psp_update_sr<PSP_SIDE>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
                                                    const MeasArgs&, int);
 template hipError_t launch_psp_epoch_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                  const EpochArgs&, int64_t, uint32_t);
+                                                  const EpochArgs&, int64_t, uint32_t, uint32_t);
 template hipError_t launch_psp_efforts_vo_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&,
                                                        const EpochArgs&);
 
@@ -755,9 +756,9 @@ hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& 
 }
 
 hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                            int64_t grid, uint32_t ev_any) {
-  return sh.so3_right ? launch_psp_epoch_sr<1>(dof, st, b, sh, ea, grid, ev_any)
-                      : launch_psp_epoch_sr<0>(dof, st, b, sh, ea, grid, ev_any);
+                            int64_t grid, uint32_t ev_any, uint32_t lds_pad) {
+  return sh.so3_right ? launch_psp_epoch_sr<1>(dof, st, b, sh, ea, grid, ev_any, lds_pad)
+                      : launch_psp_epoch_sr<0>(dof, st, b, sh, ea, grid, ev_any, lds_pad);
 }
 
 hipError_t launch_psp_efforts_vo(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,

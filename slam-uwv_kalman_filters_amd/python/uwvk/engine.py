@@ -177,6 +177,11 @@ class PoseUKFBatch:
         (PSP, dense, literal), like the oracle's or_set_so3_right."""
         _chk(self.L.uwvk_pose_set_option(self.h, 5, int(bool(on))), "set_option")
 
+    def set_lds_pad(self, nbytes):
+        """UWVK_OPT_LDS_PAD (diagnostic): dynamic LDS bytes per PSP epoch
+        workgroup, unused, to lower its occupancy (epoch-kernel occupancy sweep)."""
+        _chk(self.L.uwvk_pose_set_option(self.h, 7, int(nbytes)), "set_option")
+
     def set_tail_chunks(self, chunks):
         """UWVK_OPT_TAIL_CHUNKS: 0 the planner's chunk count, 2..8 forced (tests)."""
         _chk(self.L.uwvk_pose_set_option(self.h, 4, int(chunks)), "set_option")
