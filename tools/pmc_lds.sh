@@ -10,7 +10,7 @@ OUT=$PWD/gpurun_out/$TAG/s$STEPS
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 60 rocprofv3 -L > "$OUT/avail.txt" 2>&1 || true
-CMD="python3 bench.py --steps $STEPS --warmup $WARM --no-cpu-baseline"
+CMD="python3 bench.py --steps $STEPS --warmup $WARM --no-cpu-baseline ${BENCH_EXTRA:-}"  # BENCH_EXTRA: e.g. --pair
 pass() {
   timeout -s KILL 150 rocprofv3 --pmc $2 --output-format csv -d "$OUT/$1" -o run -- $CMD > "$OUT/$1.json" 2> "$OUT/$1.err" || { echo "pass $1 failed"; tail -5 "$OUT/$1.err"; exit 1; }
 }

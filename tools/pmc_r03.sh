@@ -9,7 +9,7 @@ TAG=$1; STEPS=$2; WARM=${3:-5}
 OUT=$PWD/gpurun_out/$TAG/s$STEPS
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-CMD="python3 bench.py --steps $STEPS --warmup $WARM --no-cpu-baseline"
+CMD="python3 bench.py --steps $STEPS --warmup $WARM --no-cpu-baseline ${BENCH_EXTRA:-}"  # BENCH_EXTRA: e.g. --pair
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $CMD > "$OUT/trace.json" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 1; }
 pass() {
   timeout -s KILL 150 rocprofv3 --pmc $2 --output-format csv -d "$OUT/$1" -o run -- $CMD > "$OUT/$1.json" 2> "$OUT/$1.err" || { echo "pass $1 failed"; tail -5 "$OUT/$1.err"; exit 1; }
