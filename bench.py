@@ -137,7 +137,8 @@ def parse():
     ap.add_argument("--c4-cycle", default="30,10",
                     help="C4 DVL drop-out cycle 'on,off' in s; e.g. 0.3,0.1 keeps every event rate of the 30/10 "
                          "cycle (0.25%% efforts epochs) inside a 2000-epoch window")
-    ap.add_argument("--vel-groups", type=int, default=-1, help="C2: -1 auto, 0 lane per filter, 1 16-lane rows")
+    ap.add_argument("--vel-groups", type=int, default=-1, help="C2: -1 auto, 0 lane per filter, 1 16-lane rows, 2 16-lane rows each run twice "
+                         "in a 32-lane group (diagnostic: twice the waves, same work per wave)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true", help="literal kernels (all 2n+1 sigma points)")
     ap.add_argument("--so3-left", action="store_true",
@@ -825,7 +826,9 @@ def bench_vel(a, engine, synth, world, rank, local, dist, B):
         "dtype": "f64", "data": "synthetic",
         "config": {"workload": "C2: VelocityUKF 4-DOF, batch %d per GPU, 1 kHz gyro + efforts, 5 Hz DVL, 10 Hz depth"
                                % B, "global_batch": B * world, "batch_per_gpu": B,
-                   "layout": "16 lanes per filter" if groups else "one filter per lane", "kernel": kname},
+                   "layout": {0: "one filter per lane", 1: "16 lanes per filter",
+                              2: "16 lanes per filter, each filter run twice in a 32-lane group (diagnostic)"}[groups],
+                   "kernel": kname if groups != 2 else kname + "<32>"},
         "roofline": {"bound": "valu-fp64", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                      "frac": tf / PEAK_FP64_TFLOPS, "traffic": None, "kernel": kname, "launches": launches,
                      "kernel_ms_per_launch": kernel_ms / launches, "algorithmic_flop_per_step": F_VEL_STEP,

@@ -587,7 +587,9 @@ typedef struct uwvk_vel_log {
 uwvk_status uwvk_vel_run_log(uwvk_vel* h, const uwvk_vel_log* log, int64_t first, int64_t count);
 /* UWVK_VEL_OPT_LANE_GROUPS: -1 (default) auto by batch size, 0 one filter per
  * lane (9 sigma points in one lane's registers), 1 one filter per 16-lane DPP
- * row (one sigma point per lane; fills the chip at small batches, e.g. C2's 4096). */
+ * row (one sigma point per lane; fills the chip at small batches, e.g. C2's 4096);
+ * 2 (diagnostic, r05) the 16-lane kernel with each filter duplicated in a second
+ * row that stores nothing: twice the waves, the same per-wave work. */
 #define UWVK_VEL_OPT_LANE_GROUPS 1
 uwvk_status uwvk_vel_set_option(uwvk_vel* h, int option, int value);
 /* setProcessNoiseCovariance [EXT pose_estimation base]: 4x4, shared by the

@@ -683,15 +683,22 @@ UWVK_DEV bool vg_update(double mu[4], double S[16], const double z[M], const dou
   return ok;
 }
 
-constexpr int VG = 16;  // lanes per filter
+// lanes per filter: 16 (one DPP row).  VG = 32 is a diagnostic (UWVK_VEL_OPT_LANE_GROUPS
+// 2, r05): every filter runs twice, in the two rows of its 32-lane group, and
+// only the first row stores; the wave's instruction stream is the VG = 16
+// kernel's, with half the filters per wave and twice the waves (2 per SIMD at
+// C2's batch 4,096, which needs <= 256 VGPR + AGPR: amdgpu_waves_per_eu(2)).
+// It prices the latency hiding a 32-lane split would get before any of the
+// split's own savings.
 
 // (r04) loop-invariant scalar data (Q0, the DVL covariance) loaded where it is
 // used: hoisted out of the epoch loop it held 50 SGPRs, which the register
 // allocator spilled to VGPR lanes and restored with v_readlane every epoch
 
-__global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, VelEpochArgs ea) {
+template <int VG>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(VG / 16, VG / 16))) void k_vel_epoch_g(VelBufs b, VelShared P0, VelEpochArgs ea) {
   VEL_PARAMS(b, P0);
-  const int g = (int)threadIdx.x & (VG - 1);
+  const int g = (int)threadIdx.x & 15;
   const int64_t B = b.batch, inst = (int64_t)blockIdx.x * (64 / VG) + (int)threadIdx.x / VG;
   const bool live = inst < B;
   const int64_t i = live ? inst : B - 1;  // dead groups compute on a copy and store nothing
@@ -772,6 +779,7 @@ __global__ __launch_bounds__(64) void k_vel_epoch_g(VelBufs b, VelShared P0, Vel
     }
   }
   if (!live) return;
+  if (VG == 32 && (threadIdx.x & 16)) return;  // the shadow row
   if (side) {
     if (ea.count > 0) {
 #pragma unroll
@@ -899,7 +907,7 @@ void uwvk_vel_destroy(uwvk_vel* h) {
 uwvk_status uwvk_vel_set_option(uwvk_vel* h, int option, int value) {
   UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
-  if (option != UWVK_VEL_OPT_LANE_GROUPS || value < -1 || value > 1) return UWVK_EINVAL;
+  if (option != UWVK_VEL_OPT_LANE_GROUPS || value < -1 || value > 2) return UWVK_EINVAL;
   h->groups = value;
   return UWVK_OK;
 }
@@ -1089,9 +1097,12 @@ uwvk_status uwvk_vel_run_log(uwvk_vel* h, const uwvk_vel_log* log, int64_t first
   for (int64_t e = first; e < first + count; e += kChunk) {
     ea.first = e;
     ea.count = std::min<int64_t>(kChunk, first + count - e);
-    if (groups)
-      hipLaunchKernelGGL(k_vel_epoch_g, dim3((unsigned)((h->batch + 3) / 4)), dim3(64), 0, h->stream, vbufs(h), h->P,
-                         ea);
+    if (groups && h->groups == 2)
+      hipLaunchKernelGGL(k_vel_epoch_g<32>, dim3((unsigned)((h->batch + 1) / 2)), dim3(64), 0, h->stream, vbufs(h),
+                         h->P, ea);
+    else if (groups)
+      hipLaunchKernelGGL(k_vel_epoch_g<16>, dim3((unsigned)((h->batch + 3) / 4)), dim3(64), 0, h->stream, vbufs(h),
+                         h->P, ea);
     else
       hipLaunchKernelGGL(k_vel_epoch, dim3(vgrid(h->batch)), dim3(64), 0, h->stream, vbufs(h), h->P, ea);
     HIPCHK(hipGetLastError());

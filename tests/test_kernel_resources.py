@@ -91,13 +91,17 @@ def test_velocity_kernels_have_no_scratch_round_trip(tmp_path):
                         "-S", "csrc/uwvk_vel.hip", "-o", out], cwd=PKG, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = open(out).read().split("\n")
-    st = [i for i, l in enumerate(lines) if re.match(r"^_Z\w*k_vel_epoch_g\w*:", l)][0]
-    en = [i for i, l in enumerate(lines) if i > st and l.startswith(".Lfunc_end")][0]
-    body = lines[st:en]
-    head = [i for i, l in enumerate(body) if "Loop Header: Depth=1" in l]
-    assert len(head) == 1, head
-    in_loop = [l.strip() for l in body[head[0]:] if "scratch_store" in l]
-    assert not in_loop, in_loop[:5]
+    # the shipped k_vel_epoch_g<16>; the <32> diagnostic (UWVK_VEL_OPT_LANE_GROUPS 2)
+    # is capped at 256 registers for 2 waves per SIMD and spills inside the loop
+    starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\w*k_vel_epoch_gILi16E\w*:", l)]
+    assert len(starts) == 1, starts
+    for st in starts:
+        en = [i for i, l in enumerate(lines) if i > st and l.startswith(".Lfunc_end")][0]
+        body = lines[st:en]
+        head = [i for i, l in enumerate(body) if "Loop Header: Depth=1" in l]
+        assert len(head) == 1, head
+        in_loop = [l.strip() for l in body[head[0]:] if "scratch_store" in l]
+        assert not in_loop, in_loop[:5]
 
 
 # A 64-bit scalar operand written as a 32-bit literal: gfx950 zero-extends it,

@@ -9,6 +9,7 @@ An optional "mfma" pass (tools/pmc_r03.sh) adds the f64 MFMA counters."""
 import csv
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -17,7 +18,9 @@ tag, steps = sys.argv[1], int(sys.argv[2])
 workload = sys.argv[3] if len(sys.argv) > 3 else "C3-dof53-b65536"
 rdir = sys.argv[4] if len(sys.argv) > 4 else "r05"
 base = os.path.join(ROOT, "gpurun_out", tag, "s%d" % steps)
-KERNEL = "k_psp_epoch<53"  # k_psp_epoch<53, QM> (r03: instantiated per process-noise shape)
+# k_psp_epoch<53, QM, ...> (r03: instantiated per process-noise shape); a
+# WORKLOAD ending in "-pair" folds the two-instances-per-wave k_psp2_epoch<53, SR>
+KERNEL = "k_psp2_epoch<53" if workload.endswith("-pair") else "k_psp_epoch<53"
 N_SIMD = 1024
 
 
@@ -42,10 +45,11 @@ waves = mix["SQ_WAVES"]
 # normalised per instance-epoch: one wave per instance, except that the tail
 # instances of a spread launch (UWVK_OPT_TAIL_SLOTS) run as several chunk
 # waves, so SQ_WAVES exceeds the batch; "per_wave_epoch" keeps its r02 name
-instances = int(workload.rsplit("-b", 1)[1])
+instances = int(re.search(r"-b(\d+)", workload).group(1))
 we = instances * steps
 e = {
-    "kernel": "k_psp_epoch<53, 1, 1, %d>" % (0 if workload.endswith("-left") else 1), "epochs_per_launch": steps, "waves": waves, "instances": instances,
+    "kernel": "k_psp2_epoch<53, 1>" if workload.endswith("-pair") else
+              "k_psp_epoch<53, 1, 1, %d>" % (0 if workload.endswith("-left") else 1), "epochs_per_launch": steps, "waves": waves, "instances": instances,
     "fetch_size_kib_raw": fetch["FETCH_SIZE"], "write_size_kib_raw": write["WRITE_SIZE"],
     "fetch_bytes": fetch["FETCH_SIZE"] * 1024 * 2, "write_bytes": write["WRITE_SIZE"] * 1024,
 }
