@@ -154,8 +154,6 @@ def parse():
     ap.add_argument("--lds-pad", type=int, default=0,
                     help="UWVK_OPT_LDS_PAD (diagnostic): unused dynamic LDS bytes per PSP epoch workgroup, lowering "
                          "its occupancy (use with --tail-slots -1)")
-    ap.add_argument("--pair", action="store_true",
-                    help="UWVK_OPT_PAIR: two instances per wavefront in the PSP epoch launch (DESIGN.md 6.1 A/B)")
     ap.add_argument("--config", default="",
                     help="YAML / JSON filter configuration (uwvk.config: PoseUKFConfig, UWVParameters, engine "
                          "options) instead of the synthetic defaults; the line names it in config.config_file")
@@ -535,8 +533,6 @@ def main():
         f.set_lds_pad(a.lds_pad)
     if a.persist >= 0:
         f.set_persist(a.persist)
-    if a.pair:
-        f.set_pair(True)
     if a.tail_chunks:
         f.set_tail_chunks(a.tail_chunks)
     if a.dense:
@@ -647,8 +643,6 @@ def main():
     evs = 0 if (f.epoch_qshape() != 1 or bool(((window & 0xC) != 0).any())) else 1
     sr = 0 if a.so3_left else 1
     kname = ("k_pose_epoch<%d>" % a.dof) if a.dense else ("k_psp_epoch<%d, %d, %d, %d>" % (a.dof, f.epoch_qshape(), evs, sr))
-    if a.pair and not a.dense and B % 2 == 0 and f.epoch_qshape() == 1 and evs == 1:
-        kname = "k_psp2_epoch<%d, %d>" % (a.dof, sr)
     workload = "%s-dof%d-b%d%s%s%s" % (log_mode, a.dof, B, "-dense" if a.dense else "",
                                        "-lad" if getattr(a, "literal_apply_delta", False) else "", "" if sr else "-left")
     pmc = pmc_entry(workload, a.steps)
@@ -712,7 +706,6 @@ def main():
                    "path": "dense (all 2n+1 sigma points)" if a.dense else "PSP (partitioned sigma points)",
                    "so3_boxplus": "left (nav frame, exp(d) q)" if a.so3_left else "right (body frame, q exp(d))",
                    "kernel": kname,
-                   "instances_per_wavefront": 2 if kname.startswith("k_psp2") else 1,
                    "config_file": a.config or None},
         "collective_check": coll_check,
         "roofline": roof,

@@ -455,14 +455,6 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   epoch kernel's rate against occupancy.  0 default;
  *   use with UWVK_OPT_TAIL_SLOTS < 0 (the tail planner assumes no pad). */
 #define UWVK_OPT_LDS_PAD 7
-/* UWVK_OPT_PAIR (r05): 1 runs the PSP run_log launch with two instances per
- *   wavefront (row phases per instance over 64 lanes, sigma-point phases of the
- *   two instances side by side in the two 32-lane halves; DESIGN.md section
- *   6.1) wherever it applies: even batch, the lane-resident process noise
- *   (uwvk_pose_epoch_qshape 1), no pressure / ADCP event in the launch, not
- *   persistent; no tail spreading.  Other launches keep one instance per
- *   wavefront.  Results equal the default path's to rounding.  0 default. */
-#define UWVK_OPT_PAIR 8
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
 /* Host-only query (no device work): the chunks per tail instance the
  * UWVK_OPT_TAIL_SLOTS planner picks for one XCD's instances over its resident

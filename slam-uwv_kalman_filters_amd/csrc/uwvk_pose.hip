@@ -67,7 +67,6 @@ struct uwvk_pose {
   // it holds when the next launch starts (every launch takes units + grid)
   int persist = 0;
   uint32_t lds_pad = 0;  // UWVK_OPT_LDS_PAD (diagnostic occupancy sweep)
-  int pair = 0;          // UWVK_OPT_PAIR: two instances per wavefront where it applies
   uint32_t* d_ticket = nullptr;
   uint32_t ticket_next = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -760,23 +759,17 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     int64_t grid = 0;
     uint32_t ev_any = 0;  // the event kinds of this launch's epochs (kernel choice)
     for (int64_t k = e; k < last; k++) ev_any |= hf[k - first];
-    if (h->pair && h->batch % 2 == 0 && q_is_simple(h) && !h->persist &&
-        !(ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP))) {
-      ea.ticket = nullptr;
-      HIPCHK(launch_psp2_epoch(h->dof, h->stream, b, sh, ea));
-    } else {
-      HIPCHK(prepare_tail(h, ea, grid));
-      if (launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid, ev_any, h->lds_pad) != hipSuccess) {
-        // a persistent launch that did not run took no tickets: restart the
-        // counter from zero (stream-ordered, before any later launch)
-        if (ea.ticket) {
-          h->ticket_next = 0;
-          (void)hipMemsetAsync(h->d_ticket, 0, 4, h->stream);
-        }
-        return UWVK_EDEVICE;
+    HIPCHK(prepare_tail(h, ea, grid));
+    if (launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid, ev_any, h->lds_pad) != hipSuccess) {
+      // a persistent launch that did not run took no tickets: restart the
+      // counter from zero (stream-ordered, before any later launch)
+      if (ea.ticket) {
+        h->ticket_next = 0;
+        (void)hipMemsetAsync(h->d_ticket, 0, 4, h->stream);
       }
-      if (ea.ticket) h->ticket_next += ea.units;  // the tickets the launch takes
+      return UWVK_EDEVICE;
     }
+    if (ea.ticket) h->ticket_next += ea.units;  // the tickets the launch takes
     if (r < first + count) {
       ea.first = r;
       ea.count = 1;
@@ -844,10 +837,6 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
   }
   if (option == UWVK_OPT_PERSIST) {
     h->persist = value ? 1 : 0;
-    return UWVK_OK;
-  }
-  if (option == UWVK_OPT_PAIR) {
-    h->pair = value ? 1 : 0;
     return UWVK_OK;
   }
   if (option == UWVK_OPT_LDS_PAD) {  // diagnostic: occupancy sweep of the epoch kernel

@@ -20,13 +20,6 @@ extern template hipError_t launch_psp_efforts_vo_sr<0>(int, hipStream_t, const P
                                                        const EpochArgs&);
 extern template hipError_t launch_psp_efforts_vo_sr<1>(int, hipStream_t, const PoseBufs&, const PoseShared&,
                                                        const EpochArgs&);
-template <int SR>
-hipError_t launch_psp2_epoch_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
-                                const EpochArgs& ea);
-extern template hipError_t launch_psp2_epoch_sr<0>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                   const EpochArgs&);
-extern template hipError_t launch_psp2_epoch_sr<1>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                   const EpochArgs&);
 extern template hipError_t launch_psp_predict_sr<0>(int, hipStream_t, const PoseBufs&, const PoseShared&, double);
 extern template hipError_t launch_psp_predict_sr<1>(int, hipStream_t, const PoseBufs&, const PoseShared&, double);
 extern template hipError_t launch_psp_update_sr<0>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
@@ -41,9 +34,6 @@ extern template hipError_t launch_psp_epoch_sr<1>(int, hipStream_t, const PoseBu
 hipError_t launch_psp_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt);
 hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                              const MeasArgs& ma, int m);
-// two instances per wavefront (UWVK_OPT_PAIR): epochs [ea.first, + ea.count) of
-// an even batch, C3 events only (acceleration, DVL), lane-resident Q
-hipError_t launch_psp2_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea);
 // run_log's velocity-only BodyEfforts epoch ea.first (constrainVelocity, PEffVO)
 hipError_t launch_psp_efforts_vo(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                                  const EpochArgs& ea);

@@ -26,7 +26,6 @@
 #define UWVK_POSE_KERNEL_BODIES
 #include "uwvk_pose_kernels.hpp"
 #include "uwvk_psp_dev.hpp"
-#include "uwvk_psp2_dev.hpp"
 #include "uwvk_psp.hpp"
 
 
@@ -653,132 +652,6 @@ __global__ __launch_bounds__(64) void k_psp_efforts_vo(PoseBufs b, PoseShared sh
   store_psp<DOF>(sm, b, inst);
 }
 
-// Two instances per wavefront (uwvk_psp2_dev.hpp, UWVK_OPT_PAIR): instances
-// 2 P and 2 P + 1 of pair P (XCD-ordered like xcd_instance), the C3 event set
-// (acceleration, DVL; no pressure / ADCP / efforts in the launch), the
-// lane-resident process noise (QM = 1), no tail spreading.  A NaN measurement
-// of one instance runs the other's update through the one-instance code.
-template <int DOF, int SR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_psp2_epoch(PoseBufs b,
-                                                                                               PoseShared sh0,
-                                                                                               EpochArgs ea) {
-  __shared__ PspSmem<DOF> smA, smB;
-  const int64_t B = b.batch;
-  const int64_t pr = xcd_instance(B >> 1);
-  const int64_t iA = 2 * pr, iB = iA + 1;
-  const int lp = lane_id();
-  const LaneQ lq = lane_q<DOF>(b.Qp, lp);
-  bool okA = true, okB = true, nanA = false, nanB = false;
-  uint32_t dvlA = 0, dvlB = 0;
-  MeasArgs ma{};
-  ProcCtx pcA, pcB;
-  for (int k = 0; k < 3; k++) {
-    pcA.w[k] = b.rot[iA * 3 + k];
-    pcB.w[k] = b.rot[iB * 3 + k];
-  }
-  {
-    double dtv = ea.dt;
-    asm volatile("" : "+v"(dtv));
-    pcA.dt = dtv;
-    pcB.dt = dtv;
-  }
-  pcA.off = nullptr;
-  pcB.off = nullptr;
-  lane_proc<DOF>(b, *b.shared, iA, lp, pcA);
-  lane_proc<DOF>(b, *b.shared, iB, lp, pcB);
-  const int64_t e_begin = ea.first, e_end = ea.first + ea.count;
-  uint32_t fl_n = 0;
-  double gA_n[3] = {0, 0, 0}, aA_n[3] = {0, 0, 0}, gB_n[3] = {0, 0, 0}, aB_n[3] = {0, 0, 0};
-  auto fetch = [&](int64_t e) {
-    fl_n = ea.flags[e];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      gA_n[k] = ea.gyro[(e * B + iA) * 3 + k];
-      aA_n[k] = ea.acc[(e * B + iA) * 3 + k];
-      gB_n[k] = ea.gyro[(e * B + iB) * 3 + k];
-      aB_n[k] = ea.acc[(e * B + iB) * 3 + k];
-    }
-  };
-  if (e_end > e_begin) fetch(e_begin);
-  load_psp<DOF>(smA, b, iA, lp);
-  load_psp<DOF>(smB, b, iB, lp);
-  double dsA = 1.0, idsA = 1.0, dsB = 1.0, idsB = 1.0;
-#pragma unroll 1
-  for (int64_t e = e_begin; e < e_end; e++) {
-    const uint32_t fl = fl_n;
-    const double gA[3] = {gA_n[0], gA_n[1], gA_n[2]}, gB[3] = {gB_n[0], gB_n[1], gB_n[2]};
-    const double zA[3] = {aA_n[0], aA_n[1], aA_n[2]}, zB[3] = {aB_n[0], aB_n[1], aB_n[2]};
-    if (e + 1 < e_end) fetch(e + 1);
-    if (all_finite(gA, 3)) {
-      for (int k = 0; k < 3; k++) pcA.w[k] = gA[k];
-    } else {
-      nanA = true;
-    }
-    if (all_finite(gB, 3)) {
-      for (int k = 0; k < 3; k++) pcB.w[k] = gB[k];
-    } else {
-      nanB = true;
-    }
-    const PoseShared& sh = shared_for_epoch(b);
-    if (((e - ea.first) & 1023) == 1023) {
-      psp_fold<DOF>(smA, dsA, idsA);
-      psp_fold<DOF>(smB, dsB, idsB);
-    }
-    bool sA = true, sB = true;
-    psp2::psp2_predict<DOF, SR>(smA, smB, sh, pcA, pcB, dsA, idsA, dsB, idsB, lq, &sA, &sB);
-    okA = okA && sA;
-    okB = okB && sB;
-    auto upd2 = [&](const auto& hm, const double* zpA, const double* zpB, const double* R, uint32_t* cA,
-                    uint32_t* cB) {
-      using HM = std::decay_t<decltype(hm)>;
-      const bool fA = all_finite(zpA, 3), fB = all_finite(zpB, 3);
-      nanA = nanA || !fA;
-      nanB = nanB || !fB;
-      double z3A[3] = {zpA[0], zpA[1], zpA[2]}, z3B[3] = {zpB[0], zpB[1], zpB[2]}, R9[9];
-      for (int k = 0; k < 9; k++) R9[k] = R[k];
-      bool uA = true, uB = true, accA = false, accB = false;
-      if (fA && fB) {
-        psp2::psp2_update<DOF, SR, HM>(smA, smB, z3A, z3B, R9, 0, hm, &uA, &uB, &accA, &accB, dsA, idsA, dsB, idsB);
-      } else if (fA) {
-        accA = psp_update<DOF, SR>(smA, z3A, R9, 0, hm, &uA, dsA, idsA);
-      } else if (fB) {
-        accB = psp_update<DOF, SR>(smB, z3B, R9, 0, hm, &uB, dsB, idsB);
-      }
-      okA = okA && uA;
-      okB = okB && uB;
-      if (cA) *cA += (fA && accA) ? 1u : 0u;
-      if (cB) *cB += (fB && accB) ? 1u : 0u;
-    };
-    if (fl & UWVK_EV_ACC) upd2(PAcc<DOF>{}, zA, zB, sh.log_acc_cov, nullptr, nullptr);
-    if (fl & UWVK_EV_DVL) {
-      const double* zdA = ea.dvl + ((int64_t)ea.dvl_index[e] * B + iA) * 3;
-      const double* zdB = ea.dvl + ((int64_t)ea.dvl_index[e] * B + iB) * 3;
-      upd2(PVel<DOF>{}, zdA, zdB, sh.log_dvl_cov, &dvlA, &dvlB);
-    }
-  }
-  (void)ma;
-  if (lane_id() == 0) {
-    const uint32_t bA = (okA ? 0u : UWVK_ST_NOTPD) | (nanA ? UWVK_ST_NAN : 0u);
-    const uint32_t bB = (okB ? 0u : UWVK_ST_NOTPD) | (nanB ? UWVK_ST_NAN : 0u);
-    if (bA) __hip_atomic_fetch_or(b.status + iA, bA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (bB) __hip_atomic_fetch_or(b.status + iB, bB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (e_end > e_begin) {
-      for (int k = 0; k < 3; k++) {
-        b.rot[iA * 3 + k] = pcA.w[k];
-        b.rot[iB * 3 + k] = pcB.w[k];
-      }
-    }
-    if (ea.accept_counts) {
-      ea.accept_counts[iA * 4] += dvlA;
-      ea.accept_counts[iB * 4] += dvlB;
-    }
-  }
-  psp_fold<DOF>(smA, dsA, idsA);
-  psp_fold<DOF>(smB, dsB, idsB);
-  store_psp<DOF>(smA, b, iA, lp);
-  store_psp<DOF>(smB, b, iB, lp);
-}
-
 }  // namespace psp
 
 template <int DOF, int SR>
@@ -828,17 +701,6 @@ hipError_t launch_psp_efforts_vo_sr(int dof, hipStream_t st, const PoseBufs& b, 
   return hipGetLastError();
 }
 
-template <int SR>
-hipError_t launch_psp2_epoch_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
-                                const EpochArgs& ea) {
-  const dim3 g((unsigned)(b.batch / 2));
-  if (dof == 53)
-    hipLaunchKernelGGL((psp::k_psp2_epoch<53, SR>), g, dim3(64), 0, st, b, sh, ea);
-  else
-    hipLaunchKernelGGL((psp::k_psp2_epoch<26, SR>), g, dim3(64), 0, st, b, sh, ea);
-  return hipGetLastError();
-}
-
 template <int DOF, int QM, int EVS, int SR>
 static void launch_epoch_q(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea, dim3 g,
                            uint32_t pad) {
@@ -879,8 +741,6 @@ template hipError_t launch_psp_epoch_sr<PSP_SIDE>(int, hipStream_t, const PoseBu
                                                   const EpochArgs&, int64_t, uint32_t, uint32_t);
 template hipError_t launch_psp_efforts_vo_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&,
                                                        const EpochArgs&);
-template hipError_t launch_psp2_epoch_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                   const EpochArgs&);
 
 #if PSP_SIDE == 0
 // the handle's side picks the instantiation set (a template parameter of every
@@ -899,10 +759,6 @@ hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const Po
                             int64_t grid, uint32_t ev_any, uint32_t lds_pad) {
   return sh.so3_right ? launch_psp_epoch_sr<1>(dof, st, b, sh, ea, grid, ev_any, lds_pad)
                       : launch_psp_epoch_sr<0>(dof, st, b, sh, ea, grid, ev_any, lds_pad);
-}
-
-hipError_t launch_psp2_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea) {
-  return sh.so3_right ? launch_psp2_epoch_sr<1>(dof, st, b, sh, ea) : launch_psp2_epoch_sr<0>(dof, st, b, sh, ea);
 }
 
 hipError_t launch_psp_efforts_vo(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,

@@ -182,11 +182,6 @@ class PoseUKFBatch:
         workgroup, unused, to lower its occupancy (epoch-kernel occupancy sweep)."""
         _chk(self.L.uwvk_pose_set_option(self.h, 7, int(nbytes)), "set_option")
 
-    def set_pair(self, on=True):
-        """UWVK_OPT_PAIR: two instances per wavefront in the run_log launches it
-        applies to (even batch, lane-resident Q, no pressure / ADCP events)."""
-        _chk(self.L.uwvk_pose_set_option(self.h, 8, int(bool(on))), "set_option")
-
     def set_tail_chunks(self, chunks):
         """UWVK_OPT_TAIL_CHUNKS: 0 the planner's chunk count, 2..8 forced (tests)."""
         _chk(self.L.uwvk_pose_set_option(self.h, 4, int(chunks)), "set_option")
