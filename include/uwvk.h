@@ -183,6 +183,9 @@ int uwvk_abi_version(void);
 /* 1 when a gfx950 device is visible and the kernels' code object loads. */
 int uwvk_device_available(int device);
 const char* uwvk_status_string(uwvk_status s);
+/* The HIP error (name, message, failing entry point) behind the calling host
+ * thread's most recent UWVK_EDEVICE, "" if none (diagnostics). */
+const char* uwvk_last_device_error(void);
 
 /* device memory helpers for device-resident logs (bench / run_log).
  * uwvk_memcpy_h2d / _d2h are synchronous with all work on the device that owns

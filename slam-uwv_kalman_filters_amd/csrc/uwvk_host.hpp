@@ -9,6 +9,10 @@
 #include "../../include/uwvk.h"
 
 namespace uwvk {
+
+// the last HIP error a uwvk_* call turned into UWVK_EDEVICE on this host
+// thread (uwvk_last_device_error); HIPCHK records it
+void note_hip_error(int err, const char* where);
 namespace host {
 
 inline void wgs84_radii(double lat0, double* rm, double* rn) {  // [EXT] GeographicProjection

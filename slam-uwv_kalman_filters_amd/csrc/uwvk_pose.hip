@@ -197,9 +197,13 @@ static hipError_t upload_shared(uwvk_pose* h, double dt) {
   return e;
 }
 
-#define HIPCHK(x)                              \
-  do {                                         \
-    if ((x) != hipSuccess) return UWVK_EDEVICE; \
+#define HIPCHK(x)                                  \
+  do {                                             \
+    const hipError_t e_ = (x);                     \
+    if (e_ != hipSuccess) {                        \
+      ::uwvk::note_hip_error((int)e_, __func__);   \
+      return UWVK_EDEVICE;                         \
+    }                                              \
   } while (0)
 
 
@@ -441,9 +445,9 @@ static uwvk_status launch_update(uwvk_pose* h, int m, const double* mu, const do
   ma.only_vel = only_vel;
   ma.accepted = h->d_accepted;
   PoseBufs b = bufs(h);
-  // the full BodyEfforts model is non-affine in 48 of 53 DOFs: the literal kernel;
-  // its velocity-only form (constrainVelocity, k = 9) runs on PSP
-  if ((K == MK_EFFORTS && !only_vel) || use_dense(h))
+  // BodyEfforts on PSP too (r05): the full model with k = 48 (psp_update_eff),
+  // its velocity-only form (constrainVelocity) with k = 9
+  if (use_dense(h))
     HIPCHK(launch_pose_update(h->dof, K, h->stream, b, h->sh, ma, m));
   else {
     HIPCHK(upload_shared(h, h->qp_dt));
@@ -733,9 +737,9 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   }
   // PSP: one launch per run of epochs up to and including the next BodyEfforts
   // epoch (its predict and other updates); that epoch's efforts update alone
-  // then goes through the literal efforts kernel, or, in its velocity-only form,
-  // the PSP constrainVelocity kernel (same HBM state layout).  Efforts is
-  // the last update of an epoch (the fused literal order), so the split is exact.
+  // then runs in its own one-wave PSP kernel (k_psp_efforts: the full model or
+  // its velocity-only form; its own register / LDS budget).  Efforts is the
+  // last update of an epoch (the fused literal order), so the split is exact.
   std::vector<uint32_t> fl;
   const uint32_t* hf = log->host_flags ? log->host_flags + first : nullptr;
   if (!hf && count > 0) {
@@ -773,10 +777,9 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     if (r < first + count) {
       ea.first = r;
       ea.count = 1;
-      if (hf[r - first] & UWVK_EV_EFFORTS_VELOCITY_ONLY)  // constrainVelocity: PSP (PEffVO)
-        HIPCHK(launch_psp_efforts_vo(h->dof, h->stream, b, sh, ea));
-      else  // measurementEfforts: the literal kernel
-        HIPCHK(launch_pose_efforts_epoch(h->dof, h->stream, b, sh, ea, 0));
+      // constrainVelocity (PEffVO) or the full measurementEfforts (psp_update_eff)
+      const int vo = (hf[r - first] & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0;
+      HIPCHK(launch_psp_efforts(h->dof, vo, h->stream, b, sh, ea));
     }
     e = last;
   }

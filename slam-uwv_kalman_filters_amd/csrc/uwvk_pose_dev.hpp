@@ -1137,7 +1137,12 @@ struct Efforts6 {
   UWVK_DEV double m(int which, int r, int c, const BLK& blk) const {
     const int k = blk_index(r, c);
     if (k >= 0 && blk.has) return blk.v[which * 9 + k];
-    return base[which * 36 + r * 6 + c];
+    // the batch-shared base matrices by scalar loads: base is global memory no
+    // kernel writes, read through the constant address space (s_load into
+    // SGPRs, used as FMA operands); as vector loads they were ~80 doubles of
+    // VGPRs held across a model evaluation
+    using CD = const __attribute__((address_space(4))) double;
+    return ((CD*)base)[which * 36 + r * 6 + c];
   }
   template <class BLK>
   UWVK_DEV void eval(const double acc6[6], const double nu[6], const double q[4], const BLK& blk, double tau[6]) const {

@@ -14,12 +14,12 @@ template <int SR>
 hipError_t launch_psp_epoch_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
                                int64_t grid, uint32_t ev_any, uint32_t lds_pad);
 template <int SR>
-hipError_t launch_psp_efforts_vo_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
-                                    const EpochArgs& ea);
-extern template hipError_t launch_psp_efforts_vo_sr<0>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                       const EpochArgs&);
-extern template hipError_t launch_psp_efforts_vo_sr<1>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                       const EpochArgs&);
+hipError_t launch_psp_efforts_sr(int dof, int vo, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                                 const EpochArgs& ea);
+extern template hipError_t launch_psp_efforts_sr<0>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
+                                                    const EpochArgs&);
+extern template hipError_t launch_psp_efforts_sr<1>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
+                                                    const EpochArgs&);
 extern template hipError_t launch_psp_predict_sr<0>(int, hipStream_t, const PoseBufs&, const PoseShared&, double);
 extern template hipError_t launch_psp_predict_sr<1>(int, hipStream_t, const PoseBufs&, const PoseShared&, double);
 extern template hipError_t launch_psp_update_sr<0>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
@@ -34,9 +34,10 @@ extern template hipError_t launch_psp_epoch_sr<1>(int, hipStream_t, const PoseBu
 hipError_t launch_psp_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt);
 hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                              const MeasArgs& ma, int m);
-// run_log's velocity-only BodyEfforts epoch ea.first (constrainVelocity, PEffVO)
-hipError_t launch_psp_efforts_vo(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
-                                 const EpochArgs& ea);
+// run_log's BodyEfforts epoch ea.first: vo 1 the velocity-only form
+// (constrainVelocity, PEffVO), 0 the full measurementEfforts (psp_update_eff)
+hipError_t launch_psp_efforts(int dof, int vo, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                              const EpochArgs& ea);
 #include <vector>
 // grid 0: one block per instance; otherwise 8 (n_x + (chunks - 1) r_x)
 // ev_any: the OR of the launch's epoch flags (selects the kernel instantiation;

@@ -1239,6 +1239,77 @@ UWVK_DEV double hfma(double h, double x, double acc) {
   return acc + h * x;
 }
 
+// apply_delta, exact form (psp_update, psp_update_eff; delta_r in lane r):
+// mu <- mu [+] delta, Sigma <- T Sigma T^T with T
+// the identity except on the orientation block.  ukfom re-spreads X_p =
+// mu [+] +-L_j, shifts every point by delta and takes the deviations from
+// mu [+] delta; on the orientation block that deviation is, for the left
+// side, log(exp(d) exp(l) q q^-1 exp(-d)) = R(exp d) l, and for the right
+// side log(exp(-d) q^-1 q exp(l) exp(d)) = R(exp d)^T l (conjugation), so
+// T = R(exp d) (SR = 0) or R(exp d)^T = R(exp(d)^-1) (SR = 1); the vector
+// deviations are L_j unchanged.  The weights (1/2 over the 2n points) give
+// T L L^T T^T exactly.
+template <int DOF, int SR>
+UWVK_DEV void psp_apply_delta(PspSmem<DOF>& sm, double dl, int l) {
+  using L = Lay<DOF>;
+  const double dv[3] = {readlane_d(dl, 3), readlane_d(dl, 4), readlane_d(dl, 5)};
+  double R[9], eq[4];  // exp(delta_ori) once: T's rotation and the mean's [+]
+  so3_exp_psp(dv, eq);
+  {
+    const double tq[4] = {eq[0], SR ? -eq[1] : eq[1], SR ? -eq[2] : eq[2], SR ? -eq[3] : eq[3]};
+    qmatrix(tq, R);
+  }
+  // (r04) rows 3..5 of every column j outside the block, and the ori x ori
+  // block R B R^T: every lane loads and computes (its column clamped into
+  // the triangle; the block's lanes 3..5 and lanes >= 9 compute values that
+  // are not stored), only the stores are masked: no load waits in branches.
+  // The block is disjoint from the rows' entries, so its loads go first too.
+  double nb;
+  {
+    const int lc = l < DOF ? l : DOF - 1;
+    const int Tl = (lc * (lc + 1)) >> 1;
+    const int e0 = pidx_sel_b(3, lc, Tl, LANE_IN(col_ge_mask<DOF>(3, false))),
+              e1 = pidx_sel_b(4, lc, Tl, LANE_IN(col_ge_mask<DOF>(4, false))),
+              e2 = pidx_sel_b(5, lc, Tl, LANE_IN(col_ge_mask<DOF>(5, false)));
+    double s0 = sm.S[e0], s1 = sm.S[e1], s2 = sm.S[e2];
+    asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2));  // loaded here, not sunk into the store branch
+    double B[9];
+#pragma unroll
+    for (int u = 0; u < 3; u++)
+#pragma unroll
+      for (int v = 0; v < 3; v++) B[u * 3 + v] = sm.S[pidx(3 + u, 3 + v)];
+    const int r = l / 3, c = l % 3;  // (r >= 3 for lanes >= 9: not stored)
+    double sb = 0.0;
+#pragma unroll
+    for (int u = 0; u < 3; u++) {
+      double t = 0.0;
+#pragma unroll
+      for (int v = 0; v < 3; v++) t += B[u * 3 + v] * sel3(R[v], R[3 + v], R[6 + v], c);
+      sb += sel3(R[u], R[3 + u], R[6 + u], r) * t;
+    }
+    nb = sb;
+    double n3[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) n3[i] = R[i * 3] * s0 + R[i * 3 + 1] * s1 + R[i * 3 + 2] * s2;
+    if (LANE_IF(l, l < DOF && !(l >= 3 && l < 6))) {
+      sm.S[e0] = n3[0];
+      sm.S[e1] = n3[1];
+      sm.S[e2] = n3[2];
+    }
+  }
+  // storage s = l takes tangent delta_{l} (l < 3) or delta_{l-1} (l >= 7): DPP wave_shr:1
+  const double dsh = dpp_d<0x138, 0xf, 0xf>(dl);
+  double mnew = flat(sm)[kFlatMu<DOF> + (l & 63)] + 1.0 * (LANE_IF(l, l < 3) ? dl : dsh);  // stored for the vector lanes only
+  asm volatile("" : "+v"(mnew));
+  double qn[4];
+  qplus_psp<SR>(eq, sm.mu + L::s_quat, qn);
+  psync();
+  if (LANE_IF(l, l < 9 && (l / 3) >= (l % 3))) sm.S[pidx(3 + l / 3, 3 + l % 3)] = nb;
+  if (LANE_IF(l, l < L::store && !(l >= 3 && l < 7))) sm.mu[l] = mnew;
+  if (LANE_IF(l, l < 4)) sm.mu[3 + l] = qn[l];
+  psync();
+}
+
 // ---------------------------------------------------------------------------
 // ukf::update [EXT], PSP form.  gate: 0 accept any, 1 d2p95.  Returns the gate
 // decision; *ok = false on a non-positive pivot of the partial Cholesky.
@@ -1460,74 +1531,390 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   }
   psync();
   PSP_PHASE(34);
-  // apply_delta, exact form: mu <- mu [+] delta, Sigma <- T Sigma T^T with T
-  // the identity except on the orientation block.  ukfom re-spreads X_p =
-  // mu [+] +-L_j, shifts every point by delta and takes the deviations from
-  // mu [+] delta; on the orientation block that deviation is, for the left
-  // side, log(exp(d) exp(l) q q^-1 exp(-d)) = R(exp d) l, and for the right
-  // side log(exp(-d) q^-1 q exp(l) exp(d)) = R(exp d)^T l (conjugation), so
-  // T = R(exp d) (SR = 0) or R(exp d)^T = R(exp(d)^-1) (SR = 1); the vector
-  // deviations are L_j unchanged.  The weights (1/2 over the 2n points) give
-  // T L L^T T^T exactly.
-  {
-    const double dv[3] = {readlane_d(dl, 3), readlane_d(dl, 4), readlane_d(dl, 5)};
-    double R[9], eq[4];  // exp(delta_ori) once: T's rotation and the mean's [+]
-    so3_exp_psp(dv, eq);
-    {
-      const double tq[4] = {eq[0], SR ? -eq[1] : eq[1], SR ? -eq[2] : eq[2], SR ? -eq[3] : eq[3]};
-      qmatrix(tq, R);
-    }
-    // (r04) rows 3..5 of every column j outside the block, and the ori x ori
-    // block R B R^T: every lane loads and computes (its column clamped into
-    // the triangle; the block's lanes 3..5 and lanes >= 9 compute values that
-    // are not stored), only the stores are masked: no load waits in branches.
-    // The block is disjoint from the rows' entries, so its loads go first too.
-    double nb;
-    {
-      const int lc = l < DOF ? l : DOF - 1;
-      const int Tl = (lc * (lc + 1)) >> 1;
-      const int e0 = pidx_sel_b(3, lc, Tl, LANE_IN(col_ge_mask<DOF>(3, false))),
-                e1 = pidx_sel_b(4, lc, Tl, LANE_IN(col_ge_mask<DOF>(4, false))),
-                e2 = pidx_sel_b(5, lc, Tl, LANE_IN(col_ge_mask<DOF>(5, false)));
-      double s0 = sm.S[e0], s1 = sm.S[e1], s2 = sm.S[e2];
-      asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2));  // loaded here, not sunk into the store branch
-      double B[9];
-#pragma unroll
-      for (int u = 0; u < 3; u++)
-#pragma unroll
-        for (int v = 0; v < 3; v++) B[u * 3 + v] = sm.S[pidx(3 + u, 3 + v)];
-      const int r = l / 3, c = l % 3;  // (r >= 3 for lanes >= 9: not stored)
-      double sb = 0.0;
-#pragma unroll
-      for (int u = 0; u < 3; u++) {
-        double t = 0.0;
-#pragma unroll
-        for (int v = 0; v < 3; v++) t += B[u * 3 + v] * sel3(R[v], R[3 + v], R[6 + v], c);
-        sb += sel3(R[u], R[3 + u], R[6 + u], r) * t;
-      }
-      nb = sb;
-      double n3[3];
-#pragma unroll
-      for (int i = 0; i < 3; i++) n3[i] = R[i * 3] * s0 + R[i * 3 + 1] * s1 + R[i * 3 + 2] * s2;
-      if (LANE_IF(l, l < DOF && !(l >= 3 && l < 6))) {
-        sm.S[e0] = n3[0];
-        sm.S[e1] = n3[1];
-        sm.S[e2] = n3[2];
-      }
-    }
-    // storage s = l takes tangent delta_{l} (l < 3) or delta_{l-1} (l >= 7): DPP wave_shr:1
-    const double dsh = dpp_d<0x138, 0xf, 0xf>(dl);
-    double mnew = flat(sm)[kFlatMu<DOF> + (l & 63)] + 1.0 * (LANE_IF(l, l < 3) ? dl : dsh);  // stored for the vector lanes only
-    asm volatile("" : "+v"(mnew));
-    double qn[4];
-    qplus_psp<SR>(eq, sm.mu + L::s_quat, qn);
-    psync();
-    if (LANE_IF(l, l < 9 && (l / 3) >= (l % 3))) sm.S[pidx(3 + l / 3, 3 + l % 3)] = nb;
-    if (LANE_IF(l, l < L::store && !(l >= 3 && l < 7))) sm.mu[l] = mnew;
-    if (LANE_IF(l, l < 4)) sm.mu[3 + l] = qn[l];
-    psync();
-  }
+  psp_apply_delta<DOF, SR>(sm, dl, l);
   PSP_PHASE(35);
+  return true;
+}
+
+
+// ---------------------------------------------------------------------------
+// measurementEfforts (PoseUKF.cpp:153-196), the full BodyEfforts update, in PSP
+// form on one wave per instance (r05; the literal two-wave kernel stays on
+// UWVK_OPT_DENSE_SIGMA).  The model is non-affine in K = HJmax DOFs (48 of 53:
+// orientation, velocity, acceleration, the 27 model parameters, the water
+// velocity; 21 of 26) and reads none after them, so PSP's prefix is k = K:
+// 2K + 1 model evaluations and no affine part (H = 0), i.e. the literal
+// update's algebra with the points j >= K folded into the centre.  LDS is the
+// epoch kernel's PspSmem (12.8 KB):
+//  - Sigma's Cholesky factor overwrites the packed triangle (all DOF columns,
+//    so the positive-definiteness flag is the literal factor's), in panels of
+//    16 columns: the panel's update by the columns before it on
+//    v_mfma_f64_16x16x4 tiles (A = -L[rows][k], B = L[panel][k]^T, the
+//    accumulator the panel's entries), then the panel's columns right-looking,
+//    lane r holding row r of the panel in registers;
+//  - lane j < K evaluates mu [+] L_j and mu [+] -L_j, lane K the centre;
+//  - C = 1/2 L_a Dz^T with Dz staged 16 columns at a time in stg, the 27
+//    sums of z through the factor's area (dead by then), Sigma re-read from
+//    HBM, Sigma -= C K^T as two rank-3 MFMA passes, the exact apply_delta.
+// ---------------------------------------------------------------------------
+// S[rows >= P][P, P + W) -= L[rows][0, P) L[P, P + W)[0, P)^T.  Tile t holds
+// rows P + 16 t + (l >> 4) + 4 i, column P + (l & 15) (the f64 C/D map); A
+// lane l: row P + 16 t + (l & 15), k = 4 s + (l >> 4); B lane l: k = 4 s +
+// (l >> 4), column P + (l & 15).  Entries outside the triangle are clamped
+// into it for the load and not stored; only columns >= P are written, only
+// columns < P are read as operands, so the tiles need no ordering.
+template <int DOF, int P, int W>
+UWVK_DEV void eff_chol_update(double* S, int l) {
+  constexpr int NRT = (DOF - P + 15) / 16, NS = P / 4;
+  const int q = (l >> 4) & 3, c = l & 15;
+  const int bc = P + c < DOF ? P + c : DOF - 1;
+  const double* Bp = S + ((bc * (bc + 1)) >> 1);
+  const bool bv = c < W;  // P + c < DOF
+  double Bop[NS];
+#pragma unroll
+  for (int s = 0; s < NS; s++) Bop[s] = bv ? Bp[4 * s + q] : 0.0;
+#pragma unroll
+  for (int t = 0; t < NRT; t++) {
+    const int ar = P + 16 * t + c;
+    const int arc = ar < DOF ? ar : DOF - 1;
+    const double* Ap = S + ((arc * (arc + 1)) >> 1);
+    const bool av = ar < DOF;
+    int idx[4];
+    bool st[4];
+    d4_t acc;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int row = P + 16 * t + q + 4 * i, col = P + c;
+      st[i] = row < DOF && bv && col <= row;
+      const int rr = row < DOF ? row : DOF - 1;
+      const int cc = col <= rr ? col : rr;
+      idx[i] = ((rr * (rr + 1)) >> 1) + cc;
+      acc[i] = S[idx[i]];
+    }
+#pragma unroll
+    for (int s = 0; s < NS; s++) acc = mfma_f64(av ? -Ap[4 * s + q] : 0.0, Bop[s], acc);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (st[i]) S[idx[i]] = acc[i];
+  }
+}
+
+// column P + J of the panel: pivot from lane P + J's registers, the column
+// broadcast through col (lane r writes slot r; one wave: LDS in order)
+template <int P, int W, int J>
+UWVK_DEV void eff_chol_step(double (&a)[W], int r, bool& ok, double* col) {
+  if constexpr (J < W) {
+    const double piv = readlane_d(a[J], P + J);
+    ok = ok && (piv > 0.0);
+    const double inv = rsqrt_f64(piv);
+    a[J] = LANE_IF(r, r >= P + J) ? a[J] * inv : 0.0;  // lane P + J: piv / sqrt(piv)
+    if constexpr (J + 1 < W) {
+      col[r & 63] = a[J];
+      wsync();
+#pragma unroll
+      for (int c = J + 1; c < W; c++) a[c] -= a[J] * col[P + c];
+#pragma unroll
+      for (int c = J + 1; c < W; c++) asm volatile("" : "+v"(a[c]));
+    }
+    eff_chol_step<P, W, J + 1>(a, r, ok, col);
+  }
+}
+
+// lanes l in [P + c, LIM) for each panel column c, as constant masks
+struct PanelMasks {
+  unsigned long long m[16];
+};
+template <int P, int W, int LIM>
+UWVK_DEV constexpr PanelMasks panel_masks() {
+  PanelMasks g{};
+  for (int c = 0; c < W; c++) {
+    unsigned long long m = 0;
+    for (int i = 0; i < 64; i++)
+      if (i >= P + c && i < LIM) m |= 1ull << i;
+    g.m[c] = m;
+  }
+  return g;
+}
+
+template <int DOF, int P>
+UWVK_DEV void eff_chol(double* S, double* col, int l, bool& ok) {
+  if constexpr (P < DOF) {
+    constexpr int W = DOF - P < 16 ? DOF - P : 16;
+    if constexpr (P > 0) {
+      eff_chol_update<DOF, P, W>(S, l);
+      psync();
+    }
+    // lanes >= DOF shadow the last row (never stored); a row above the panel
+    // column reads a later entry of the triangle, selected away
+    const int rr = l < DOF ? l : DOF - 1;
+    double* Sr = S + ((rr * (rr + 1)) >> 1) + P;
+    constexpr PanelMasks ld = panel_masks<P, W, 64>(), stm = panel_masks<P, W, DOF>();
+    double a[W];
+#pragma unroll
+    for (int c = 0; c < W; c++) {
+      const double v = Sr[c];
+      a[c] = LANE_IN(ld.m[c]) ? v : 0.0;
+    }
+    eff_chol_step<P, W, 0>(a, l, ok, col);
+#pragma unroll
+    for (int c = 0; c < W; c++)
+      if (LANE_IN(stm.m[c])) Sr[c] = a[c];
+    psync();
+    eff_chol<DOF, P + 16>(S, col, l, ok);
+  }
+}
+
+// point mu [+] sg L_j over the first K DOFs (L in place in S; L[d][j] = 0 for
+// j > d); sg = 0: the centre, bitwise mu.  The orientation first
+// (eff_point_quat), for both signs before any model evaluation: so3_exp_psp's
+// library fallback then runs with almost nothing else live (inside an
+// evaluation it stacked ~90 VGPRs on the model's)
+template <int DOF, int SR>
+UWVK_DEV void eff_point_quat(const PspSmem<DOF>& sm, int j, double sg, double (&q)[4]) {
+  using L = Lay<DOF>;
+  double v[3];
+#pragma unroll
+  for (int d = 3; d < 6; d++) {
+    const bool in = j <= d;
+    const double ld = sm.S[d * (d + 1) / 2 + (in ? j : d)];
+    v[d - 3] = sg * (in ? ld : 0.0);
+  }
+  double e[4];
+  so3_exp_psp(v, e);
+  qplus_psp<SR>(e, sm.mu + L::s_quat, q);
+}
+template <int DOF, int K, class HM>
+UWVK_DEV void eff_point(const PspSmem<DOF>& sm, const HM& h, int j, double sg, const double (&q)[4],
+                        double (&z)[6]) {
+  using L = Lay<DOF>;
+  double x[L::store];
+#pragma unroll
+  for (int s = 0; s < L::store; s++) x[s] = sm.mu[s];
+#pragma unroll
+  for (int i = 0; i < 4; i++) x[L::s_quat + i] = q[i];
+#pragma unroll
+  for (int d = 0; d < K; d++) {
+    if (d >= 3 && d < 6) continue;
+    const bool in = j <= d;
+    const double ld = sm.S[d * (d + 1) / 2 + (in ? j : d)];
+    x[d2s(d)] = sm.mu[d2s(d)] + sg * (in ? ld : 0.0);
+  }
+  h(x, z);
+}
+
+// R sums over NL lanes through a CAP-double buffer, in rounds of CAP / NL rows
+template <int R, int NL, int CAP, int C0 = 0>
+UWVK_DEV void lds_sums_cap(const double (&v)[R], double* buf, int l, double (&out)[R]) {
+  if constexpr (C0 < R) {
+    constexpr int CH0 = CAP / NL, CH = (R - C0) < CH0 ? (R - C0) : CH0;
+    static_assert(NL % 2 == 0 && NL <= 64 && CH0 >= 1, "transpose buffer");
+    if (l < NL) {
+#pragma unroll
+      for (int i = 0; i < CH; i++) buf[i * NL + l] = v[C0 + i];
+    }
+    wsync();
+    const double* row = buf + (l < CH ? l : 0) * NL;
+    double p[NL / 2];
+#pragma unroll
+    for (int k = 0; k < NL / 2; k++) p[k] = row[2 * k] + row[2 * k + 1];
+#pragma unroll
+    for (int w = 1; w < NL / 2; w *= 2)
+#pragma unroll
+      for (int k = 0; k + w < NL / 2; k += 2 * w) p[k] += p[k + w];
+#pragma unroll
+    for (int i = 0; i < CH; i++) out[C0 + i] = readlane_d(p[0], i);
+    wsync();  // every lane's reads of this round before the next round's writes
+    lds_sums_cap<R, NL, CAP, C0 + CH>(v, buf, l, out);
+  }
+}
+
+// S x = b for a symmetric positive definite M x M S (lower triangle packed,
+// row i at i (i + 1) / 2): S = L L^T (1 / L_ii kept), then two substitutions
+template <int M>
+UWVK_DEV void spd_factor(const double (&S)[M * (M + 1) / 2], double (&L)[M * (M + 1) / 2], double (&idg)[M]) {
+#pragma unroll
+  for (int j = 0; j < M; j++) {
+    double d = S[j * (j + 1) / 2 + j];
+#pragma unroll
+    for (int k = 0; k < j; k++) d -= L[j * (j + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+    idg[j] = rsqrt_f64(d);
+    L[j * (j + 1) / 2 + j] = d * idg[j];
+#pragma unroll
+    for (int i = j + 1; i < M; i++) {
+      double t = S[i * (i + 1) / 2 + j];
+#pragma unroll
+      for (int k = 0; k < j; k++) t -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+      L[i * (i + 1) / 2 + j] = t * idg[j];
+    }
+  }
+}
+template <int M>
+UWVK_DEV void spd_solve(const double (&L)[M * (M + 1) / 2], const double (&idg)[M], const double (&b)[M],
+                        double (&x)[M]) {
+  double y[M];
+#pragma unroll
+  for (int i = 0; i < M; i++) {
+    double t = b[i];
+#pragma unroll
+    for (int k = 0; k < i; k++) t -= L[i * (i + 1) / 2 + k] * y[k];
+    y[i] = t * idg[i];
+  }
+#pragma unroll
+  for (int i = M - 1; i >= 0; i--) {
+    double t = y[i];
+#pragma unroll
+    for (int k = i + 1; k < M; k++) t -= L[k * (k + 1) / 2 + i] * x[k];
+    x[i] = t * idg[i];
+  }
+}
+
+// the full BodyEfforts update (gate: accept any).  sig_hbm: the instance's
+// Sigma in HBM (what sm.S held before the factor overwrote it); z and R are
+// read where they are used (held in registers through the factor and the
+// points they were 84 VGPRs of the kernel's peak)
+template <int DOF, int SR, class HM>
+UWVK_DEV bool psp_update_eff(PspSmem<DOF>& sm, const double* sig_hbm, const HM& h, const double* z,
+                             const double* Rm, bool* ok) {
+  using G = PG<DOF>;
+  constexpr int M = 6, K = HJmax<HM, DOF>::value, NL = (K + 2) & ~1;
+  static_assert(K < 64 && NL <= 64, "one point pair per lane, the centre in lane K");
+  int l = olane();
+  bool cok = true;
+  eff_chol<DOF, 0>(sm.S, sm.stg, l, cok);
+  l = olane();
+  const bool pt = LANE_IF(l, l < K);
+  const int j = pt ? l : 0;
+  const double sg = pt ? 1.0 : 0.0;
+  double zp[M], zn[M], zc[M];
+  {
+    // the two evaluations one after the other: a scheduling barrier and a
+    // memory clobber keep the second's LDS reads (and the values the compiler
+    // would otherwise share between them) out of the first (register peak)
+    double qp[4], qn[4];
+    eff_point_quat<DOF, SR>(sm, j, sg, qp);
+    eff_point_quat<DOF, SR>(sm, j, -sg, qn);
+    __builtin_amdgcn_sched_barrier(0);
+    eff_point<DOF, K>(sm, h, j, sg, qp, zp);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    eff_point<DOF, K>(sm, h, j, -sg, qn, zn);
+  }
+#pragma unroll
+  for (int a = 0; a < M; a++) zc[a] = readlane_d(zp[a], K);
+  // C_r = 1/2 sum_{j < K} L[r][j] Dz_j, Dz_j = z_{j+} - z_{j-} from lane j,
+  // staged CH columns at a time
+  double C[M];
+  {
+    constexpr int CH = 16;
+    static_assert(CH * M <= G::STG, "Dz chunk (PG::STG)");
+    const int rr = l < DOF ? l : DOF - 1;
+    const double* Lr = sm.S + ((rr * (rr + 1)) >> 1);
+    double c[M];
+#pragma unroll
+    for (int a = 0; a < M; a++) c[a] = 0.0;
+#pragma unroll
+    for (int j0 = 0; j0 < K; j0 += CH) {
+      if (l >= j0 && l < j0 + CH && l < K) {
+#pragma unroll
+        for (int a = 0; a < M; a++) sm.stg[(l - j0) * M + a] = zp[a] - zn[a];
+      }
+      wsync();
+#pragma unroll
+      for (int jj = 0; jj < CH && j0 + jj < K; jj++) {
+        const int jv = j0 + jj;
+        const double lv = Lr[jv <= rr ? jv : rr];
+        const double lr = jv <= rr ? lv : 0.0;
+#pragma unroll
+        for (int a = 0; a < M; a++) c[a] += lr * sm.stg[jj * M + a];
+#pragma unroll
+        for (int a = 0; a < M; a++) asm volatile("" : "+v"(c[a])::"memory");
+      }
+      wsync();
+    }
+#pragma unroll
+    for (int a = 0; a < M; a++) C[a] = 0.5 * c[a];
+  }
+  psync();  // every lane's reads of L: the triangle's area takes the sums
+  constexpr int R = M + M * (M + 1) / 2;
+  double sums[R];
+  {
+    double up[M], un[M], v[R];
+#pragma unroll
+    for (int a = 0; a < M; a++) {
+      up[a] = pt ? zp[a] - zc[a] : 0.0;
+      un[a] = pt ? zn[a] - zc[a] : 0.0;
+      v[a] = up[a] + un[a];
+    }
+    int k = M;
+#pragma unroll
+    for (int a = 0; a < M; a++)
+#pragma unroll
+      for (int b2 = 0; b2 <= a; b2++) v[k++] = up[a] * up[b2] + un[a] * un[b2];
+    lds_sums_cap<R, NL, G::NP>(v, sm.S, l, sums);
+  }
+  constexpr double wc = 1.0 + 2.0 * (DOF - K);
+  constexpr int NS = M * (M + 1) / 2;
+  double Sl[NS], nu[M];  // innovation covariance (lower, packed), z - zbar
+  {
+    double m[M], e[M];
+#pragma unroll
+    for (int a = 0; a < M; a++) {
+      m[a] = sums[a] * (1.0 / (double)G::N);
+      const double zb = zc[a] + m[a];
+      e[a] = zc[a] - zb;
+      nu[a] = z[a] - zb;
+    }
+    int k = M, t = 0;
+#pragma unroll
+    for (int a = 0; a < M; a++)
+#pragma unroll
+      for (int b2 = 0; b2 <= a; b2++) {
+        const double s = sums[k++] - m[a] * sums[b2] - m[b2] * sums[a] + (2.0 * K) * m[a] * m[b2];
+        Sl[t++] = 0.5 * (s + wc * e[a] * e[b2]) + Rm[a * M + b2];
+      }
+  }
+  // K_r = S^-1 C_r (lane r), delta_r = C_r . S^-1 nu (S symmetric positive definite)
+  double Kg[M], dl = 0.0;
+  {
+    double Ls[NS], idg[M], w[M];
+    spd_factor<M>(Sl, Ls, idg);
+    spd_solve<M>(Ls, idg, nu, w);
+    spd_solve<M>(Ls, idg, C, Kg);
+#pragma unroll
+    for (int i = 0; i < M; i++) dl += C[i] * w[i];
+  }
+  *ok = cok;
+  // Sigma back from HBM (the factor and the sums overwrote the triangle)
+  {
+    double sv[G::NSLOT];
+#pragma unroll
+    for (int t = 0; t < G::NSLOT; t++) {
+      const int ee = l + 64 * t;
+      sv[t] = ee < G::NP ? sig_hbm[ee] : 0.0;
+    }
+    wsync();  // the sums' reads of the area before its rewrite
+#pragma unroll
+    for (int t = 0; t < G::NSLOT; t++) {
+      const int ee = l + 64 * t;
+      if (ee < G::NP) sm.S[ee] = sv[t];
+    }
+  }
+  psync();
+  {
+    double c0[3], k0[3], c1[3], k1[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      c0[i] = C[i];
+      k0[i] = Kg[i];
+      c1[i] = C[3 + i];
+      k1[i] = Kg[3 + i];
+    }
+    rankm_mfma_o<DOF, 3>(sm.S, sm.stg, c0, k0, l);
+    psync();
+    rankm_mfma_o<DOF, 3>(sm.S, sm.stg, c1, k1, l);
+  }
+  psync();
+  psp_apply_delta<DOF, SR>(sm, dl, l);
   return true;
 }
 

@@ -272,6 +272,35 @@ UWVK_DEV bool do_update_vo(PspSmem<DOF>& sm, const PoseShared& sh, const PoseBuf
   return psp_update<DOF, SR>(sm, z, R, 0, hm, ok, ds, ids);
 }
 
+// measurementEfforts (PoseUKF.cpp:153-196, the full model) in PSP form
+// (psp_update_eff): the inputs frozen at mu as the literal kernel's
+// do_update_efforts<DOF, 0> builds them, including its side effect on the
+// shared model (PoseUKF.cpp:173: the pre-update mean's parameter blocks)
+template <int DOF, int SR>
+UWVK_DEV bool do_update_eff(PspSmem<DOF>& sm, const PoseShared& sh, const PoseBufs& b, int64_t inst,
+                            const double* zin, const double* Rin, bool* ok) {
+  using L = Lay<DOF>;
+  HEfforts<DOF> h;
+  h.ef.base = b.uwv;
+  h.ef.weight = sh.uwv_weight;
+  h.ef.buoyancy = sh.uwv_buoyancy;
+  for (int k = 0; k < 3; k++) { h.ef.cog[k] = sh.cog[k]; h.ef.cob[k] = sh.cob[k]; }
+  const double w[3] = {b.rot[inst * 3], b.rot[inst * 3 + 1], b.rot[inst * 3 + 2]};
+  double wb[3];
+  rotation_rate_body_mu<DOF>(sm.mu, sh, w, wb);
+  for (int k = 0; k < 3; k++) { h.wb[k] = wb[k]; h.imu[k] = sh.p.imu_in_body[k]; }
+  if constexpr (L::has_params) {
+    double* model = b.model + inst * 27;
+    const int l = lane_id();
+    if (l < 9) {
+      model[l] = sm.mu[L::s_inertia + l];
+      model[9 + l] = sm.mu[L::s_lin + l];
+      model[18 + l] = sm.mu[L::s_quad + l];
+    }
+  }
+  return psp_update_eff<DOF, SR>(sm, b.sigma + inst * (int64_t)PG<DOF>::NP, h, zin, Rin, ok);
+}
+
 template <int DOF, int SR>
 __global__ __launch_bounds__(64) void k_psp_predict(PoseBufs b, PoseShared sh, double dt) {
   __shared__ PspSmem<DOF> sm;
@@ -310,7 +339,9 @@ __global__ __launch_bounds__(64) void k_psp_update(PoseBufs b, PoseShared sh, Me
   load_psp<DOF>(sm, b, inst);
   bool ok = true;
   bool acc;
-  if constexpr (KIND == MK_EFFORTS) acc = do_update_vo<DOF, SR>(sm, sh, b, inst, z, R, &ok, 1.0, 1.0);  // only_vel
+  if constexpr (KIND == MK_EFFORTS)
+    acc = ma.only_vel ? do_update_vo<DOF, SR>(sm, sh, b, inst, z, R, &ok, 1.0, 1.0)
+                      : do_update_eff<DOF, SR>(sm, sh, b, inst, z, R, &ok);
   else acc = do_update<DOF, KIND, SR>(sm, sh, inst, z, R, ma, &ok, 1.0, 1.0);
   if (lane_id() == 0) {
     if (!ok) b.status[inst] |= UWVK_ST_NOTPD;
@@ -628,12 +659,17 @@ __global__ __launch_bounds__(64) void k_psp_epoch_p(PoseBufs b, PoseShared sh0, 
   }
 }
 
-// run_log's velocity-only BodyEfforts epoch (UWVK_EV_EFFORTS_VELOCITY_ONLY):
-// after the k_psp_epoch launch that ran the epoch's predict and other updates,
-// the constrainVelocity update alone (the last update of the epoch), the same
-// bookkeeping as k_pose_efforts_epoch
-template <int DOF, int SR>
-__global__ __launch_bounds__(64) void k_psp_efforts_vo(PoseBufs b, PoseShared sh, EpochArgs ea) {
+// run_log's BodyEfforts epoch: after the k_psp_epoch launch that ran the
+// epoch's predict and other updates, the efforts update alone (the last update
+// of the epoch), VO 1 its velocity-only form (UWVK_EV_EFFORTS_VELOCITY_ONLY,
+// constrainVelocity), VO 0 the full model; the same bookkeeping as the literal
+// k_pose_efforts_epoch
+template <int DOF, int VO, int SR>
+__global__ __launch_bounds__(64)
+#ifdef EFFWPE
+__attribute__((amdgpu_waves_per_eu(EFFWPE, EFFWPE)))
+#endif
+void k_psp_efforts(PoseBufs b, PoseShared sh, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const int64_t B = b.batch, inst = xcd_instance(B), e = ea.first;
   if (!(ea.flags[e] & UWVK_EV_EFFORTS)) return;
@@ -644,7 +680,9 @@ __global__ __launch_bounds__(64) void k_psp_efforts_vo(PoseBufs b, PoseShared sh
   }
   load_psp<DOF>(sm, b, inst);
   bool ok = true;
-  const bool acc = do_update_vo<DOF, SR>(sm, sh, b, inst, z, ea.e_cov, &ok, 1.0, 1.0);
+  bool acc;
+  if constexpr (VO) acc = do_update_vo<DOF, SR>(sm, sh, b, inst, z, ea.e_cov, &ok, 1.0, 1.0);
+  else acc = do_update_eff<DOF, SR>(sm, sh, b, inst, z, ea.e_cov, &ok);
   if (lane_id() == 0) {
     if (!ok) b.status[inst] |= UWVK_ST_NOTPD;
     if (ea.accept_counts) ea.accept_counts[inst * 4 + 3] += acc ? 1u : 0u;
@@ -667,8 +705,7 @@ static hipError_t psp_update_dof(int kind, hipStream_t st, const PoseBufs& b, co
     case MK_Z: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_Z, SR>), g, t, 0, st, b, sh, ma, m); break;
     case MK_GEO: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_GEO, SR>), g, t, 0, st, b, sh, ma, m); break;
     case MK_DELAYED: hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_DELAYED, SR>), g, t, 0, st, b, sh, ma, m); break;
-    case MK_EFFORTS:  // PSP covers the velocity-only form (constrainVelocity) alone
-      if (!ma.only_vel) return hipErrorInvalidValue;
+    case MK_EFFORTS:  // the full model (psp_update_eff) or its velocity-only form (ma.only_vel)
       hipLaunchKernelGGL((psp::k_psp_update<DOF, MK_EFFORTS, SR>), g, t, 0, st, b, sh, ma, m);
       break;
     default: return hipErrorInvalidValue;
@@ -692,12 +729,16 @@ hipError_t launch_psp_update_sr(int dof, int kind, hipStream_t st, const PoseBuf
 }
 
 template <int SR>
-hipError_t launch_psp_efforts_vo_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
-                                    const EpochArgs& ea) {
-  if (dof == 53)
-    hipLaunchKernelGGL((psp::k_psp_efforts_vo<53, SR>), dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, ea);
-  else
-    hipLaunchKernelGGL((psp::k_psp_efforts_vo<26, SR>), dim3((unsigned)b.batch), dim3(64), 0, st, b, sh, ea);
+hipError_t launch_psp_efforts_sr(int dof, int vo, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                                 const EpochArgs& ea) {
+  const dim3 g((unsigned)b.batch), t(64);
+  if (dof == 53) {
+    if (vo) hipLaunchKernelGGL((psp::k_psp_efforts<53, 1, SR>), g, t, 0, st, b, sh, ea);
+    else hipLaunchKernelGGL((psp::k_psp_efforts<53, 0, SR>), g, t, 0, st, b, sh, ea);
+  } else {
+    if (vo) hipLaunchKernelGGL((psp::k_psp_efforts<26, 1, SR>), g, t, 0, st, b, sh, ea);
+    else hipLaunchKernelGGL((psp::k_psp_efforts<26, 0, SR>), g, t, 0, st, b, sh, ea);
+  }
   return hipGetLastError();
 }
 
@@ -739,8 +780,8 @@ template hipError_t launch_psp_update_sr<PSP_SIDE>(int, int, hipStream_t, const 
                                                    const MeasArgs&, int);
 template hipError_t launch_psp_epoch_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&,
                                                   const EpochArgs&, int64_t, uint32_t, uint32_t);
-template hipError_t launch_psp_efforts_vo_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                       const EpochArgs&);
+template hipError_t launch_psp_efforts_sr<PSP_SIDE>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
+                                                    const EpochArgs&);
 
 #if PSP_SIDE == 0
 // the handle's side picks the instantiation set (a template parameter of every
@@ -761,9 +802,9 @@ hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const Po
                       : launch_psp_epoch_sr<0>(dof, st, b, sh, ea, grid, ev_any, lds_pad);
 }
 
-hipError_t launch_psp_efforts_vo(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
-                                 const EpochArgs& ea) {
-  return sh.so3_right ? launch_psp_efforts_vo_sr<1>(dof, st, b, sh, ea) : launch_psp_efforts_vo_sr<0>(dof, st, b, sh, ea);
+hipError_t launch_psp_efforts(int dof, int vo, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
+                              const EpochArgs& ea) {
+  return sh.so3_right ? launch_psp_efforts_sr<1>(dof, vo, st, b, sh, ea) : launch_psp_efforts_sr<0>(dof, vo, st, b, sh, ea);
 }
 
 // XCC placement probe: block b writes the XCC it runs on (hardware XCC_ID).

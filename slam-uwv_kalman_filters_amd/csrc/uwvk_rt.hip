@@ -3,10 +3,20 @@
 // libuwvk.so: without a gfx950 device every handle creation fails loudly.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstring>
 
 #include "../../include/uwvk.h"
 #include "uwvk_dev.hpp"
+
+namespace uwvk {
+// uwvk_last_device_error: the HIP error behind the thread's last UWVK_EDEVICE
+thread_local char g_last_hip_error[160] = "";
+void note_hip_error(int err, const char* where) {
+  std::snprintf(g_last_hip_error, sizeof(g_last_hip_error), "%s: %s (in %s)", hipGetErrorName((hipError_t)err),
+                hipGetErrorString((hipError_t)err), where ? where : "?");
+}
+}  // namespace uwvk
 
 __global__ void uwvk_probe_kernel(int* out) {
   if (threadIdx.x == 0) out[0] = 0x5a5a;
@@ -33,6 +43,8 @@ int uwvk_device_available(int device) {
   (void)hipFree(d);
   return ok && h == 0x5a5a;
 }
+
+const char* uwvk_last_device_error(void) { return uwvk::g_last_hip_error; }
 
 const char* uwvk_status_string(uwvk_status s) {
   switch (s) {

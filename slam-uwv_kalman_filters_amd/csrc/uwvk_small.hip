@@ -14,6 +14,7 @@
 
 #include "uwvk_aug_dev.hpp"
 #include "../../include/uwvk.h"
+#include "uwvk_host.hpp"
 
 using namespace uwvk;
 using namespace uwvk::aug;
@@ -234,9 +235,13 @@ bool finite_all(const double* a, size_t n) {
 
 }  // namespace
 
-#define HIPCHK(x)                               \
-  do {                                          \
-    if ((x) != hipSuccess) return UWVK_EDEVICE; \
+#define HIPCHK(x)                                  \
+  do {                                             \
+    const hipError_t e_ = (x);                     \
+    if (e_ != hipSuccess) {                        \
+      ::uwvk::note_hip_error((int)e_, __func__);   \
+      return UWVK_EDEVICE;                         \
+    }                                              \
   } while (0)
 
 // ===========================================================================

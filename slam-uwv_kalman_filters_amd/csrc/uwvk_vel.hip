@@ -839,9 +839,13 @@ static VelBufs vbufs(const uwvk_vel* h) {
   return b;
 }
 
-#define HIPCHK(x)                              \
-  do {                                         \
-    if ((x) != hipSuccess) return UWVK_EDEVICE; \
+#define HIPCHK(x)                                  \
+  do {                                             \
+    const hipError_t e_ = (x);                     \
+    if (e_ != hipSuccess) {                        \
+      ::uwvk::note_hip_error((int)e_, __func__);   \
+      return UWVK_EDEVICE;                         \
+    }                                              \
   } while (0)
 
 static unsigned vgrid(int64_t B) { return (unsigned)((B + 63) / 64); }

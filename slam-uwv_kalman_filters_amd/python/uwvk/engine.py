@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("UWVK_LIB") or os.path.join(PKG, "libuwvk.so")
 
 # every symbol include/uwvk.h declares (checked by tests/test_abi.py)
 SYMBOLS = [
-    "uwvk_abi_version", "uwvk_device_available", "uwvk_status_string", "uwvk_device_malloc", "uwvk_device_free",
+    "uwvk_abi_version", "uwvk_device_available", "uwvk_status_string", "uwvk_last_device_error", "uwvk_device_malloc", "uwvk_device_free",
     "uwvk_memcpy_h2d", "uwvk_memcpy_d2h", "uwvk_memcpy_h2d_on", "uwvk_memcpy_d2h_on",
     "uwvk_pose_create", "uwvk_pose_destroy", "uwvk_pose_batch", "uwvk_pose_dof", "uwvk_pose_stream",
     "uwvk_pose_synchronize", "uwvk_pose_init_from_config", "uwvk_pose_init_from_state",
@@ -56,7 +56,14 @@ VP = C.c_void_p
 class UWVKError(RuntimeError):
     def __init__(self, code, where=""):
         self.code = code
-        super().__init__("%s%s" % (abi.STATUS.get(code, "UWVK_%d" % code), (" in " + where) if where else ""))
+        detail = ""
+        if code == 5 and _LIB is not None:  # UWVK_EDEVICE: the HIP error behind it
+            try:
+                detail = (_LIB.uwvk_last_device_error() or b"").decode()
+            except Exception:
+                detail = ""
+        super().__init__("%s%s%s" % (abi.STATUS.get(code, "UWVK_%d" % code), (" in " + where) if where else "",
+                                     (" [" + detail + "]") if detail else ""))
 
 
 def lib(path=None):
@@ -68,6 +75,7 @@ def lib(path=None):
             raise OSError("%s: ABI version %d, this binding needs %d (include/uwvk.h)"
                           % (path or LIB_PATH, L.uwvk_abi_version(), ABI_VERSION))
         L.uwvk_status_string.restype = C.c_char_p
+        L.uwvk_last_device_error.restype = C.c_char_p
         L.uwvk_pose_batch.restype = C.c_int64
         L.uwvk_pose_stream.restype = VP
         L.uwvk_vel_stream.restype = VP

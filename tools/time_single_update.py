@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Times single-call updates at batch 65,536: the literal BodyEfforts update
-(uwvk_pose_update_efforts), its velocity-only form (constrainVelocity) on PSP
-(r05) and on the literal kernel, and the acceleration update on the dense path:
+"""Times single-call updates at batch 65,536: the BodyEfforts update
+(uwvk_pose_update_efforts) on PSP (r05) and on the literal kernel, its
+velocity-only form (constrainVelocity) on PSP (r05) and on the literal kernel, and the acceleration update on the dense path:
 HIP events on the handle's stream around 5 calls each (each call includes its
 measurement upload).  UWVK_LIB selects a variant library."""
 import os
@@ -26,6 +26,7 @@ acc = np.tile([0.0, 0.0, 9.81], (B, 1)) + rng.normal(0, 1e-3, (B, 3))
 acov = np.eye(3) * 1e-4
 out = {}
 for name, call in (("efforts", lambda: f.update("efforts", eff, ecov, only_vel=0)),
+                   ("efforts_dense", lambda: f.update("efforts", eff, ecov, only_vel=0)),
                    ("efforts_vo_psp", lambda: f.update("efforts", eff, ecov, only_vel=1)),
                    ("efforts_vo_dense", lambda: f.update("efforts", eff, ecov, only_vel=1)),
                    ("acceleration_dense", lambda: f.update("acceleration", acc, acov))):
