@@ -664,12 +664,11 @@ __global__ __launch_bounds__(64) void k_psp_epoch_p(PoseBufs b, PoseShared sh0, 
 // of the epoch), VO 1 its velocity-only form (UWVK_EV_EFFORTS_VELOCITY_ONLY,
 // constrainVelocity), VO 0 the full model; the same bookkeeping as the literal
 // k_pose_efforts_epoch
+// (r05: capped at 3 waves per SIMD, 168 VGPRs and 12 B/lane of scratch, the
+// full update ran 1.420 against 1.415 ms per call: the 2-wave allocation stays,
+// profiles/r05/r05f/single_update*.txt)
 template <int DOF, int VO, int SR>
-__global__ __launch_bounds__(64)
-#ifdef EFFWPE
-__attribute__((amdgpu_waves_per_eu(EFFWPE, EFFWPE)))
-#endif
-void k_psp_efforts(PoseBufs b, PoseShared sh, EpochArgs ea) {
+__global__ __launch_bounds__(64) void k_psp_efforts(PoseBufs b, PoseShared sh, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const int64_t B = b.batch, inst = xcd_instance(B), e = ea.first;
   if (!(ea.flags[e] & UWVK_EV_EFFORTS)) return;

@@ -71,6 +71,21 @@ def test_psp_epoch_kernels_keep_three_waves_per_simd(src, side):
         assert r["vgpr"] + r.get("agpr", 0) <= 168 and r["scratch"] == 0 and r["occupancy"] >= 3, (name, r)
 
 
+# The BodyEfforts kernels (k_psp_efforts<DOF, VO, SR>, r05): no scratch, at
+# least 2 waves per SIMD (one instance per wave, so 8 instances per CU; the
+# literal two-wave kernel held 4).  Their register peak is the model
+# evaluation: so3_exp_psp's library fallback inside an evaluation, or the two
+# evaluations of a lane overlapped by the scheduler, took the full update to
+# 512 registers with spills (psp_update_eff's comments).
+@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
+@pytest.mark.parametrize("src,side", [("csrc/uwvk_psp_k.hip", 0), ("csrc/uwvk_psp_k_r.hip", 1)])
+def test_efforts_kernels_fit_two_waves_per_simd(src, side):
+    u = kernel_usage(src, ("_ZN4uwvk3psp13k_psp_effortsILi",))
+    assert len(u) == 4, sorted(u)  # DOF 53 / 26 x {full, velocity-only}
+    for name, r in u.items():
+        assert r["vgpr"] + r.get("agpr", 0) <= 256 and r["scratch"] == 0 and r["occupancy"] >= 2, (name, r)
+
+
 # The VelocityUKF kernels: no scratch round trip per epoch.  k_vel_epoch_g (C2)
 # had 272 B/lane until r04: vg_point's select chain over L[k][0..3] by the
 # lane's column was turned into one lane-indexed load from a private copy of L,
