@@ -8,17 +8,26 @@ persistent grid from <DOF, 1, 0, 0> on the assumption that all of them fit the
 same budget.  A harmless-looking change once took the kernel to 173 VGPRs,
 800 B/lane of scratch and 2 waves per SIMD (a noinline helper taking the
 EpochArgs reference); this test catches that class of regression before a GPU
-run.  Usage is collected per mangled name, so no instantiation hides another."""
+run.  Usage is collected per mangled name, so no instantiation hides another.
+
+Each translation unit is compiled once per flag set (assembly and the
+resource remarks from one hipcc run, the IR from another), all of them in
+parallel on first use, and shared by the tests below."""
+import concurrent.futures as cf
+import functools
 import os
 import re
 import shutil
 import subprocess
+import tempfile
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 HIPCC = "/opt/rocm/bin/hipcc"
+BASE = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only"]
+HAVE_HIPCC = bool(shutil.which(HIPCC) or os.path.exists(HIPCC))
 
 
 def psp_flags():
@@ -29,17 +38,55 @@ def psp_flags():
     raise AssertionError("PSP_FLAGS not found in the Makefile")
 
 
+def tu_flags(src):
+    """A translation unit's extra Makefile flags."""
+    return tuple(psp_flags()) if os.path.basename(src)[:-4] in ("uwvk_psp_k", "uwvk_psp_k_r") else ()
+
+
+@functools.lru_cache(maxsize=None)
+def compile_asm(src, flags):
+    """(gfx950 assembly, resource-usage remarks) of one translation unit."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "tu.s")
+        cmd = [HIPCC, *BASE, *flags, "-S", src, "-o", out, "-Rpass-analysis=kernel-resource-usage"]
+        r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return open(out).read(), r.stderr
+
+
+@functools.lru_cache(maxsize=None)
+def compile_ir(src, flags):
+    """The optimised LLVM IR of one translation unit."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "tu.ll")
+        cmd = [HIPCC, *BASE, *flags, "-S", "-emit-llvm", src, "-o", out]
+        r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return open(out).read()
+
+
+ALL_TUS = sorted(os.path.join("csrc", f) for f in os.listdir(os.path.join(PKG, "csrc")) if f.endswith(".hip"))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _prewarm():
+    """Every compile the module needs, in parallel, before its first test."""
+    if not HAVE_HIPCC:
+        return
+    jobs = [(compile_asm, src, tu_flags(src)) for src in ALL_TUS] + [(compile_ir, src, tu_flags(src)) for src in ALL_TUS]
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(8, os.cpu_count() or 1))) as ex:
+        for f in [ex.submit(fn, src, fl) for fn, src, fl in jobs]:
+            f.result()
+
+
 def kernel_usage(src, mangled_prefixes, extra=(), flags=None):
     """{mangled name: {vgpr, agpr, scratch, occupancy}} for every kernel whose
     mangled name starts with one of mangled_prefixes (flags: the unit's extra
-    Makefile flags, PSP_FLAGS by default)."""
-    cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-           *(psp_flags() if flags is None else flags), *extra, "-c", src, "-o", os.devnull,
-           "-Rpass-analysis=kernel-resource-usage"]
-    r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=900)
-    assert r.returncode == 0, r.stderr[-2000:]
+    Makefile flags by default; extra: more flags, for experiments)."""
+    fl = tuple(tu_flags(src) if flags is None else flags) + tuple(extra)
+    _, remarks = compile_asm(src, fl)
     out, cur = {}, None
-    for line in r.stderr.splitlines():
+    for line in remarks.splitlines():
         m = re.search(r"Function Name: (\S+)", line)
         if m:
             cur = m.group(1)
@@ -59,7 +106,7 @@ def kernel_usage(src, mangled_prefixes, extra=(), flags=None):
 PREFIXES = ("_ZN4uwvk3psp11k_psp_epochILi", "_ZN4uwvk3psp13k_psp_epoch_pILi")
 
 
-@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
+@pytest.mark.skipif(not HAVE_HIPCC, reason="no hipcc")
 @pytest.mark.parametrize("src,side", [("csrc/uwvk_psp_k.hip", 0), ("csrc/uwvk_psp_k_r.hip", 1)])
 def test_psp_epoch_kernels_keep_three_waves_per_simd(src, side):
     u = kernel_usage(src, PREFIXES)
@@ -77,7 +124,7 @@ def test_psp_epoch_kernels_keep_three_waves_per_simd(src, side):
 # evaluation: so3_exp_psp's library fallback inside an evaluation, or the two
 # evaluations of a lane overlapped by the scheduler, took the full update to
 # 512 registers with spills (psp_update_eff's comments).
-@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
+@pytest.mark.skipif(not HAVE_HIPCC, reason="no hipcc")
 @pytest.mark.parametrize("src,side", [("csrc/uwvk_psp_k.hip", 0), ("csrc/uwvk_psp_k_r.hip", 1)])
 def test_efforts_kernels_fit_two_waves_per_simd(src, side):
     u = kernel_usage(src, ("_ZN4uwvk3psp13k_psp_effortsILi",))
@@ -94,18 +141,14 @@ def test_efforts_kernels_fit_two_waves_per_simd(src, side):
 # profiles/r04/vpt/).  Since the r04 no-hoist change (+3%, profiles/r04/nh/) the kernel
 # keeps 168 B/lane of loop-invariant values written once before the epoch
 # loop and only read inside it; a scratch store inside the loop fails here.
-@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
-def test_velocity_kernels_have_no_scratch_round_trip(tmp_path):
+@pytest.mark.skipif(not HAVE_HIPCC, reason="no hipcc")
+def test_velocity_kernels_have_no_scratch_round_trip():
     u = kernel_usage("csrc/uwvk_vel.hip", ("_ZN12_GLOBAL__N_1", "_ZN4uwvk"), flags=[])
     names = [n for n in u if "k_vel_" in n]
     assert any("k_vel_epoch_g" in n for n in names) and len(names) >= 6, sorted(u)
     for n in names:
         assert "k_vel_epoch_g" in n or u[n]["scratch"] == 0, (n, u[n])
-    out = str(tmp_path / "vel.s")
-    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-                        "-S", "csrc/uwvk_vel.hip", "-o", out], cwd=PKG, capture_output=True, text=True, timeout=900)
-    assert r.returncode == 0, r.stderr[-2000:]
-    lines = open(out).read().split("\n")
+    lines = compile_asm("csrc/uwvk_vel.hip", ())[0].split("\n")
     # the shipped k_vel_epoch_g<16>; the <32> diagnostic (UWVK_VEL_OPT_LANE_GROUPS 2)
     # is capped at 256 registers for 2 waves per SIMD and spills inside the loop
     starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\w*k_vel_epoch_gILi16E\w*:", l)]
@@ -151,22 +194,14 @@ def test_sext32_literal_scan_catches_the_hazard():
     assert not sext32_literals("  s_mov_b64 s[4:5], -2\n  s_mov_b64 vcc, 0x3fffffff\n  s_movk_i32 s2, 0xffe0\n")
 
 
-ALL_TUS = sorted(os.path.join("csrc", f) for f in os.listdir(os.path.join(PKG, "csrc")) if f.endswith(".hip"))
 
 
-@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
+@pytest.mark.skipif(not HAVE_HIPCC, reason="no hipcc")
 @pytest.mark.parametrize("src", ALL_TUS)
-def test_isa_has_no_zero_extended_64bit_literal(src, tmp_path):
+def test_isa_has_no_zero_extended_64bit_literal(src):
     """The hazard comes from the compiler, not from the PSP code: every
     translation unit of libuwvk.so, each with its Makefile flags."""
-    name = os.path.basename(src)[:-4]
-    flags = psp_flags() if name in ("uwvk_psp_k", "uwvk_psp_k_r") else []
-    out = str(tmp_path / (name + ".s"))
-    cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-           *flags, "-S", src, "-o", out]
-    r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=900)
-    assert r.returncode == 0, r.stderr[-2000:]
-    bad = sext32_literals(open(out).read())
+    bad = sext32_literals(compile_asm(src, tu_flags(src))[0])
     assert not bad, bad[:10]
 
 
@@ -198,15 +233,8 @@ def test_ir_cast_scan_catches_the_r04o_pattern():
     assert not ir_cast_findings("  %717 = addrspacecast ptr %24 to ptr addrspace(4)\n")
 
 
-@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="no hipcc")
+@pytest.mark.skipif(not HAVE_HIPCC, reason="no hipcc")
 @pytest.mark.parametrize("src", ALL_TUS)
-def test_no_private_to_constant_address_space_cast(src, tmp_path):
-    name = os.path.basename(src)[:-4]
-    flags = psp_flags() if name in ("uwvk_psp_k", "uwvk_psp_k_r") else []
-    out = str(tmp_path / (name + ".ll"))
-    cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
-           *flags, "-S", "-emit-llvm", src, "-o", out]
-    r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=900)
-    assert r.returncode == 0, r.stderr[-2000:]
-    bad = ir_cast_findings(open(out).read())
+def test_no_private_to_constant_address_space_cast(src):
+    bad = ir_cast_findings(compile_ir(src, tu_flags(src)))
     assert not bad, bad[:10]
