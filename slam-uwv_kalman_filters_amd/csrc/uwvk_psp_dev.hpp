@@ -49,6 +49,16 @@
 namespace uwvk {
 namespace psp {
 
+// (r05) a partial Cholesky is one serial chain (pivot readlane -> rsqrt ->
+// scale -> column broadcast -> update, per column): the wave in it runs at
+// raised issue priority (s_setprio 1) so that its next step issues ahead of the
+// SIMD's other waves; interleaved A/B, six rounds: 200 epochs 62.21-62.43 ->
+// 61.86-62.04 ms, 20 epochs 6.56-6.63 -> 6.53-6.60 ms (profiles/r05/ab_prio/).
+// Raising it over the manifold mean, the gain or apply_delta as well did not
+// help (same runs).
+UWVK_DEV void chain_prio_hi() { __builtin_amdgcn_s_setprio(1); }
+UWVK_DEV void chain_prio_lo() { __builtin_amdgcn_s_setprio(0); }
+
 template <int DOF>
 struct PG {
   static constexpr int NP = DOF * (DOF + 1) / 2;     // packed entries
@@ -625,7 +635,9 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   const double wv_add = sh.p.water_velocity_scale * (vs0 * vs0 + vs1 * vs1 + vs2 * vs2) * dt;
   // partial Cholesky and row staging
   double a[K];
+  chain_prio_hi();
   const bool ok = pchol<DOF, K, PredRows>(sm.S, l, a, ds, sm.stg);
+  chain_prio_lo();
   PSP_PHASE(20);
   // sigma points: lanes < 2K plus the centre lane 2K; orientation output only
   const bool pt = LANE_IF(l, l < 2 * K), ctr = LANE_IF(l, l == 2 * K);
@@ -1324,7 +1336,9 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double a[KA];
   bool cok = true;
   if constexpr (K > 0) {
+    chain_prio_hi();
     cok = pchol<DOF, K, HM>(sm.S, l, a, ds, sm.stg);
+    chain_prio_lo();
   }
   PSP_PHASE(30);
   [[maybe_unused]] const bool pt = LANE_IF(l, l < 2 * K);  // the non-lds_sums path (PSP_FAST & 256 off)
