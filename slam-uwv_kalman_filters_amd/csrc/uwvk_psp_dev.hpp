@@ -54,8 +54,11 @@ namespace psp {
 // raised issue priority (s_setprio 1) so that its next step issues ahead of the
 // SIMD's other waves; interleaved A/B, six rounds: 200 epochs 62.21-62.43 ->
 // 61.86-62.04 ms, 20 epochs 6.56-6.63 -> 6.53-6.60 ms (profiles/r05/ab_prio/).
-// Raising it over the manifold mean, the gain or apply_delta as well did not
-// help (same runs).
+// The predict's X = 1/2 A L_a Delta loop (one LDS broadcast and FMA per j)
+// likewise: 200 epochs 61.52-61.90 -> 61.27-61.66 ms, ten rounds, 20 epochs
+// within noise (profiles/r05/ab_prio/round3-4.txt).  Raising it over the
+// manifold mean, the update's points, the gain, apply_delta or the BodyEfforts
+// factor did not help (same runs).
 UWVK_DEV void chain_prio_hi() { __builtin_amdgcn_s_setprio(1); }
 UWVK_DEV void chain_prio_lo() { __builtin_amdgcn_s_setprio(0); }
 
@@ -703,6 +706,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   for (int i = 0; i < 3; i++) dd[i] = d[i] - swap_pair_d(d[i]);
   // ori x lin: X_r = 1/2 (A (L_a Delta))_r, lane r
   double X[3];
+  chain_prio_hi();  // the broadcast loop over Delta_j is a chain too (r05 A/B below)
   {
     double Y[3] = {0.0, 0.0, 0.0};
     // Delta_j staged in stg (free after the ori x ori sums) by lane 2j and read
@@ -734,6 +738,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       asm volatile("" : "+v"(Y[0]), "+v"(Y[1]), "+v"(Y[2])::"memory");
     }
     wsync();  // stg is rewritten by the next phase's users
+    chain_prio_lo();
     const int cp = proc_couple(l);
     const int src = cp >= 0 ? cp : l;
     const double ar = 1.0 + dt * pc.nt_tan;  // proc_diag_sel's value (nt_tan = 0 off the scaled DOFs)
