@@ -706,7 +706,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   for (int i = 0; i < 3; i++) dd[i] = d[i] - swap_pair_d(d[i]);
   // ori x lin: X_r = 1/2 (A (L_a Delta))_r, lane r
   double X[3];
-  chain_prio_hi();  // the broadcast loop over Delta_j is a chain too (r05 A/B below)
+  chain_prio_hi();  // the broadcast loop over Delta_j is a chain too (see chain_prio_hi)
   {
     double Y[3] = {0.0, 0.0, 0.0};
     // Delta_j staged in stg (free after the ori x ori sums) by lane 2j and read
