@@ -8,6 +8,8 @@
 # occupancy sweep (tools/gpu_r05c.sh) that prices the paired kernel's 1.5
 # waves per SIMD.  Every step has its own time limit; the first failure ends
 # the script.  Usage (repo root, on the box): bash tools/gpu_r05d.sh TAG
+# (The pair kernel, --pair and tests/test_gpu_pair.py were removed after this
+# session's measurement; commit 582df31 is the tree it ran on.)
 set -u
 TAG=$1
 OUT=$PWD/gpurun_out/$TAG
