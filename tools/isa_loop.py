@@ -10,15 +10,17 @@ import os
 import subprocess
 import sys
 
+# UWVK_SR=0: the left-side instantiation (uwvk_psp_k.hip); default the right side
+SR = os.environ.get("UWVK_SR", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 out = "/tmp/psp_loop.s"
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
                 "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form",
                 *sys.argv[1:], "-I", os.path.join(PKG, "csrc"), "-I", os.path.join(ROOT, "include"),
-                "-S", "-o", out, os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
+                "-S", "-o", out, os.path.join(PKG, "csrc", "uwvk_psp_k_r.hip" if SR == "1" else "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
 s = open(out).read().split("\n")
-name="_ZN4uwvk3psp11k_psp_epochILi53ELi1ELi1ELi0EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE"
+name="_ZN4uwvk3psp11k_psp_epochILi53ELi1ELi1ELi%sEEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % SR
 st=[i for i,l in enumerate(s) if l.startswith(name+":")][0]
 en=[i for i,l in enumerate(s) if i>st and l.startswith(".Lfunc_end")][0]
 L=[l.strip() for l in s[st:en] if l.strip() and not l.strip().startswith(';')]

@@ -11,6 +11,8 @@ import re
 import subprocess
 import sys
 
+# UWVK_SR=0: the left-side instantiation (uwvk_psp_k.hip); default the right side
+SR = os.environ.get("UWVK_SR", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 dof = sys.argv[1] if len(sys.argv) > 1 else "53"
@@ -18,9 +20,9 @@ extra = sys.argv[2:]
 out = "/tmp/psp_phases.s"
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
                 "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-mfma-vgpr-form", "-DUWVK_STAMPS", *extra, "-S", "-o", out,
-                os.path.join(PKG, "csrc", "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
+                os.path.join(PKG, "csrc", "uwvk_psp_k_r.hip" if SR == "1" else "uwvk_psp_k.hip")], check=True, stderr=subprocess.DEVNULL)
 s = open(out).read().split("\n")
-name = "_ZN4uwvk3psp11k_psp_epochILi%sELi1ELi1ELi0EEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % dof
+name = "_ZN4uwvk3psp11k_psp_epochILi%sELi1ELi1ELi%sEEEvNS_8PoseBufsENS_10PoseSharedENS_9EpochArgsE" % (dof, SR)
 st = [i for i, l in enumerate(s) if l.startswith(name + ":")][0]
 en = [i for i, l in enumerate(s) if i > st and l.startswith(".Lfunc_end")][0]
 INT = re.compile(r"v_(add|sub|subrev|mul_lo|mul_hi|mad|lshl|lshr|ashr|and|or|xor|bfe|bfi|max|min|cvt|mul_u32|"
