@@ -320,8 +320,15 @@ def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_in
         # counter-based: one stream per (instance, measurement kind), record-major
         return normals_rec(seed, first_instance, batch, stream, first_record * group, records, group)
 
-    sg = 1e-4 / np.sqrt(dt)
-    sa = 1e-3 / np.sqrt(dt)
+    # gyro: the rate noise the filter's process model assumes for the config's
+    # rotation_rate.randomwalk (1e-4): the orientation block of Q is
+    # randomwalk^2 (PoseUKF.cpp:408) scaled by dt^2 per step (:462), i.e. a
+    # per-sample rate noise of sd randomwalk.  (Before r05 this drew sd
+    # randomwalk / sqrt(dt), 1/dt times the variance, and the ensemble NEES of
+    # long windows grew with the window: 9 -> 102 over 40 s, roll / pitch
+    # overconfident; tools/nees_components.py)
+    sg = cfg.rotation_rate.randomwalk[0]
+    sa = 1e-3 / np.sqrt(dt)  # a measurement: acc_cov = sa^2 below
     gyro = rec(0, epoch0, epochs, 3)  # [epochs][batch][3]
     gyro *= sg
     gyro += tr.gyro[k][:, None, :]
