@@ -1135,10 +1135,25 @@ UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop
       base[i] = q * x + (x * (x + 1) / 2) + tq;
     }
     d4_t acc[I + 1];
+    // (r05) the tile loads are volatile LDS reads through one pointer per row
+    // (tile J at the immediate offset 128 J): one ds_read_b64 per element
+    // straight into its MFMA tuple.  Plain loads were paired across tiles J
+    // and J + 1 (16 apart) into ds_read2_b64 and split again by v_mov_b32 (48
+    // per rank-3 update), and the stores rematerialised their addresses (2
+    // VALU each): -43 VALU per update, C3 +1% (profiles/r05/r05k/)
+    using LdsV = const volatile __attribute__((address_space(3))) double*;
+    LdsV rp[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      rp[i] = (LdsV)(S + base[i]);
+      // opaque, so that the masked diagonal stores reuse the register rather
+      // than rematerialise the address
+      asm volatile("" : "+v"(rp[i]));
+    }
 #pragma unroll
     for (int J = 0; J <= I; J++)
 #pragma unroll
-      for (int i = 0; i < 4; i++) acc[J][i] = S[base[i] + 16 * J];
+      for (int i = 0; i < 4; i++) acc[J][i] = rp[i][16 * J];
 #pragma unroll
     for (int J = 0; J <= I; J++) acc[J] = mfma_f64(Aop[I], Bop[J], acc[J]);
     // one empty asm over every accumulator: all MFMAs issue before the first
@@ -1153,11 +1168,12 @@ UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop
         lane_mask([](int l) constexpr { return (l & 15) <= ((l >> 4) & 3) + 4; }),
         lane_mask([](int l) constexpr { return (l & 15) <= ((l >> 4) & 3) + 8; }),
         lane_mask([](int l) constexpr { return (l & 15) <= ((l >> 4) & 3) + 12; })};
+    using LdsW = __attribute__((address_space(3))) double*;
 #pragma unroll
     for (int J = 0; J <= I; J++)
 #pragma unroll
       for (int i = 0; i < 4; i++)
-        if (J < I || LANE_IN(diagm[i])) S[base[i] + 16 * J] = acc[J][i];
+        if (J < I || LANE_IN(diagm[i])) ((LdsW)rp[i])[16 * J] = acc[J][i];
     rankm_block<DOF, I + 1, NT>(S, Aop, Bop, q, c, tq);
   }
 }
