@@ -183,6 +183,12 @@ UWVK_DEV constexpr unsigned long long rows_mask() {
   for (int k = 0; k < RL::NR; k++) m |= 1ull << RL::rows[k];
   return m;
 }
+template <class RL>
+UWVK_DEV constexpr bool rows_ascending() {
+  for (int k = 1; k < RL::NR; k++)
+    if (RL::rows[k] <= RL::rows[k - 1]) return false;
+  return true;
+}
 
 // ---------------------------------------------------------------------------
 // DPP wave reductions (no LDS crossbar): row_shr 1/2/3 -> 4-lane sums,
@@ -438,9 +444,12 @@ UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* s
 #pragma unroll
   for (int c = 0; c < K; c++) a[c] = Sr[c] * (scaled_dof(c) ? dl * readlane_d(dl, c) : dl);
   bool ok = true;
-  int q = -1;
-#pragma unroll
-  for (int k = 0; k < RL::NR; k++) q = LANE_IN(1ull << RL::rows[k]) ? k : q;
+  // the staged-row slot of lane r is its rank among the staged rows (the row
+  // list is ascending): the set bits of the constant row mask below the lane,
+  // two v_mbcnt instead of a select per staged row
+  static_assert(rows_ascending<RL>(), "RL::rows ascending");
+  constexpr unsigned long long rm = rows_mask<RL>();
+  const int q = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(rm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)rm, 0u));
   static_assert(RL::NR >= 1 && STG_ROWS + RL::NR * K <= 115, "staging area (PG::STG)");
   const double p0 = readlane_d(a[0], 0);
   const double inv0 = rsqrt_f64(p0);
@@ -1377,25 +1386,29 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   // H and P first: P reads the staged rows, after which stg holds the
   // transposed sums.  One round of M + M(M+1)/2 sums over the 2K point lanes:
   // u = z_p - z_0, s = sum u, m = s / N; sum dz dz^T = sum u u^T - m s^T - s m^T + 2K m m^T
+  // H as every lane computes it (the same values in VGPRs; r05: read back as
+  // uniform SGPR pairs they were spilled to VGPR lanes and reloaded, 10
+  // v_readlane per update, profiles/r05/r05m/); its structural zeros and ones
+  // stay compile-time constants for hfma
   double Hs[M][NCA];
-  {
-    double H[M][NCA];
-    hm.jac(sm.mu, H);
-#pragma unroll
-    for (int i = 0; i < M; i++)
-#pragma unroll
-      for (int t = 0; t < NC; t++) Hs[i][t] = readlane_d(H[i][t], 0);
-  }
+  hm.jac(sm.mu, Hs);
   double Pl = 0.0;
   if constexpr (K > 0) {
     const int q = LANE_IF(l, l < M * K) ? l : 0;
     const int i = q / K, j = q - (q / K) * K;
+    // (r05) every row's sum with H's uniform entries as operands (structural
+    // zeros dropped by hfma), then one select of the lane's row: selecting
+    // H[i][t] per column first cost 2 (M - 1) v_cndmask and the SGPR-to-VGPR
+    // moves for every t (the same products in the same order)
+    double lv[NCA];
 #pragma unroll
-    for (int t = 0; t < NC; t++) {
-      double h = Hs[0][t];
+    for (int t = 0; t < NC; t++) lv[t] = sm.stg[STG_ROWS + row_pos(HM::rows, HM::cols[t]) * K + j];
 #pragma unroll
-      for (int ii = 1; ii < M; ii++) h = (i == ii) ? Hs[ii][t] : h;
-      Pl += h * sm.stg[STG_ROWS + row_pos(HM::rows, HM::cols[t]) * K + j];
+    for (int ii = 0; ii < M; ii++) {
+      double pr = 0.0;
+#pragma unroll
+      for (int t = 0; t < NC; t++) pr = hfma(Hs[ii][t], lv[t], pr);
+      Pl = (ii == 0 || i == ii) ? pr : Pl;
     }
     constexpr int R = M + M * (M + 1) / 2;
     double v[R], sums[R];
