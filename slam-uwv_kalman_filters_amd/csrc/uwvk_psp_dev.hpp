@@ -1456,7 +1456,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   for (int i = 0; i < M; i++) Gr[i] = 0.0;
 #pragma unroll
   for (int t = 0; t < NC; t++) {
-    double s = sm.S[pidx_sel(HM::cols[t], rl, Trl)];
+    double s = sm.S[pidx_sel_b(HM::cols[t], rl, Trl, LANE_IN(col_ge_mask<DOF>(HM::cols[t], false)))];
     if (scaled_dof(HM::cols[t])) s = s * readlane_d(ds, HM::cols[t]);
 #pragma unroll
     for (int i = 0; i < M; i++) Gr[i] = hfma(Hs[i][t], s, Gr[i]);
