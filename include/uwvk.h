@@ -40,8 +40,18 @@ extern "C" {
  *   2  uwvk_pose_ensemble_stats / _allreduce write 3*store+2 doubles (was
  *      3*store+1: the count of instances left out of the NEES sum was added);
  *      uwvk_pose_init_from_state reads only the lower triangle of P;
- *      uwvk_memcpy_h2d / _d2h wait for the buffer's own device only. */
-#define UWVK_ABI_VERSION 2
+ *      uwvk_memcpy_h2d / _d2h wait for the buffer's own device only.
+ *   3  (r05/r06) the default UWVK_OPT_SO3_RIGHT of pose and ipose handles is 1
+ *      (body-frame SO3 [+], MTK's SO3::boxplus; was 0, nav frame): a caller
+ *      that wants the old convention sets the option to 0;
+ *      new entry points uwvk_last_device_error, uwvk_synth_normal_at,
+ *      uwvk_ipose_set_option;
+ *      a tail-chunk hand-off that timed out is an error of the API, not only
+ *      the instances' UWVK_ST_SCHEDULE bit: the next uwvk_pose_synchronize
+ *      or uwvk_pose_run_log on the handle after the launch has completed
+ *      returns UWVK_ESCHEDULE (once); new option UWVK_OPT_WAIT_BOUND;
+ *      UWVK_OPT_PERSIST defaults to 1 (no dispatch-order assumption). */
+#define UWVK_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum uwvk_status {
@@ -52,7 +62,9 @@ typedef enum uwvk_status {
   UWVK_ENOMODEL = 4, /* VelocityUKF predict without setupMotionModel (VelocityUKF.cpp:117-118) */
   UWVK_EDEVICE = 5,  /* no gfx950 device / HIP runtime error */
   UWVK_ENOMEM = 6,
-  UWVK_ENOTINIT = 7  /* state or process noise not initialised */
+  UWVK_ENOTINIT = 7, /* state or process noise not initialised */
+  UWVK_ESCHEDULE = 8 /* a run_log tail-chunk hand-off timed out (instances flagged UWVK_ST_SCHEDULE);
+                        returned by the next uwvk_pose_synchronize / uwvk_pose_run_log */
 } uwvk_status;
 
 /* per-instance status bits (uwvk_pose_get_status / uwvk_vel_get_status) */
@@ -440,24 +452,33 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   kernels are instantiated per side, SR); the oracle's or_set_so3_right is
  *   the same switch. */
 #define UWVK_OPT_SO3_RIGHT 5
-/* UWVK_OPT_PERSIST: scheduling of the PSP run_log launch.  0 (default): one
- *   workgroup per instance (plus UWVK_OPT_TAIL_SLOTS spreading, which needs the
- *   round-robin XCD placement of uwvk_xcd_round_robin; without it the launch
- *   falls back to the persistent form).  1: persistent workgroups, as many as
- *   are resident, run their own unit first and then take work units (whole
- *   instances, then the epoch chunks of the last chunks x resident-slots
- *   instances) from a ticket counter: faster XCDs and CUs take more units, no
- *   workgroup dispatch between units, and a chunk's hand-off waits only on a
- *   unit a running workgroup holds (no placement assumption).  Results are
- *   bitwise those of 0.  (MI355X, C3 batch 65,536: 0.2-0.5% faster over 200
- *   epochs, 0.5-0.9% slower over 20) */
+/* UWVK_OPT_PERSIST: scheduling of the PSP run_log launch.  1 (default since
+ *   r06): persistent workgroups, as many as are resident, run their own unit
+ *   first and then take work units (whole instances, then the epoch chunks of
+ *   the last chunks x resident-slots instances) from a ticket counter: faster
+ *   XCDs and CUs take more units, no workgroup dispatch between units, and a
+ *   chunk's hand-off waits only on a unit a running workgroup holds (no
+ *   placement or dispatch-order assumption).  0: one workgroup per instance
+ *   (plus UWVK_OPT_TAIL_SLOTS spreading, which relies on the round-robin XCD
+ *   placement of uwvk_xcd_round_robin and in-order dispatch; without the
+ *   placement the launch falls back to the persistent form).  Results are
+ *   bitwise the same.  (MI355X, C3 batch 65,536, four interleaved rounds: tie,
+ *   200.6 against 200.9 M steps/s over 20 epochs, 219.2 against 219.1 M over
+ *   200) */
 #define UWVK_OPT_PERSIST 6
 /* UWVK_OPT_LDS_PAD (diagnostic, r05): bytes of dynamic LDS requested per PSP
  *   epoch workgroup on top of its static 12.8 KB, unused by the kernel: it only
  *   lowers the resident workgroups per CU (12 -> 9 / 6 / 4 ...), to measure the
- *   epoch kernel's rate against occupancy.  0 default;
- *   use with UWVK_OPT_TAIL_SLOTS < 0 (the tail planner assumes no pad). */
+ *   epoch kernel's rate against occupancy.  0 default,
+ *   at most 160 KiB minus the static 12.8 KB (else UWVK_EINVAL); a non-zero pad
+ *   turns tail spreading off (the planners assume the unpadded occupancy). */
 #define UWVK_OPT_LDS_PAD 7
+/* UWVK_OPT_WAIT_BOUND (tests, r06): sleeps of ~1.7 us a tail chunk waits for
+ *   its predecessor's hand-off before it gives up (UWVK_ST_SCHEDULE, and
+ *   the next synchronize / run_log returns UWVK_ESCHEDULE).  < 0 (default): the planner's
+ *   bound (~2 s plus 64-128 sleeps per epoch); 0 forces every hand-off of a
+ *   spread launch to time out. */
+#define UWVK_OPT_WAIT_BOUND 8
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
 /* Host-only query (no device work): the chunks per tail instance the
  * UWVK_OPT_TAIL_SLOTS planner picks for one XCD's instances over its resident

@@ -21,9 +21,14 @@ namespace uwvk {
 // device current for the duration of the call (allocations, launches, copies)
 // and restores the caller's device on return, so one thread may drive handles
 // on several GPUs.  device < 0 (a null handle): no-op.
+// clears the calling thread's uwvk_last_device_error text (uwvk_rt.hip): every
+// public entry point starts with a DeviceGuard, so the text always belongs to
+// the current call's UWVK_EDEVICE, never an earlier, unrelated failure
+void clear_hip_error();
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int device) {
+    clear_hip_error();
     int cur = -1;
     if (device < 0 || hipGetDevice(&cur) != hipSuccess || cur == device) return;
     if (hipSetDevice(device) == hipSuccess) prev = cur;

@@ -65,9 +65,14 @@ struct uwvk_pose {
   uint32_t tail_tag = 0;
   // persistent epoch kernel (UWVK_OPT_PERSIST): ticket counter and the value
   // it holds when the next launch starts (every launch takes units + grid)
-  int persist = 0;
+  int persist = 1;  // UWVK_OPT_PERSIST (default since r06)
   uint32_t lds_pad = 0;  // UWVK_OPT_LDS_PAD (diagnostic occupancy sweep)
+  int wait_bound = -1;   // UWVK_OPT_WAIT_BOUND: < 0 the planner's bound, else that many sleeps (tests)
   uint32_t* d_ticket = nullptr;
+  // hand-off fault word: pinned, coherent host memory the epoch kernel writes
+  // directly (no copy on the stream); read after the stream has drained
+  uint32_t* h_fault = nullptr;
+  uint32_t* d_fault = nullptr;  // its device address
   uint32_t ticket_next = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   aug::VisStage vis;  // visual-landmark update staging
@@ -242,6 +247,8 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
             hipMalloc(&h->d_shared, sizeof(PoseShared)) == hipSuccess &&
             hipMalloc(&h->d_Qp, n * (n + 1) * 8) == hipSuccess && hipMalloc(&h->d_qband, 128 * 8) == hipSuccess &&
             hipMalloc(&h->d_ticket, 4) == hipSuccess &&
+            hipHostMalloc((void**)&h->h_fault, 4, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+            hipHostGetDevicePointer((void**)&h->d_fault, h->h_fault, 0) == hipSuccess &&
             hipEventCreate(&h->ev0) == hipSuccess && hipEventCreate(&h->ev1) == hipSuccess;
   if (!ok) {
     uwvk_pose_destroy(h);
@@ -251,6 +258,7 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
   (void)hipMemsetAsync(h->d_rot, 0, B * 3 * 8, h->stream);
   (void)hipMemsetAsync(h->d_Q, 0, n * n * 8, h->stream);
   (void)hipMemsetAsync(h->d_ticket, 0, 4, h->stream);
+  *h->h_fault = 0;
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     uwvk_pose_destroy(h);
     return UWVK_EDEVICE;
@@ -268,6 +276,7 @@ void uwvk_pose_destroy(uwvk_pose* h) {
                   (void*)h->d_accepted, (void*)h->d_scratch, (void*)h->d_shared, (void*)h->d_Qp, (void*)h->d_qband,
                   (void*)h->d_tail_flag, (void*)h->d_tail_carry, (void*)h->d_ticket})
     if (p) (void)hipFree(p);
+  if (h->h_fault) (void)hipHostFree(h->h_fault);
   h->vis.release();
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -278,10 +287,19 @@ void uwvk_pose_destroy(uwvk_pose* h) {
 int64_t uwvk_pose_batch(const uwvk_pose* h) { return h ? h->batch : 0; }
 int uwvk_pose_dof(const uwvk_pose* h) { return h ? h->dof : 0; }
 void* uwvk_pose_stream(const uwvk_pose* h) { return h ? (void*)h->stream : nullptr; }
+// a tail-chunk hand-off that timed out in a launch that has completed (the
+// kernel wrote the handle's host-mapped fault word); reported once
+static bool take_fault(uwvk_pose* h) {
+  if (!__atomic_load_n(h->h_fault, __ATOMIC_ACQUIRE)) return false;
+  __atomic_store_n(h->h_fault, 0u, __ATOMIC_RELEASE);
+  return true;
+}
+
 uwvk_status uwvk_pose_synchronize(uwvk_pose* h) {
   UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
-  return hipStreamSynchronize(h->stream) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return UWVK_EDEVICE;
+  return take_fault(h) ? UWVK_ESCHEDULE : UWVK_OK;
 }
 
 // Both init calls replace the reference's constructors (PoseUKF.cpp:288-391):
@@ -646,7 +664,7 @@ static hipError_t prepare_persist(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
   ea.chunks = 1;
   ea.tail0 = B;
   ea.r_x = 0;
-  int c = h->tail_slots < 0 || s <= 0 ? 1 : tail_plan(h, B, s, ea.count);
+  int c = h->tail_slots < 0 || h->lds_pad > 0 || s <= 0 ? 1 : tail_plan(h, B, s, ea.count);
   if (c > 1) {
     const int64_t r = c * s;
     hipError_t e = tail_buffers(h, r, 8 * s);
@@ -660,6 +678,7 @@ static hipError_t prepare_persist(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
     // a chunk waits at most for its predecessor's unit and the unit its block
     // held before it: ~2 of the launch's epochs per wave, see prepare_tail
     ea.wait_bound = (uint32_t)std::min<uint64_t>(0xffffffffull, (1ull << 20) + 128ull * (uint64_t)ea.count);
+    if (h->wait_bound >= 0) ea.wait_bound = (uint32_t)h->wait_bound;
   }
   const int64_t units = ea.tail0 + (int64_t)ea.chunks * ea.r_x;
   grid = std::min<int64_t>(units, slots);
@@ -680,7 +699,9 @@ static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
   ea.ticket = nullptr;
   grid = 0;
   if (h->persist) return prepare_persist(h, ea, grid);
-  if (h->tail_slots < 0 || h->batch % 8 != 0) return hipSuccess;
+  // an LDS pad lowers the resident blocks below what the tail plan assumes:
+  // no spreading then (UWVK_OPT_LDS_PAD is a diagnostic of the unspread launch)
+  if (h->tail_slots < 0 || h->lds_pad > 0 || h->batch % 8 != 0) return hipSuccess;
   // placement not the round-robin the XCD-ordered tail plan needs (a
   // partitioned device, another runtime): the ticket-ordered persistent
   // launch spreads the tail without any placement assumption
@@ -703,6 +724,7 @@ static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
   // epochs; one sleep is ~1.7 us and an epoch ~20 us per wave at full
   // occupancy: 64 sleeps per epoch is a wide margin, plus ~2 s of slack
   ea.wait_bound = (uint32_t)std::min<uint64_t>(0xffffffffull, (1ull << 20) + 64ull * (uint64_t)ea.count);
+  if (h->wait_bound >= 0) ea.wait_bound = (uint32_t)h->wait_bound;
   grid = 8 * (n + (c - 1) * r);
   return hipSuccess;
 }
@@ -712,6 +734,9 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   UWVK_DEVICE_GUARD(h);
   if (!h || !log || first < 0 || count < 0 || first + count > log->epochs || log->adcp_cells > 8) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
+  // ABI 3: a hand-off timeout of an earlier, completed launch is reported here
+  // (or by uwvk_pose_synchronize), before any new work is queued
+  if (take_fault(h)) return UWVK_ESCHEDULE;
   EpochArgs ea{};
   ea.flags = log->flags; ea.gyro = log->gyro; ea.acc = log->acc;
   std::memcpy(ea.acc_cov, log->acc_cov, sizeof(ea.acc_cov));
@@ -752,6 +777,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   std::memcpy(h->sh.log_dvl_cov, log->dvl_cov, sizeof(h->sh.log_dvl_cov));
   HIPCHK(upload_shared(h, log->dt));
   const PoseShared sh = h->sh;  // after upload_shared (it refreshes the Q shape)
+  ea.fault = h->d_fault;
   int64_t e = first;
   while (e < first + count) {
     int64_t r = e;
@@ -764,7 +790,9 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     uint32_t ev_any = 0;  // the event kinds of this launch's epochs (kernel choice)
     for (int64_t k = e; k < last; k++) ev_any |= hf[k - first];
     HIPCHK(prepare_tail(h, ea, grid));
-    if (launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid, ev_any, h->lds_pad) != hipSuccess) {
+    const hipError_t le = launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid, ev_any, h->lds_pad);
+    if (le != hipSuccess) {
+      ::uwvk::note_hip_error((int)le, "launch_psp_epoch");
       // a persistent launch that did not run took no tickets: restart the
       // counter from zero (stream-ordered, before any later launch)
       if (ea.ticket) {
@@ -843,8 +871,13 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
     return UWVK_OK;
   }
   if (option == UWVK_OPT_LDS_PAD) {  // diagnostic: occupancy sweep of the epoch kernel
-    if (value < 0 || value > 150 * 1024) return UWVK_EINVAL;
+    // the pad plus the kernel's static PspSmem<53> must fit gfx950's 160 KiB
+    if (value < 0 || value > 160 * 1024 - (int)psp_epoch_lds_bytes(53)) return UWVK_EINVAL;
     h->lds_pad = (uint32_t)value;
+    return UWVK_OK;
+  }
+  if (option == UWVK_OPT_WAIT_BOUND) {  // tests: force hand-off timeouts (0 = every one)
+    h->wait_bound = value;
     return UWVK_OK;
   }
   return UWVK_EINVAL;

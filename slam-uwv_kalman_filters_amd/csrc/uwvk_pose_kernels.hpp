@@ -67,6 +67,9 @@ struct EpochArgs {
   // instance tail0 + t at unit tail0 + k r_x + t (r_x tail instances)
   uint32_t* ticket;
   uint32_t ticket_base;
+  // the handle's hand-off fault word (pinned host memory): set to 1 by any
+  // chunk whose predecessor's hand-off timed out (UWVK_ESCHEDULE)
+  uint32_t* fault;
   uint32_t units;       // tail0 + chunks * r_x
 };
 

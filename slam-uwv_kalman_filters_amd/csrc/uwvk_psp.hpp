@@ -45,6 +45,8 @@ hipError_t launch_psp_efforts(int dof, int vo, hipStream_t st, const PoseBufs& b
 // lds_pad: UWVK_OPT_LDS_PAD's dynamic LDS bytes per workgroup (diagnostic)
 hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
                             int64_t grid = 0, uint32_t ev_any = 0xffffffffu, uint32_t lds_pad = 0);
+// static LDS of one k_psp_epoch workgroup (sizeof PspSmem<dof>)
+size_t psp_epoch_lds_bytes(int dof);
 // resident k_psp_epoch blocks per XCD (occupancy x CUs / 8), 0 if unknown
 int64_t psp_epoch_slots_per_xcd(int dof, int device);
 // resident blocks of the static (k_psp_epoch) or persistent (k_psp_epoch_p)

@@ -1817,7 +1817,13 @@ UWVK_DEV void spd_solve(const double (&L)[M * (M + 1) / 2], const double (&idg)[
 }
 
 // the full BodyEfforts update (gate: accept any).  sig_hbm: the instance's
-// Sigma in HBM (what sm.S held before the factor overwrote it); z and R are
+// Sigma in HBM (what sm.S held before the factor overwrote it).
+// PRECONDITION: sm.S holds Sigma itself, not the epoch kernel's time-scaled
+// Sigma~ = D^-1 Sigma D^-1 (ds = ids = 1: the state load_psp leaves), and
+// sig_hbm holds the same Sigma.  Both callers (k_psp_efforts, k_psp_update)
+// load the instance just before the call; fusing this update into
+// k_psp_epoch's epoch loop needs psp_fold first (tests/test_gpu_efforts.py
+// holds run_log's efforts epochs to the literal kernel at a full grid).  z and R are
 // read where they are used (held in registers through the factor and the
 // points they were 84 VGPRs of the kernel's peak)
 template <int DOF, int SR, class HM>

@@ -602,14 +602,21 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
 #endif
 }
 
+// PSP_EPOCH_ATTR: an attribute hook for occupancy A/Bs (make variant VFLAGS=...),
+// empty in the product build
+#ifndef PSP_EPOCH_ATTR
+#define PSP_EPOCH_ATTR
+#endif
 template <int DOF, int QM, int EVS, int SR>
-__global__ __launch_bounds__(64) void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
+__global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmem<DOF> sm;
   const int64_t B = b.batch;
   const TailUnit tu = tail_unit(ea, B);
   if (tu.chunk > 0 && !tail_wait(ea.tail_flag + tu.tslot, ea.tag * 16u + (uint32_t)tu.chunk, ea.wait_bound)) {
-    if (lane_id() == 0)  // atomic: the late predecessor may still flag the same word
+    if (lane_id() == 0) {  // atomic: the late predecessor may still flag the same word
       __hip_atomic_fetch_or(b.status + tu.inst, UWVK_ST_SCHEDULE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ea.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // host-mapped word
+    }
     return;
   }
   const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
@@ -642,8 +649,10 @@ __global__ __launch_bounds__(64) void k_psp_epoch_p(PoseBufs b, PoseShared sh0, 
     const TailUnit tu = ticket_unit(ea, u);
     uint32_t vn = 0;
     if (tu.chunk > 0 && !tail_wait_t<true>(ea.tail_flag + tu.tslot, ea.tag * 16u + (uint32_t)tu.chunk, ea.wait_bound)) {
-      if (lane_id() == 0)
+      if (lane_id() == 0) {
         __hip_atomic_fetch_or(b.status + tu.inst, UWVK_ST_SCHEDULE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ea.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // host-mapped word
+      }
       u = grid + ticket_value(ea, ticket_issue(ea));
       pre.have = false;
 #pragma unroll
@@ -854,6 +863,8 @@ int xcd_round_robin(int device) {
   cache[device].store(ok, std::memory_order_release);
   return ok;
 }
+
+size_t psp_epoch_lds_bytes(int dof) { return dof == 53 ? sizeof(psp::PspSmem<53>) : sizeof(psp::PspSmem<26>); }
 
 int64_t psp_epoch_slots_per_xcd(int dof, int device) { return psp_epoch_slots(dof, device, false) / 8; }
 

@@ -12,6 +12,7 @@
 namespace uwvk {
 // uwvk_last_device_error: the HIP error behind the thread's last UWVK_EDEVICE
 thread_local char g_last_hip_error[160] = "";
+void clear_hip_error() { g_last_hip_error[0] = 0; }
 void note_hip_error(int err, const char* where) {
   std::snprintf(g_last_hip_error, sizeof(g_last_hip_error), "%s: %s (in %s)", hipGetErrorName((hipError_t)err),
                 hipGetErrorString((hipError_t)err), where ? where : "?");
@@ -56,6 +57,7 @@ const char* uwvk_status_string(uwvk_status s) {
     case UWVK_EDEVICE: return "UWVK_EDEVICE: no usable gfx950 device / HIP error";
     case UWVK_ENOMEM: return "UWVK_ENOMEM: device allocation failed";
     case UWVK_ENOTINIT: return "UWVK_ENOTINIT: filter state not initialised";
+    case UWVK_ESCHEDULE: return "UWVK_ESCHEDULE: a tail-chunk hand-off timed out (re-initialise the flagged instances)";
   }
   return "UWVK_?";
 }
@@ -67,7 +69,10 @@ uwvk_status uwvk_device_malloc(int device, size_t bytes, void** out) {
   uwvk::DeviceGuard g(device);
   return hipMalloc(out, bytes ? bytes : 16) == hipSuccess ? UWVK_OK : UWVK_ENOMEM;
 }
-uwvk_status uwvk_device_free(void* p) { return hipFree(p) == hipSuccess ? UWVK_OK : UWVK_EDEVICE; }
+uwvk_status uwvk_device_free(void* p) {
+  uwvk::clear_hip_error();
+  return hipFree(p) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
+}
 // Synchronous with ALL device work: every handle launches on its own
 // non-blocking stream, which the null-stream hipMemcpy does not wait for, so
 // a read after run_log(sync = 0) would otherwise race the epoch kernels.
@@ -92,11 +97,13 @@ uwvk_status uwvk_memcpy_d2h(void* dst, const void* src, size_t bytes) {
 // Stream-ordered: queued on `stream` (a handle's uwvk_*_stream), behind
 // everything already queued there; returns once the copy has completed.
 uwvk_status uwvk_memcpy_h2d_on(void* dst, const void* src, size_t bytes, void* stream) {
+  uwvk::clear_hip_error();
   hipStream_t st = (hipStream_t)stream;
   if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st) != hipSuccess) return UWVK_EDEVICE;
   return hipStreamSynchronize(st) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
 }
 uwvk_status uwvk_memcpy_d2h_on(void* dst, const void* src, size_t bytes, void* stream) {
+  uwvk::clear_hip_error();
   hipStream_t st = (hipStream_t)stream;
   if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) return UWVK_EDEVICE;
   return hipStreamSynchronize(st) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;

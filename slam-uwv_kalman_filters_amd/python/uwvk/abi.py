@@ -101,7 +101,7 @@ EV_EFFORTS = 0x10
 EV_EFFORTS_VELOCITY_ONLY = 0x20
 
 STATUS = {0: "UWVK_OK", 1: "UWVK_EINVAL", 2: "UWVK_ENAN", 3: "UWVK_ENOTPD", 4: "UWVK_ENOMODEL",
-          5: "UWVK_EDEVICE", 6: "UWVK_ENOMEM", 7: "UWVK_ENOTINIT"}
+          5: "UWVK_EDEVICE", 6: "UWVK_ENOMEM", 7: "UWVK_ENOTINIT", 8: "UWVK_ESCHEDULE"}
 
 # storage / tangent layout of PoseState (PoseState.hpp:29-45)
 FULL = dict(dof=53, store=54, s_pos=0, s_quat=3, s_vel=7, s_acc=10, s_bg=13, s_ba=16, s_grav=19,

@@ -48,7 +48,7 @@ SYMBOLS = [
 ]
 
 _LIB = None
-ABI_VERSION = 2  # include/uwvk.h UWVK_ABI_VERSION this binding is written against
+ABI_VERSION = 3  # include/uwvk.h UWVK_ABI_VERSION this binding is written against
 DP = C.POINTER(C.c_double)
 VP = C.c_void_p
 
@@ -202,6 +202,11 @@ class PoseUKFBatch:
         """UWVK_OPT_PERSIST: run_log on resident workgroups that take work units
         from a ticket counter (bitwise the same results as one workgroup per instance)."""
         _chk(self.L.uwvk_pose_set_option(self.h, 6, int(bool(on))), "set_option")
+
+    def set_wait_bound(self, sleeps):
+        """UWVK_OPT_WAIT_BOUND (tests): < 0 the planner's hand-off wait bound, else
+        that many ~1.7 us sleeps; 0 makes every hand-off of a spread launch time out."""
+        _chk(self.L.uwvk_pose_set_option(self.h, 8, int(sleeps)), "set_option")
 
     def set_literal_apply_delta(self, on=True):
         """ukfom's literal apply_delta re-spread instead of the exact T Sigma T^T form."""

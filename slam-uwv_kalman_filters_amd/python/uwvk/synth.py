@@ -322,12 +322,13 @@ def make_pose_log(batch, epochs, mode="C3", seed=SEED, dof=53, dt=1e-3, first_in
 
     # gyro: the rate noise the filter's process model assumes for the config's
     # rotation_rate.randomwalk (1e-4): the orientation block of Q is
-    # randomwalk^2 (PoseUKF.cpp:408) scaled by dt^2 per step (:462), i.e. a
-    # per-sample rate noise of sd randomwalk.  (Before r05 this drew sd
+    # diag(randomwalk^2) (PoseUKF.cpp:409) scaled by dt^2 per step (:460), i.e. a
+    # per-sample rate noise of sd randomwalk on each axis (the 3-vector: an
+    # anisotropic config's y / z axes get their own sd).  (Before r05 this drew sd
     # randomwalk / sqrt(dt), 1/dt times the variance, and the ensemble NEES of
     # long windows grew with the window: 9 -> 102 over 40 s, roll / pitch
     # overconfident; tools/nees_components.py)
-    sg = cfg.rotation_rate.randomwalk[0]
+    sg = np.array([cfg.rotation_rate.randomwalk[k] for k in range(3)])
     sa = 1e-3 / np.sqrt(dt)  # a measurement: acc_cov = sa^2 below
     gyro = rec(0, epoch0, epochs, 3)  # [epochs][batch][3]
     gyro *= sg

@@ -28,7 +28,7 @@ def test_library_exports_every_symbol():
     L = C.CDLL(engine.LIB_PATH)
     missing = [s for s in header_functions() if not hasattr(L, s)]
     assert not missing, missing
-    assert L.uwvk_abi_version() == engine.ABI_VERSION == 2
+    assert L.uwvk_abi_version() == engine.ABI_VERSION == 3
 
 
 def test_no_cpu_fallback():

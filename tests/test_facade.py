@@ -12,7 +12,7 @@ PKG = os.path.join(ROOT, "slam-uwv_kalman_filters_amd")
 
 def _build(tmp, name="facade_test"):
     exe = os.path.join(tmp, name)
-    cmd = ["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(PKG, "include"),
+    cmd = ["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-I", os.path.join(PKG, "include"),
            os.path.join(HERE, "cpp", name + ".cpp"), "-o", exe,
            "-L", PKG, "-luwvk", "-Wl,-rpath," + PKG,
            "-L", os.path.join(ROOT, "oracle"), "-loracle", "-Wl,-rpath," + os.path.join(ROOT, "oracle"), "-lm"]
@@ -20,7 +20,7 @@ def _build(tmp, name="facade_test"):
     return exe
 
 
-@pytest.mark.parametrize("name", ["facade_test", "facade_small_test"])
+@pytest.mark.parametrize("name", ["facade_test", "facade_small_test", "reference_calls", "linalg_test"])
 def test_facade_compiles(tmp_path, name):
     _build(str(tmp_path), name)
 
@@ -38,5 +38,28 @@ def test_facade_small_filters_match_oracle(tmp_path):
     """BottomUKF / IndirectPoseUKF facades (incl. the visual update's feature packing)."""
     exe = _build(str(tmp_path), "facade_small_test")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_reference_call_forms_match_oracle(tmp_path):
+    """tests/cpp/reference_calls.cpp uses only the reference's
+    call forms (<uwv_kalman_filters/PoseUKF.hpp>, batch-1 constructors, nested
+    MEASUREMENT types, integrateMeasurement(adcp, cell_weighting),
+    resetFilterWithExternalPose(Affine3d), VelocityUKF::BodyEffortsMeasurement, ...)
+    and matches the CPU oracle on every update kind."""
+    exe = _build(str(tmp_path), "reference_calls")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_reference_value_types(tmp_path):
+    """The facade's Eigen stand-ins and reference value types (CPU): Eigen's
+    storage / comma-init / quaternion conventions against the oracle's
+    quaternion algebra, the PoseState store layout, the config conversions."""
+    exe = _build(str(tmp_path), "linalg_test")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr

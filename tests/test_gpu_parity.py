@@ -120,6 +120,10 @@ def test_single_update(eng, orc, dof, kind, path):
                                                   (53, "C3", 400, "dense"), (53, "C4", 1000, "dense"),
                                                   (53, "C3", 400, "literal"), (53, "C4", 1000, "literal")])
 def test_run_log(eng, orc, dof, mode, epochs, path):
+    """C3 over 400 epochs (IMU + 2 DVL), C4 over 1000 (IMU, 5 DVL, 10 pressure,
+    1 ADCP x 4 cells); at the default 30 s / 10 s cycle the 1 s of C4 holds no
+    drop-out, so no BodyEfforts epoch: the efforts split is covered by
+    test_run_log_long_single_launch and the golden pose_c4* fixtures."""
     cfg, uwv, log, o, g = _pair(eng, orc, 4, dof, mode, epochs, path=path)
     counts_o = o.run_log(log)
     dlog = g.upload_log(log)
@@ -283,8 +287,19 @@ def test_nan_measurement_rejected(eng):
 
 def test_run_log_long_single_launch(eng, orc):
     """3000 C4 epochs in ONE run_log call: exercises the PSP kernel's periodic
-    fold of the time scale (every 1024 epochs) and the efforts-epoch split."""
-    cfg, uwv, log, o, g = _pair(eng, orc, 3, 53, "C4", 3000)
+    fold of the time scale (every 1024 epochs) and the efforts-epoch split.  The
+    drop-out cycle is compressed (0.5 s on / 0.25 s off) so that the 3 s hold
+    DVL drop-outs and their BodyEfforts epochs (the default 30 s / 10 s cycle
+    would hold none)."""
+    from uwvk import abi, synth
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(3, 3000, "C4", dropout_on=0.5, dropout_off=0.25)
+    n_eff = int(((log["flags"] & abi.EV_EFFORTS) != 0).sum())
+    assert n_eff >= 8, n_eff  # the launch really splits at efforts epochs, before and after the fold
+    assert ((log["flags"][1024:] & abi.EV_EFFORTS) != 0).any()
+    o = orc.OraclePoseBatch(3, 53)
+    g = eng.PoseUKFBatch(3, 53)
+    init_both(o, g, cfg, uwv, log)
     counts_o = o.run_log(log)
     dlog = g.upload_log(log)
     acc = eng.DeviceBuffer(np.zeros((3, 4), np.uint32))

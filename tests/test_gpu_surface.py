@@ -352,8 +352,8 @@ def _xcd_samples(B, n=16):
 def test_c4_full_batch_sampled(eng, orc):
     """C4 at batch 65,536 over 2,000 epochs with the drop-out cycle compressed
     100x (0.3 s / 0.1 s: 8 DVL, 2 ADCP, 20 pressure and 7 BodyEfforts epochs):
-    the PSP launches split at the efforts epochs and k_pose_efforts_epoch at
-    2 waves/SIMD, as in the C4 bench.  Sampled instances against the oracle
+    the PSP launches split at the efforts epochs and the efforts update on
+    k_psp_efforts (PSP, k = 48, since r05), as in the C4 bench.  Sampled instances against the oracle
     (their logs are generated alone: the Philox streams are keyed by the
     global instance id), no status bits, and a second run bitwise equal."""
     from uwvk import abi, synth
@@ -390,6 +390,59 @@ def test_c4_full_batch_sampled(eng, orc):
         o = orc.OraclePoseBatch(1, 53)
         o.init_from_config(li["pos0"], li["pos_cov"], li["rot0"], li["rot_cov"], cfg, uwv)
         o.set_process_noise_from_config(cfg, 1e-3)
+        co = o.run_log(li)
+        np.testing.assert_array_equal(co[0], counts[i])
+        xo, Po = o.get_state()
+        se = state_err(xg[i:i + 1], xo, Po, 53).max()
+        ce = cov_err(Pg[i:i + 1], Po).max()
+        assert se < TOL_LOG and ce < TOL_LOG, "instance %d: state %g cov %g" % (i, se, ce)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("persist", [None, 0])
+def test_headline_shape_sampled(eng, orc, persist):
+    """The exact shape of the driver's bench line: C3 at
+    batch 65,536, the Monte-Carlo start through the second constructor
+    (bench.initialise "mc", PoseUKF.cpp:374-391), the DVL-aligned log
+    (bench.window_shift) with its 5-epoch warm-up launch, then the 20-epoch
+    window in ONE run_log launch on k_psp_epoch<53, 1, 1, 1> (right SO3 side,
+    no pressure / ADCP events) with the default scheduler (persistent, tail
+    chunks spread over the ticket counter) and, persist=0, the static
+    tail-spread launch.  16+ XCD-spread instances (tail instances included)
+    against the oracle, each run alone on its own one-instance log (the
+    Philox streams are keyed by the global instance id)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from uwvk import synth
+    B, warmup, steps = 65536, 5, 20
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log, shift = bench.dvl_aligned_log(synth, B, warmup, steps, "C3", 53, 0, cfg=cfg)
+    e0 = shift + warmup
+    assert int(((log["flags"][e0:] & 2) != 0).sum()) >= 1  # the window holds its DVL epoch
+    g = _mk(eng, B, 53)
+    if persist is not None:
+        g.set_persist(persist)
+    bench.initialise(g, log, cfg, uwv, "mc")
+    g.set_process_noise_from_config(cfg, log["dt"])
+    dlog = g.upload_log(log)
+    acc = eng.DeviceBuffer(np.zeros((B, 4), np.uint32))
+    g.run_log(dlog, 0, e0, accept_counts=acc)
+    g.run_log(dlog, e0, steps, accept_counts=acc)
+    counts = acc.read(np.uint32, (B, 4))
+    assert not g.get_status().any()
+    xg, Pg = g.get_state()
+    assert np.all(np.isfinite(xg)) and np.all(np.isfinite(Pg))
+    del log, dlog
+    samples = _xcd_samples(B)
+    # the persistent plan's tail units are the last instances of the batch
+    samples = sorted(set(samples) | {B - 2, B - 100, B - 3000})
+    for i in samples:
+        li, _ = bench.dvl_aligned_log(synth, 1, warmup, steps, "C3", 53, i, cfg=cfg)
+        o = orc.OraclePoseBatch(1, 53)
+        bench.initialise(o, li, cfg, uwv, "mc", first_instance=i)
+        o.set_process_noise_from_config(cfg, li["dt"])
         co = o.run_log(li)
         np.testing.assert_array_equal(co[0], counts[i])
         xo, Po = o.get_state()

@@ -167,3 +167,40 @@ def test_persist_default_plan_repeat(eng):
     got = _run(eng, B, 53, log, cfg, uwv, 0, [(0, 30), (30, 30)], persist=True)
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("persist", [False, True])
+def test_handoff_timeout_is_an_error(eng, persist):
+    """ABI 3: a timed-out tail-chunk hand-off makes
+    uwvk_pose_run_log return UWVK_ESCHEDULE (not only a status bit), the
+    chunks after it flag their instances UWVK_ST_SCHEDULE, every other instance
+    is bitwise the unspread run, and the handle's fault word is cleared: the
+    next launch without forced timeouts returns OK again."""
+    from uwvk import synth
+    n, slots, E = 12, 3, 20
+    B = 8 * n
+    assert eng.lib().uwvk_pose_tail_chunks(n, slots, E) > 1
+    assert eng.lib().uwvk_pose_tail_chunks(B, 8 * slots, E) > 1  # the persistent plan
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(B, E, "C3")
+    ref = _run(eng, B, 53, log, cfg, uwv, -1, [(0, E)])
+    g = eng.PoseUKFBatch(B, 53)
+    g.set_tail_slots(slots)
+    g.set_persist(persist)
+    g.set_wait_bound(0)  # every chunk k > 0 gives up at once
+    g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    g.set_process_noise_from_config(cfg, 1e-3)
+    dlog = g.upload_log(log)
+    with pytest.raises(eng.UWVKError, match="UWVK_ESCHEDULE"):
+        g.run_log(dlog, 0, E)
+    g.synchronize()
+    st = g.get_status()
+    bad = (st & 0x8) != 0
+    assert bad.any() and not bad.all()
+    x, P = g.get_state()
+    np.testing.assert_array_equal(x[~bad], ref[0][~bad])
+    np.testing.assert_array_equal(P[~bad], ref[1][~bad])
+    # the fault word was cleared: an unspread launch reports OK
+    g.set_tail_slots(-1)
+    g.set_wait_bound(-1)
+    g.run_log(dlog, 0, E)
