@@ -93,6 +93,13 @@ def psp_flops(n=53, k_pred=15, updates=((6, 3, 7),)):
 
 F_STEP_PSP = psp_flops()
 F_UPD3_PSP = psp_flops(updates=((6, 3, 7), (6, 3, 3))) - F_STEP_PSP  # one DVL update
+# the parameter-decoupled kernel (UWVK_OPT_PARAM_BLOCK): the
+# 26-DOF layout's PSP step plus the 27 parameters alone (time scale 2 + its
+# reciprocal with two Newton steps 8, dt^2 Q band 3, mean decay 3 per epoch):
+# the work it executes, not the 53-DOF algebra's zeros
+F_PD_PARAMS = 27 * 16
+F_STEP_PSP_PD = psp_flops(26) + F_PD_PARAMS
+F_UPD3_PSP_PD = psp_flops(26, updates=((6, 3, 7), (6, 3, 3))) - psp_flops(26)
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector = matrix) spec; probe measured 74 (profiles/r01_probe_fp64.txt)
 PEAK_HBM_GBS = 8000.0
 
@@ -149,6 +156,9 @@ def parse():
     ap.add_argument("--persist", type=int, default=-1,
                     help="UWVK_OPT_PERSIST: 1 persistent workgroups taking work units from a ticket counter, "
                          "0 one workgroup per instance, -1 the engine default")
+    ap.add_argument("--param-block", type=int, default=-1,
+                    help="UWVK_OPT_PARAM_BLOCK: -1 the engine's default (on), 0 always the general 53-DOF kernel, "
+                         "1 the parameter-decoupled kernel while the model-parameter block is uncoupled")
     ap.add_argument("--tail-slots", type=int, default=0,
                     help="UWVK_OPT_TAIL_SLOTS: 0 runtime occupancy, > 0 blocks per XCD, < 0 no tail spreading")
     ap.add_argument("--lds-pad", type=int, default=0,
@@ -533,6 +543,8 @@ def main():
         f.set_lds_pad(a.lds_pad)
     if a.persist >= 0:
         f.set_persist(a.persist)
+    if a.param_block >= 0:
+        f.set_param_block(a.param_block)
     if a.tail_chunks:
         f.set_tail_chunks(a.tail_chunks)
     if a.dense:
@@ -576,6 +588,7 @@ def main():
     # segments' timed runs.  Without segments this is one timed region.
     wall, kernel_ms, stats, pieces, windows = 0.0, 0.0, None, 0, []
     truth = log["truth"]
+    pd_window = None  # the parameter-decoupled kernel at the window's start (UWVK_OPT_PARAM_BLOCK)
     for si, (s0, s1) in enumerate(seg_bounds):
         if seg:
             print("segment %d/%d: epochs [%d, %d)" % (si + 1, len(seg_bounds), s0, s1), file=sys.stderr, flush=True)
@@ -593,6 +606,8 @@ def main():
             reduce_stats(truth.state(min(max(e0, s0), s1), a.dof))
         lo = max(s0, e0)
         if lo < s1:
+            if pd_window is None:
+                pd_window = bool(f.param_block()) and not a.dense
             windows.append(log["flags"][lo - s0:])
             w_s, k_ms, st, n = timed_run(f, dlog, s0, lo, s1, cut_abs, reduce_stats, truth, a.dof, barrier)
             wall, kernel_ms, pieces = wall + w_s, kernel_ms + k_ms, pieces + n
@@ -634,7 +649,7 @@ def main():
     # the engine's own flop model: the useful work it does
     lad = getattr(a, "literal_apply_delta", False)  # the literal re-spread: the reference's own flops
     step_model, upd_model = ((F_STEP, F_UPD3) if lad else (F_STEP_EXEC, F_UPD3_EXEC)) if a.dense \
-        else (F_STEP_PSP, F_UPD3_PSP)
+        else ((F_STEP_PSP_PD, F_UPD3_PSP_PD) if pd_window else (F_STEP_PSP, F_UPD3_PSP))
     flops_model = B * (step_model * a.steps + upd_model * n_dvl)
     eff_tf = flops_ref / (kernel_ms * 1e-3) / 1e12
     model_tf = flops_model / (kernel_ms * 1e-3) / 1e12
@@ -642,9 +657,17 @@ def main():
     # 1 when the window holds no pressure / ADCP epoch (0x4 | 0x8)
     evs = 0 if (f.epoch_qshape() != 1 or bool(((window & 0xC) != 0).any())) else 1
     sr = 0 if a.so3_left else 1
-    kname = ("k_pose_epoch<%d>" % a.dof) if a.dense else ("k_psp_epoch<%d, %d, %d, %d>" % (a.dof, f.epoch_qshape(), evs, sr))
-    workload = "%s-dof%d-b%d%s%s%s" % (log_mode, a.dof, B, "-dense" if a.dense else "",
-                                       "-lad" if getattr(a, "literal_apply_delta", False) else "", "" if sr else "-left")
+    persist = a.persist if a.persist >= 0 else 1  # the engine's default scheduler (UWVK_OPT_PERSIST)
+    kfam = "k_psp_epoch_p" if persist else "k_psp_epoch"
+    if a.dense:
+        kname = "k_pose_epoch<%d>" % a.dof
+    elif pd_window:  # 53-DOF state on the 26-DOF layout (the parameter-decoupled kernel)
+        kname = "%s<26, %d, %d, %d, 1> (53-DOF state, parameter-decoupled)" % (kfam, f.epoch_qshape(), evs, sr)
+    else:
+        kname = "%s<%d, %d, %d, %d>" % (kfam, a.dof, f.epoch_qshape(), evs, sr)
+    workload = "%s-dof%d-b%d%s%s%s%s" % (log_mode, a.dof, B, "-dense" if a.dense else "",
+                                         "-lad" if getattr(a, "literal_apply_delta", False) else "", "" if sr else "-left",
+                                         "-pd" if pd_window else "")
     pmc = pmc_entry(workload, a.steps)
     cr = None if a.dense or launches != 1 else counter_roofline(pmc, B, a.steps, kernel_ms)
     traffic = pmc.get("bytes_per_launch") if pmc.get("epochs_per_launch") == a.steps and launches == 1 else None
@@ -667,6 +690,12 @@ def main():
                                    "active per VALU cycle), plus the MFMA flops" % lanes) if frac_active is not None else None,
             "counters": cr,
             "model_flop_per_step": step_model,
+            "frac_53dof_model": ((B * (F_STEP_PSP * a.steps + F_UPD3_PSP * n_dvl)) / (kernel_ms * 1e-3) / 1e12
+                                 / PEAK_FP64_TFLOPS) if pd_window else None,
+            "frac_53dof_model_note": ("the general 53-DOF kernel's useful-flop model (51,140 flop per step) over "
+                                      "this run's time: the work the parameter-decoupled kernel does not have to "
+                                      "do (the parameter block's zeros) counted as done; for comparison with the "
+                                      "general kernel's frac, not the roofline") if pd_window else None,
             "model_tflops": model_tf,
             "effective_tflops": eff_tf,
             "effective_note": "reference-equivalent rate: SURVEY 8(d)'s literal-ukfom work (1,554,084 flop per "

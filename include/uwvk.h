@@ -479,6 +479,18 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   bound (~2 s plus 64-128 sleeps per epoch); 0 forces every hand-off of a
  *   spread launch to time out. */
 #define UWVK_OPT_WAIT_BOUND 8
+/* UWVK_OPT_PARAM_BLOCK (r06): 1 (default) runs run_log's PSP epoch launches of
+ *   a 53-DOF handle on the parameter-decoupled kernel while the 27 model-
+ *   parameter DOFs (inertia, linear / quadratic damping) are uncoupled: their
+ *   rows of Sigma zero off the diagonal (as PoseUKF.cpp:333-335 make P0; checked
+ *   on the host at init) and Q diagonal there (PoseUKF.cpp:417-422).  That
+ *   kernel keeps the other 26 DOFs in the 26-DOF layout with the 53-DOF
+ *   sigma-point weights and evolves each parameter alone; the results are the
+ *   53-DOF kernel's.  The full BodyEfforts update (and
+ *   any literal-kernel step) couples the block: the handle then runs the
+ *   general kernel until it is re-initialised.  0: always the general kernel.
+ *   uwvk_pose_param_block says which the next launch runs. */
+#define UWVK_OPT_PARAM_BLOCK 9
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
 /* Host-only query (no device work): the chunks per tail instance the
  * UWVK_OPT_TAIL_SLOTS planner picks for one XCD's instances over its resident
@@ -493,6 +505,9 @@ int64_t uwvk_pose_resident_slots(int dof, int device);
  * shape (no coupling of the rewritten rows < 9, band <= 2; the default
  * configuration's), 2 = general (psp_predict QM). */
 int uwvk_pose_epoch_qshape(const uwvk_pose* h);
+/* Host-only query: 1 when the next run_log PSP launch runs the
+ * parameter-decoupled kernel (UWVK_OPT_PARAM_BLOCK), else 0. */
+int uwvk_pose_param_block(uwvk_pose* h);
 /* 1 when a probe grid on device showed round-robin workgroup placement over 8
  * XCCs (block b on the XCC of block b % 8, read from the hardware XCC_ID
  * register): the placement tail spreading's hand-off order relies on.  0 on a

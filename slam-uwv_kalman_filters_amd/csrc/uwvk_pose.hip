@@ -67,6 +67,13 @@ struct uwvk_pose {
   // it holds when the next launch starts (every launch takes units + grid)
   int persist = 1;  // UWVK_OPT_PERSIST (default since r06)
   uint32_t lds_pad = 0;  // UWVK_OPT_LDS_PAD (diagnostic occupancy sweep)
+  // the parameter-decoupled epoch kernel (psp::PspSmemPD):
+  // pdec = the 27 model-parameter DOFs' rows of Sigma are zero off the diagonal
+  // (checked on the host at init; cleared by the full BodyEfforts update and by
+  // any literal-kernel step, which do not keep those zeros exact)
+  int pd_opt = 1;  // UWVK_OPT_PARAM_BLOCK
+  bool pdec = false;
+  double* d_Qp_pd = nullptr;  // the PD table: the 26-DOF subset's {A A, dt^2 Q}, then the parameters' diagonal
   int wait_bound = -1;   // UWVK_OPT_WAIT_BOUND: < 0 the planner's bound, else that many sleeps (tests)
   uint32_t* d_ticket = nullptr;
   // hand-off fault word: pinned, coherent host memory the epoch kernel writes
@@ -136,6 +143,22 @@ static bool q_is_simple(const uwvk_pose* h) {
   return true;
 }
 
+// the process noise leaves the parameter block decoupled: no Q entry in a
+// parameter row / column (tangent 19..45) off the diagonal
+static bool q_params_diag(const uwvk_pose* h) {
+  if (h->dof != 53) return false;
+  if (h->Qh.empty()) return true;
+  for (int i = 0; i < 53; i++)
+    for (int j = 0; j < 53; j++)
+      if (i != j && ((i >= 19 && i <= 45) || (j >= 19 && j <= 45)) && h->Qh[(size_t)i * 53 + j] != 0.0) return false;
+  return true;
+}
+// the next PSP epoch launch runs the parameter-decoupled kernel (after
+// upload_shared: q_simple is the current Q's)
+static bool use_pd(const uwvk_pose* h) {
+  return h->pd_opt && h->pdec && h->dof == 53 && h->sh.q_simple && q_params_diag(h);
+}
+
 static hipError_t upload_shared(uwvk_pose* h, double dt) {
   hipError_t e = hipSuccess;
   if (dt != h->qp_dt) {
@@ -189,6 +212,24 @@ static hipError_t upload_shared(uwvk_pose* h, double dt) {
     h->sh.q_simple = q_is_simple(h) ? 1 : 0;
     e = hipMemcpyAsync(h->d_Qp, qp.data(), qp.size() * 8, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h->d_qband, band.data(), 128 * 8, hipMemcpyHostToDevice, h->stream);
+    // the PD kernel's table: the 26-DOF subset's entries in its packed order,
+    // then parameter t's (19 + t, 19 + t) entry at 351 + t (psp::lane_q PD)
+    std::vector<double> qpd((351 + 32) * 2, 0.0);
+    if (n == 53) {
+      auto m = [](int d) { return d < 19 ? d : d + 27; };
+      for (int i = 0, k = 0; i < 26; i++)
+        for (int j = 0; j <= i; j++, k++) {
+          const int I = m(i), J = m(j), k53 = I * (I + 1) / 2 + J;
+          qpd[2 * k] = qp[2 * k53];
+          qpd[2 * k + 1] = qp[2 * k53 + 1];
+        }
+      for (int t = 0; t < 27; t++) {
+        const int d = 19 + t, k53 = d * (d + 1) / 2 + d;
+        qpd[2 * (351 + t)] = qp[2 * k53];
+        qpd[2 * (351 + t) + 1] = qp[2 * k53 + 1];
+      }
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h->d_Qp_pd, qpd.data(), qpd.size() * 8, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);  // qp, band are locals
     if (e != hipSuccess) return e;
     h->qp_dt = dt;
@@ -246,6 +287,7 @@ uwvk_status uwvk_pose_create(int64_t batch, int dof, int device, uwvk_pose** out
             hipMalloc(&h->d_accepted, B) == hipSuccess && hipMalloc(&h->d_scratch, (B * 3 + 256 + ((B + 63) / 64) * kStatsMaxOut) * 8) == hipSuccess &&
             hipMalloc(&h->d_shared, sizeof(PoseShared)) == hipSuccess &&
             hipMalloc(&h->d_Qp, n * (n + 1) * 8) == hipSuccess && hipMalloc(&h->d_qband, 128 * 8) == hipSuccess &&
+            hipMalloc(&h->d_Qp_pd, (351 + 32) * 2 * 8) == hipSuccess &&
             hipMalloc(&h->d_ticket, 4) == hipSuccess &&
             hipHostMalloc((void**)&h->h_fault, 4, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
             hipHostGetDevicePointer((void**)&h->d_fault, h->h_fault, 0) == hipSuccess &&
@@ -274,6 +316,7 @@ void uwvk_pose_destroy(uwvk_pose* h) {
   for (void* p : {(void*)h->d_mu, (void*)h->d_sigma, (void*)h->d_Q, (void*)h->d_rot, (void*)h->d_off,
                   (void*)h->d_model, (void*)h->d_uwv, (void*)h->d_status, (void*)h->d_meas, (void*)h->d_mask,
                   (void*)h->d_accepted, (void*)h->d_scratch, (void*)h->d_shared, (void*)h->d_Qp, (void*)h->d_qband,
+                  (void*)h->d_Qp_pd,
                   (void*)h->d_tail_flag, (void*)h->d_tail_carry, (void*)h->d_ticket})
     if (p) (void)hipFree(p);
   if (h->h_fault) (void)hipHostFree(h->h_fault);
@@ -324,6 +367,20 @@ static uwvk_status upload_state(uwvk_pose* h, const std::vector<double>& x, cons
     for (int i = 0, k = 0; i < h->dof; i++)
       for (int j = 0; j <= i; j++, k++) Pp[b * tn + k] = P[(b * h->dof + i) * h->dof + j];
   HIPCHK(hipMemcpyAsync(h->d_sigma, Pp.data(), Pp.size() * 8, hipMemcpyHostToDevice, h->stream));
+  // the parameter block decoupled (PD kernel): every lower-triangle entry in a
+  // parameter row or column (tangent 19..45) off the diagonal is zero
+  h->pdec = false;
+  if (h->dof == 53) {
+    bool dec = true;
+    for (int64_t b = 0; b < h->batch && dec; b++)
+      for (int i = 19, k0 = 19 * 20 / 2; i < 53 && dec; k0 += ++i)
+        for (int j = 0; j < i; j++)
+          if ((i <= 45 || (j >= 19 && j <= 45)) && Pp[b * tn + k0 + j] != 0.0) {
+            dec = false;
+            break;
+          }
+    h->pdec = dec;
+  }
   HIPCHK(hipMemcpyAsync(h->d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d_model, model.data(), model.size() * 8, hipMemcpyHostToDevice, h->stream));
   double uw[108];
@@ -411,8 +468,10 @@ uwvk_status uwvk_pose_predict(uwvk_pose* h, double dt) {
   if (!h) return UWVK_EINVAL;
   if (!h->has_state) return UWVK_ENOTINIT;
   PoseBufs b = bufs(h);
-  if (use_dense(h))
+  if (use_dense(h)) {
+    h->pdec = false;  // the literal covariance GEMM does not keep the parameter block's zeros exact
     HIPCHK(launch_pose_predict(h->dof, h->stream, b, h->sh, dt));
+  }
   else {
     // upload_shared recomputes the Q shape (q_bw, q_simple, qlo, qoff) for this dt:
     // the by-value PoseShared handed to the kernel must be taken after it
@@ -465,6 +524,9 @@ static uwvk_status launch_update(uwvk_pose* h, int m, const double* mu, const do
   PoseBufs b = bufs(h);
   // BodyEfforts on PSP too (r05): the full model with k = 48 (psp_update_eff),
   // its velocity-only form (constrainVelocity) with k = 9
+  // the literal kernels, and the full BodyEfforts model (non-affine in the
+  // parameters), couple the parameter block: no PD kernel afterwards
+  if (use_dense(h) || (K == MK_EFFORTS && !only_vel)) h->pdec = false;
   if (use_dense(h))
     HIPCHK(launch_pose_update(h->dof, K, h->stream, b, h->sh, ma, m));
   else {
@@ -541,6 +603,7 @@ uwvk_status uwvk_pose_update_visual_landmark(uwvk_pose* h, int32_t n_features, c
     (void)hipStreamSynchronize(h->stream);
     return (uwvk_status)st;
   }
+  h->pdec = false;  // the literal augmented update (all sigma points)
   const hipError_t e = launch_pose_visual(h->dof, h->sh.so3_right, h->stream, bufs(h), va);
   if (hipStreamSynchronize(h->stream) != hipSuccess || e != hipSuccess) return UWVK_EDEVICE;
   return UWVK_OK;
@@ -656,10 +719,10 @@ static int tail_plan(uwvk_pose* h, int64_t n, int64_t s, int64_t count) {
 // units); the last r = chunks x slots instances run as epoch chunks, claimed
 // in chunk order (uwvk_psp_k.hip, k_psp_epoch_p).  UWVK_OPT_TAIL_SLOTS < 0
 // turns the chunks off, > 0 plans for that many slots per XCD.
-static hipError_t prepare_persist(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
+static hipError_t prepare_persist(uwvk_pose* h, EpochArgs& ea, int64_t& grid, int pd) {
   const int64_t B = h->batch;
-  const int64_t s = h->tail_slots > 0 ? 8 * h->tail_slots : psp_epoch_slots(h->dof, h->device, true);
-  const int64_t slots = psp_epoch_slots(h->dof, h->device, true);
+  const int64_t s = h->tail_slots > 0 ? 8 * h->tail_slots : psp_epoch_slots(h->dof, h->device, true, pd);
+  const int64_t slots = psp_epoch_slots(h->dof, h->device, true, pd);
   if (slots <= 0) return hipErrorInvalidValue;
   ea.chunks = 1;
   ea.tail0 = B;
@@ -694,20 +757,20 @@ static hipError_t prepare_persist(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
 
 // the tail layout of one PSP epoch launch (uwvk_psp_k.hip, plan_tail), cached
 // per (instances per XCD, slots, epochs); fills ea's tail fields and the grid
-static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid) {
+static hipError_t prepare_tail(uwvk_pose* h, EpochArgs& ea, int64_t& grid, int pd) {
   ea.chunks = 1;
   ea.ticket = nullptr;
   grid = 0;
-  if (h->persist) return prepare_persist(h, ea, grid);
+  if (h->persist) return prepare_persist(h, ea, grid, pd);
   // an LDS pad lowers the resident blocks below what the tail plan assumes:
   // no spreading then (UWVK_OPT_LDS_PAD is a diagnostic of the unspread launch)
   if (h->tail_slots < 0 || h->lds_pad > 0 || h->batch % 8 != 0) return hipSuccess;
   // placement not the round-robin the XCD-ordered tail plan needs (a
   // partitioned device, another runtime): the ticket-ordered persistent
   // launch spreads the tail without any placement assumption
-  if (!xcd_round_robin(h->device)) return prepare_persist(h, ea, grid);
+  if (!xcd_round_robin(h->device)) return prepare_persist(h, ea, grid, pd);
   const int64_t n = h->batch / 8;
-  const int64_t s = h->tail_slots > 0 ? h->tail_slots : psp_epoch_slots_per_xcd(h->dof, h->device);
+  const int64_t s = h->tail_slots > 0 ? h->tail_slots : psp_epoch_slots_per_xcd(h->dof, h->device, pd);
   const int c = tail_plan(h, n, s, ea.count);
   if (c <= 1) return hipSuccess;
   const int64_t r = c * s;
@@ -753,6 +816,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   ea.accept_counts = accept_counts;
   PoseBufs b = bufs(h);
   if (use_dense(h)) {  // literal kernels: one fused launch per epoch
+    h->pdec = false;
     for (int64_t e = first; e < first + count; e++) {
       ea.first = e;
       ea.count = 1;
@@ -789,8 +853,13 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     int64_t grid = 0;
     uint32_t ev_any = 0;  // the event kinds of this launch's epochs (kernel choice)
     for (int64_t k = e; k < last; k++) ev_any |= hf[k - first];
-    HIPCHK(prepare_tail(h, ea, grid));
-    const hipError_t le = launch_psp_epoch(h->dof, h->stream, b, sh, ea, grid, ev_any, h->lds_pad);
+    // the parameter-decoupled kernel while the parameter block is decoupled
+    // (every launch before the first full BodyEfforts epoch of an init's life)
+    const int pd = use_pd(h) ? 1 : 0;
+    PoseBufs bl = b;
+    if (pd) bl.Qp = h->d_Qp_pd;
+    HIPCHK(prepare_tail(h, ea, grid, pd));
+    const hipError_t le = launch_psp_epoch(h->dof, h->stream, bl, sh, ea, grid, ev_any, h->lds_pad, pd);
     if (le != hipSuccess) {
       ::uwvk::note_hip_error((int)le, "launch_psp_epoch");
       // a persistent launch that did not run took no tickets: restart the
@@ -807,6 +876,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
       ea.count = 1;
       // constrainVelocity (PEffVO) or the full measurementEfforts (psp_update_eff)
       const int vo = (hf[r - first] & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0;
+      if (!vo) h->pdec = false;  // the full model couples the parameters (PD off from here)
       HIPCHK(launch_psp_efforts(h->dof, vo, h->stream, b, sh, ea));
     }
     e = last;
@@ -880,12 +950,22 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
     h->wait_bound = value;
     return UWVK_OK;
   }
+  if (option == UWVK_OPT_PARAM_BLOCK) {
+    h->pd_opt = value ? 1 : 0;
+    return UWVK_OK;
+  }
   return UWVK_EINVAL;
 }
 
 int64_t uwvk_pose_resident_slots(int dof, int device) {
   if (dof != 53 && dof != 26) return 0;
   return psp_epoch_slots_per_xcd(dof, device);
+}
+
+int uwvk_pose_param_block(uwvk_pose* h) {
+  if (!h) return 0;
+  // q_simple is refreshed by upload_shared; evaluate it on the current Q
+  return (h->pd_opt && h->pdec && h->dof == 53 && q_is_simple(h) && q_params_diag(h)) ? 1 : 0;
 }
 
 int uwvk_xcd_round_robin(int device) { return xcd_round_robin(device); }

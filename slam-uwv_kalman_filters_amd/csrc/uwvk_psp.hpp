@@ -12,7 +12,7 @@ hipError_t launch_psp_update_sr(int dof, int kind, hipStream_t st, const PoseBuf
                                 const MeasArgs& ma, int m);
 template <int SR>
 hipError_t launch_psp_epoch_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                               int64_t grid, uint32_t ev_any, uint32_t lds_pad);
+                               int64_t grid, uint32_t ev_any, uint32_t lds_pad, int pd);
 template <int SR>
 hipError_t launch_psp_efforts_sr(int dof, int vo, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
                                  const EpochArgs& ea);
@@ -27,9 +27,9 @@ extern template hipError_t launch_psp_update_sr<0>(int, int, hipStream_t, const 
 extern template hipError_t launch_psp_update_sr<1>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
                                                    const MeasArgs&, int);
 extern template hipError_t launch_psp_epoch_sr<0>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                  const EpochArgs&, int64_t, uint32_t, uint32_t);
+                                                  const EpochArgs&, int64_t, uint32_t, uint32_t, int);
 extern template hipError_t launch_psp_epoch_sr<1>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                  const EpochArgs&, int64_t, uint32_t, uint32_t);
+                                                  const EpochArgs&, int64_t, uint32_t, uint32_t, int);
 // the handle's side (sh.so3_right) picks the launcher
 hipError_t launch_psp_predict(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, double dt);
 hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
@@ -43,15 +43,18 @@ hipError_t launch_psp_efforts(int dof, int vo, hipStream_t st, const PoseBufs& b
 // ev_any: the OR of the launch's epoch flags (selects the kernel instantiation;
 // all bits set is always correct)
 // lds_pad: UWVK_OPT_LDS_PAD's dynamic LDS bytes per workgroup (diagnostic)
+// pd: dof 53 on the parameter-decoupled kernel (psp::PspSmemPD; b.Qp the host's
+// PD table, sh.q_simple required)
 hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                            int64_t grid = 0, uint32_t ev_any = 0xffffffffu, uint32_t lds_pad = 0);
+                            int64_t grid = 0, uint32_t ev_any = 0xffffffffu, uint32_t lds_pad = 0, int pd = 0);
 // static LDS of one k_psp_epoch workgroup (sizeof PspSmem<dof>)
 size_t psp_epoch_lds_bytes(int dof);
 // resident k_psp_epoch blocks per XCD (occupancy x CUs / 8), 0 if unknown
-int64_t psp_epoch_slots_per_xcd(int dof, int device);
+int64_t psp_epoch_slots_per_xcd(int dof, int device, int pd = 0);
 // resident blocks of the static (k_psp_epoch) or persistent (k_psp_epoch_p)
-// epoch kernel on the device (occupancy x CUs), 0 if unknown
-int64_t psp_epoch_slots(int dof, int device, bool persist);
+// epoch kernel on the device (occupancy x CUs), 0 if unknown; pd: the
+// parameter-decoupled kernel's
+int64_t psp_epoch_slots(int dof, int device, bool persist, int pd = 0);
 // chunks per tail instance for one XCD's n instances over s resident blocks in
 // a count-epoch launch (1: no tail spreading)
 int plan_tail(int64_t n, int64_t s, int64_t count);

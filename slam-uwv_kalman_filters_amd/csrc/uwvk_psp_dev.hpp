@@ -92,6 +92,46 @@ static_assert(offsetof(PspSmem<53>, mu) == sizeof(double) * PG<53>::NP, "mu foll
 static_assert(offsetof(PspSmem<53>, stg) == sizeof(double) * (PG<53>::NP + Lay<53>::store), "stg follows mu");
 static_assert(offsetof(PspSmem<26>, mu) == sizeof(double) * PG<26>::NP, "mu follows S");
 static_assert(offsetof(PspSmem<26>, stg) == sizeof(double) * (PG<26>::NP + Lay<26>::store), "stg follows mu");
+// (r06) the parameter-decoupled epoch kernel (PD).  A
+// 53-DOF instance whose 27 model-parameter DOFs (inertia, linear and quadratic
+// damping: tangent 19..45, store 20..46) are uncoupled from every other DOF and
+// from each other -- their rows of Sigma are zero off the diagonal, as the
+// reference's P0 and Q make them (PoseUKF.cpp:333-335, :417-422) and as the
+// IMU / DVL / pressure / ADCP / position updates keep them -- evolves exactly
+// as follows: the other 26 DOFs run the unscented transform of the 53-DOF
+// filter (sigma-point weights of n = 53), and each parameter DOF alone decays
+// toward its offset (PoseUKF.cpp:50-72) with A_ii^2 Sigma_ii + dt^2 Q_ii.  The
+// PD kernel runs the 26-DOF layout (Lay<26>: the same DOFs in the same order)
+// with the 53-DOF weights; parameter t lives in lane 27 + t: its time scale in
+// the lane's ds / ids (the tail hand-off carries all 64 lanes), its Sigma~_ii
+// and mean in LDS (PspSmemPD).  The zeros are never touched, so the results
+// are those of the 53-DOF kernel up to the sign of zero entries.
+constexpr int kPdLane0 = 27, kPdN = 27;  // parameter t in lane kPdLane0 + t
+template <int DOF>
+struct alignas(16) PspSmemPD : PspSmem<DOF> {
+  double pS[32];  // Sigma~_ii of parameter t (time-scaled like Sigma~)
+  double pm[32];  // its mean (store 20 + t of the 53-DOF layout)
+};
+template <int DOF, int PD>
+struct SmemT {
+  using type = PspSmem<DOF>;
+};
+template <int DOF>
+struct SmemT<DOF, 1> {
+  using type = PspSmemPD<DOF>;
+};
+template <int DOF>
+UWVK_DEV double* pd_ptr(PspSmem<DOF>&) {
+  return nullptr;
+}
+template <int DOF>
+UWVK_DEV double* pd_ptr(PspSmemPD<DOF>& s) {
+  return s.pS;  // pm at +32
+}
+// 26-layout tangent DOF / store index -> the 53-layout one (parameters removed)
+UWVK_DEV constexpr int pd_dof(int d) { return d < 19 ? d : d + 27; }
+UWVK_DEV constexpr int pd_store(int s) { return s < 20 ? s : s + 27; }
+
 template <int DOF>
 UWVK_DEV double* flat(PspSmem<DOF>& sm) {
   return reinterpret_cast<double*>(&sm);
@@ -594,7 +634,9 @@ struct PredRows {
 struct LaneQ {
   double q0, q1, q2;
 };
-template <int DOF>
+// PD: fq is the 26-DOF subset's table followed by the parameters' diagonal
+// entries (parameter t at NP + t), the host's PD table (uwvk_pose.hip)
+template <int DOF, int PD = 0>
 UWVK_DEV LaneQ lane_q(const double* fq, int l) {
   const double2* f2 = reinterpret_cast<const double2*>(fq);
   LaneQ q{0.0, 0.0, 0.0};
@@ -602,6 +644,9 @@ UWVK_DEV LaneQ lane_q(const double* fq, int l) {
     q.q0 = f2[pidx(l, l)].y;
     if (l >= 1) q.q1 = f2[pidx(l, l - 1)].y;
     if (l >= 2) q.q2 = f2[pidx(l, l - 2)].y;
+  }
+  if constexpr (PD) {
+    if (l >= kPdLane0 && l < kPdLane0 + kPdN) q.q0 = f2[PG<DOF>::NP + (l - kPdLane0)].y;
   }
   return q;
 }
@@ -612,13 +657,17 @@ UWVK_DEV LaneQ lane_q(const double* fq, int l) {
 // (sh.q_simple: lane-resident band <= 2), 2 known general.  The epoch kernel is
 // instantiated for 1 and 2 and the host picks one: with both branches in one
 // kernel the epoch loop ran 0.7-0.8% slower (profiles/r03/qm/).
-template <int DOF, int QM = 0, int SR = 0>
+// PD (the parameter-decoupled kernel, see PspSmemPD): DOF = 26 layout with the
+// 53-DOF weights; px: the parameters' LDS (pS, pm at + 32)
+template <int DOF, int QM = 0, int SR = 0, int PD = 0>
 UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx& pc, const double* Q,
                           const double* fq, double& ds, double& ids, const LaneQ& lq,
-                          Stamper* st = nullptr) {
+                          Stamper* st = nullptr, double* px = nullptr) {
   using L = Lay<DOF>;
   using G = PG<DOF>;
   constexpr int K = G::KP;
+  static_assert(!PD || (DOF == 26 && QM == 1), "PD: the 26-DOF layout, lane-resident Q");
+  constexpr int NW = PD ? 53 : DOF;  // the filter's n (sigma-point weights)
   int l = olane();  // re-laundered per phase (PSP_PHASE)
   const double dt = pc.dt, dt2 = dt * dt;
   // process-noise shaping from the pre-predict mean (PoseUKF.cpp:448-460)
@@ -661,7 +710,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   }
   PSP_PHASE(21);
   // manifold mean of the orientations (ukfom: ref = X_0, Gauss-Newton, |d| <= 1e-6)
-  constexpr double wc = 1.0 + 2.0 * (DOF - K);
+  constexpr double wc = 1.0 + 2.0 * (NW - K);
   double mq[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) mq[i] = readlane_d(o[i], 2 * K);
@@ -675,7 +724,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       nrm = 0.0;
 #pragma unroll
       for (int i = 0; i < 3; i++) {
-        d[i] = wave_sum_dpp<2 * K + 1>(w * d[i]) * (1.0 / (double)G::N);
+        d[i] = wave_sum_dpp<2 * K + 1>(w * d[i]) * (1.0 / (double)(2 * NW + 1));
         nrm += d[i] * d[i];
       }
       double e[4], q[4];
@@ -800,7 +849,8 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     nv[q] = t0 + dt * t1;  // A_rr = 1 for pos/vel rows
   }
   // new time scale d' = A_ll d (A_ll = 1 on the unscaled DOFs)
-  if (LANE_IF(l, l < DOF && scaled_dof(l))) {
+  // (PD: the parameters' lanes too; pc.nt_tan holds their decay rate)
+  if (LANE_IF(l, (l < DOF && scaled_dof(l)) || (PD && l >= kPdLane0 && l < kPdLane0 + kPdN))) {
     ds = aj * ds;
     double rc = __builtin_amdgcn_rcp(ds);  // d in (0, 1]: two Newton steps
     rc = fma(rc, fma(-ds, rc, 1.0), rc);
@@ -933,6 +983,14 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       band(std::true_type{});
     else
       band(std::false_type{});
+    if constexpr (PD) {  // the parameters' diagonal: the band's k = 0 entry, as above
+      if (LANE_IF(l, l >= kPdLane0 && l < kPdLane0 + kPdN)) {
+        const int t = (l - kPdLane0) & 31;
+        const double v = px[t];
+        const double f = lq.q0 * (ids * ids);
+        if (lq.q0 != 0.0) px[t] = v + f;
+      }
+    }
     for (int k = 3; k <= (QM == 1 ? 0 : bw); k++) {  // uniform bound: wide Q bands only
       const double idj = shfl_d(ids, l - k >= 0 ? l - k : 0);
       const int j = l - k;
@@ -950,9 +1008,17 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   static_assert(Lay<DOF>::store + PG<DOF>::STG >= 64, "mu reads of lanes >= store stay in PspSmem");
   double mv = proc_vect_lane(l & 63, flat(sm) + kFlatMu<DOF>, pc);
   asm volatile("" : "+v"(mv));
+  [[maybe_unused]] double mvp = 0.0;  // PD: the parameters' means (lane 27 + t, px + 32)
+  if constexpr (PD) {
+    mvp = proc_vect_lane((l - kPdLane0) & 31, px + 32, pc);
+    asm volatile("" : "+v"(mvp));
+  }
   psync();
   if (LANE_IF(l, l < L::store && !(l >= 3 && l < 7))) sm.mu[l] = mv;
   if (LANE_IF(l, l < 4)) sm.mu[3 + l] = mq[l];
+  if constexpr (PD) {
+    if (LANE_IF(l, l >= kPdLane0 && l < kPdLane0 + kPdN)) px[32 + ((l - kPdLane0) & 31)] = mvp;
+  }
   psync();
   PSP_PHASE(26);
   return ok;
@@ -961,8 +1027,8 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
 // Sigma~ -> Sigma (d folded in, d = 1 afterwards): row sweep, lane l owns
 // column l of every row i >= l (uniform row offset, d_i a uniform read-back);
 // d = 1 on the unscaled DOFs, so their entries are multiplied by 1 (bitwise kept)
-template <int DOF>
-UWVK_DEV void psp_fold(PspSmem<DOF>& sm, double& ds, double& ids) {
+template <int DOF, int PD = 0>
+UWVK_DEV void psp_fold(PspSmem<DOF>& sm, double& ds, double& ids, double* px = nullptr) {
   const int l = olane();
   psync();
   const double dl = l < DOF ? ds : 1.0;
@@ -987,6 +1053,12 @@ UWVK_DEV void psp_fold(PspSmem<DOF>& sm, double& ds, double& ids) {
       const double di = readlane_d(ds, i < DOF ? i : DOF - 1);
       double* dst = (i < DOF && l <= i) ? sm.S + e[r] : sm.stg + (l & 63);
       *dst = v[r] * (di * dl);
+    }
+  }
+  if constexpr (PD) {  // the parameters' diagonal: d_i d_i as for any (i, i)
+    if (LANE_IF(l, l >= kPdLane0 && l < kPdLane0 + kPdN)) {
+      const int t = (l - kPdLane0) & 31;
+      px[t] = px[t] * (ds * ds);
     }
   }
   psync();
@@ -1356,7 +1428,9 @@ UWVK_DEV void psp_apply_delta(PspSmem<DOF>& sm, double dl, int l) {
 // ukf::update [EXT], PSP form.  gate: 0 accept any, 1 d2p95.  Returns the gate
 // decision; *ok = false on a non-positive pivot of the partial Cholesky.
 // ---------------------------------------------------------------------------
-template <int DOF, int SR, class HM>
+// NW: the filter's n for the sigma-point weights (53 in the PD kernel's 26-DOF
+// layout, else DOF)
+template <int DOF, int SR, class HM, int NW = DOF>
 UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const double (&Rm)[HM::M * HM::M], int gate,
                          const HM& hm, bool* ok, double ds, double ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
@@ -1381,7 +1455,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double zc[M], zb[M], e[M];
 #pragma unroll
   for (int i = 0; i < M; i++) zc[i] = readlane_d(zp[i], 2 * K);
-  constexpr double wc = 1.0 + 2.0 * (DOF - K);
+  constexpr double wc = 1.0 + 2.0 * (NW - K);
   double S[M * M];
   // H and P first: P reads the staged rows, after which stg holds the
   // transposed sums.  One round of M + M(M+1)/2 sums over the 2K point lanes:
@@ -1424,7 +1498,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     double m[M];
 #pragma unroll
     for (int i2 = 0; i2 < M; i2++) {
-      m[i2] = sums[i2] * (1.0 / (double)G::N);
+      m[i2] = sums[i2] * (1.0 / (double)(2 * NW + 1));
       zb[i2] = zc[i2] + m[i2];
       e[i2] = zc[i2] - zb[i2];
     }

@@ -129,7 +129,7 @@ UWVK_DEV void load_psp(PspSmem<DOF>& sm, const PoseBufs& b, int64_t inst, int l 
 // per-lane process-model constants of storage component s (PoseUKF.cpp:24-79):
 // the state it integrates (pos <- vel, vel <- acc), or its Markov decay -1/tau
 // and the offset it decays towards
-template <int DOF>
+template <int DOF, int PD = 0>
 UWVK_DEV void lane_proc(const PoseBufs& b, const PoseShared& sh, int64_t inst, int s, ProcCtx& pc) {
   using L = Lay<DOF>;
   const uwvk_pose_parameter& P = sh.p;
@@ -152,6 +152,87 @@ UWVK_DEV void lane_proc(const PoseBufs& b, const PoseShared& sh, int64_t inst, i
   // A_ll = 1 + dt nt_tan is one FMA per predict (0 keeps A_ll = 1 exactly)
   pc.nt_tan = 0.0;
   if (s < DOF && scaled_dof(s)) pc.nt_tan = tan_ntau_sel<DOF>(s, sh);
+  if constexpr (PD) {
+    // parameter t = s - 27 of the 53-DOF state (inertia, lin / quad damping,
+    // 9 each, column-major): its mean's decay rate and offset, and the same
+    // rate for its tangent DOF's time scale (the 53-DOF kernel's lanes 20 + t
+    // and 19 + t hold the same values)
+    if (s >= kPdLane0 && s < kPdLane0 + kPdN) {
+      const int t = s - kPdLane0;
+      const double nt = t < 9 ? sh.ntau[2] : (t < 18 ? sh.ntau[3] : sh.ntau[4]);
+      pc.vpart = -1;
+      pc.nt_lane = nt;
+      pc.off_lane = b.off[inst * 28 + t];
+      pc.nt_tan = nt;
+    }
+  }
+}
+
+// PD: the 53-DOF instance's HBM state through the 26-DOF layout.  Packed
+// 26-layout entry e = (i, j) -> the 53-layout packed index (row / column DOF
+// maps pd_dof); a float row estimate corrected by one step either way.
+UWVK_DEV int pd_pidx(int e) {
+  int i = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+  if (((i + 1) * (i + 2)) / 2 <= e) i++;
+  if ((i * (i + 1)) / 2 > e) i--;
+  const int j = e - (i * (i + 1)) / 2;
+  const int I = pd_dof(i), J = pd_dof(j);
+  return (I * (I + 1)) / 2 + J;
+}
+UWVK_DEV constexpr int pd_diag53(int t) { return ((19 + t) * (20 + t)) / 2 + 19 + t; }  // parameter t's (i, i)
+
+// the PD kernel's load: Sigma~'s 26-DOF subset, the mean's 27 stored values,
+// the parameters' diagonal and means (lanes 27..53) into LDS
+UWVK_DEV void load_psp_pd(PspSmem<26>& sm, double* px, const PoseBufs& b, int64_t inst, int l) {
+  using G = PG<26>;
+  const double* gs = b.sigma + inst * (int64_t)PG<53>::NP;
+  const double* gm = b.mu + inst * (int64_t)Lay<53>::store;
+  double v[G::NSLOT];
+#pragma unroll
+  for (int t = 0; t < G::NSLOT; t++) {
+    const int e = l + 64 * t;
+    v[t] = e < G::NP ? gs[pd_pidx(e)] : 0.0;
+  }
+  const double m = l < Lay<26>::store ? gm[pd_store(l)] : 0.0;
+  const bool pl = l >= kPdLane0 && l < kPdLane0 + kPdN;
+  const int tp = pl ? l - kPdLane0 : 0;
+  const double ps = pl ? gs[pd_diag53(tp)] : 0.0, pm = pl ? gm[20 + tp] : 0.0;
+#pragma unroll
+  for (int t = 0; t < G::NSLOT; t++) {
+    const int e = l + 64 * t;
+    if (e < G::NP) sm.S[e] = v[t];
+  }
+  if (l < Lay<26>::store) sm.mu[l] = m;
+  if (pl) {
+    px[tp] = ps;
+    px[32 + tp] = pm;
+  }
+  psync();
+}
+
+// the PD kernel's store: the same entries back (the parameters' off-diagonal
+// zeros are never written)
+UWVK_DEV void store_psp_pd(const PspSmem<26>& sm, const double* px, const PoseBufs& b, int64_t inst, int l) {
+  using G = PG<26>;
+  double* gs = b.sigma + inst * (int64_t)PG<53>::NP;
+  double* gm = b.mu + inst * (int64_t)Lay<53>::store;
+  double v[G::NSLOT];
+#pragma unroll
+  for (int t = 0; t < G::NSLOT; t++) v[t] = flat(sm)[l + 64 * t];  // S at offset 0 (over-reads stay in PspSmem)
+  const double m = flat(sm)[kFlatMu<26> + (l & 63)];
+  const bool pl = l >= kPdLane0 && l < kPdLane0 + kPdN;
+  const int tp = (l - kPdLane0) & 31;
+  const double ps = px[tp], pm = px[32 + tp];
+#pragma unroll
+  for (int t = 0; t < G::NSLOT; t++) {
+    const int e = l + 64 * t;
+    if (e < G::NP) gs[pd_pidx(e)] = v[t];
+  }
+  if (l < Lay<26>::store) gm[pd_store(l)] = m;
+  if (pl) {
+    gs[pd_diag53(tp)] = ps;
+    gm[20 + tp] = pm;
+  }
 }
 
 template <int DOF>
@@ -190,31 +271,32 @@ UWVK_DEV void copy_zr(const double* zin, const double* Rin, double (&z)[M], doub
 }
 
 // one measurement update of kind KIND on instance inst (PSP form, SO3 side SR)
-template <int DOF, int KIND, int SR>
+// NW: the filter's n for the sigma-point weights (psp_update)
+template <int DOF, int KIND, int SR, int NW = DOF>
 UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, const double* zin, const double* Rin,
                         const MeasArgs& ma, bool* ok, double ds, double ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   if constexpr (KIND == MK_ACC) {
     double z[3], R[9];
     copy_zr<3>(zin, Rin, z, R);
-    return psp_update<DOF, SR>(sm, z, R, 0, PAcc<DOF>{}, ok, ds, ids, st);
+    return psp_update<DOF, SR, PAcc<DOF>, NW>(sm, z, R, 0, PAcc<DOF>{}, ok, ds, ids, st);
   } else if constexpr (KIND == MK_VEL) {
     double z[3], R[9];
     copy_zr<3>(zin, Rin, z, R);
-    return psp_update<DOF, SR>(sm, z, R, 0, PVel<DOF>{}, ok, ds, ids, st);
+    return psp_update<DOF, SR, PVel<DOF>, NW>(sm, z, R, 0, PVel<DOF>{}, ok, ds, ids, st);
   } else if constexpr (KIND == MK_PRESSURE) {
     double z[1], R[1];
     copy_zr<1>(zin, Rin, z, R);
     PPressure<DOF> h;
     h.h.s[0] = ma.v3[0]; h.h.s[1] = ma.v3[1]; h.h.s[2] = ma.v3[2];
     h.h.patm = sh.p.atmospheric_pressure;
-    return psp_update<DOF, SR>(sm, z, R, 0, h, ok, ds, ids, st);
+    return psp_update<DOF, SR, PPressure<DOF>, NW>(sm, z, R, 0, h, ok, ds, ids, st);
   } else if constexpr (KIND == MK_WATER) {
     double z[2], R[4];
     copy_zr<2>(zin, Rin, z, R);
     PWater<DOF> h;
     h.cw = ma.extra ? ma.extra[inst] : 0.0;
-    return psp_update<DOF, SR>(sm, z, R, 1, h, ok, ds, ids, st);
+    return psp_update<DOF, SR, PWater<DOF>, NW>(sm, z, R, 1, h, ok, ds, ids, st);
   } else if constexpr (KIND == MK_XY || KIND == MK_GEO || KIND == MK_DELAYED) {
     double z[2], R[4];
     copy_zr<2>(zin, Rin, z, R);
@@ -232,12 +314,12 @@ UWVK_DEV bool do_update(PspSmem<DOF>& sm, const PoseShared& sh, int64_t inst, co
       z[0] = zin[0] + (sm.mu[L::s_pos] - ma.extra[2 * inst]);
       z[1] = zin[1] + (sm.mu[L::s_pos + 1] - ma.extra[2 * inst + 1]);
     }
-    return psp_update<DOF, SR>(sm, z, R, gate, PXY<DOF>{}, ok, ds, ids, st);
+    return psp_update<DOF, SR, PXY<DOF>, NW>(sm, z, R, gate, PXY<DOF>{}, ok, ds, ids, st);
   } else {
     static_assert(KIND == MK_Z, "PSP update kind");
     double z[1], R[1];
     copy_zr<1>(zin, Rin, z, R);
-    return psp_update<DOF, SR>(sm, z, R, 0, PZ<DOF>{}, ok, ds, ids, st);
+    return psp_update<DOF, SR, PZ<DOF>, NW>(sm, z, R, 0, PZ<DOF>{}, ok, ds, ids, st);
   }
 }
 
@@ -404,13 +486,17 @@ template <int DOF>
 struct PspPre {
   double v[PG<DOF>::NSLOT];
   double m;
+  double ps, pm;  // PD: the lane's parameter diagonal entry and mean
   bool have;
 };
 
-template <int DOF, bool PERSIST, int QM, int EVS, int SR, class Again>
-UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea, const TailUnit& tu0,
+// PD: the parameter-decoupled kernel (PspSmemPD): the 26-DOF layout of a
+// 53-DOF instance, px its parameters' LDS
+template <int DOF, bool PERSIST, int QM, int EVS, int SR, int PD, class Again>
+UWVK_DEV void psp_unit(PspSmem<DOF>& sm, double* px, const PoseBufs& b, const EpochArgs& ea, const TailUnit& tu0,
                        const LaneQ& lq, Again again, int64_t tlw, int lp, uint32_t* next = nullptr,
                        PspPre<DOF>* pre = nullptr) {
+  constexpr int NW = PD ? 53 : DOF;  // the filter's n (sigma-point weights)
   const int64_t B = b.batch;
   const int64_t inst = tu0.inst, e_begin = tu0.e0, e_end = tu0.e1;
 #ifdef UWVK_STAMPS
@@ -451,7 +537,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     pc.dt = dtv;
   }
   pc.off = nullptr;
-  lane_proc<DOF>(b, *b.shared, inst, lp, pc);
+  lane_proc<DOF, PD>(b, *b.shared, inst, lp, pc);
   // the next epoch's IMU inputs are prefetched one epoch ahead (their load
   // latency overlaps this epoch's arithmetic)
   uint32_t fl_n = 0;
@@ -474,7 +560,15 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
       if (e < G::NP) sm.S[e] = pre->v[t];
     }
     if (l < Lay<DOF>::store) sm.mu[l] = pre->m;
+    if constexpr (PD) {
+      if (l >= kPdLane0 && l < kPdLane0 + kPdN) {
+        px[l - kPdLane0] = pre->ps;
+        px[32 + l - kPdLane0] = pre->pm;
+      }
+    }
     psync();
+  } else if constexpr (PD) {
+    load_psp_pd(sm, px, b, inst, PERSIST ? olane() : lane_id());
   } else {
     load_psp<DOF>(sm, b, inst, PERSIST ? olane() : lane_id());
   }
@@ -505,12 +599,12 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     }
     const PoseShared& sh = shared_for_epoch(b);
     UWVK_STAMP(41);
-    if (((e - ea.first) & 1023) == 1023) psp_fold<DOF>(sm, ds, ids);  // keep d in range
-    bool sok = psp_predict<DOF, QM, SR>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, st);
+    if (((e - ea.first) & 1023) == 1023) psp_fold<DOF, PD>(sm, ds, ids, px);  // keep d in range
+    bool sok = psp_predict<DOF, QM, SR, PD>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, st, px);
     ok = ok && sok;
     if (fl & UWVK_EV_ACC) {
       if (all_finite(za, 3)) {
-        do_update<DOF, MK_ACC, SR>(sm, sh, inst, za, sh.log_acc_cov, ma, &sok, ds, ids, st);
+        do_update<DOF, MK_ACC, SR, NW>(sm, sh, inst, za, sh.log_acc_cov, ma, &sok, ds, ids, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -519,7 +613,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + inst) * 3;
       if (all_finite(z, 3)) {
-        cnt[0] += do_update<DOF, MK_VEL, SR>(sm, sh, inst, z, sh.log_dvl_cov, ma, &sok, ds, ids, st);
+        cnt[0] += do_update<DOF, MK_VEL, SR, NW>(sm, sh, inst, z, sh.log_dvl_cov, ma, &sok, ds, ids, st);
         ok = ok && sok;
       } else {
         nan = true;
@@ -532,7 +626,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     if (fl & UWVK_EV_PRESSURE) {
       const double* z = ea.pressure + (int64_t)ea.p_index[e] * B + inst;
       if (all_finite(z, 1)) {
-        cnt[1] += do_update<DOF, MK_PRESSURE, SR>(sm, sh, inst, z, &ea.p_cov, ma, &sok, ds, ids);
+        cnt[1] += do_update<DOF, MK_PRESSURE, SR, NW>(sm, sh, inst, z, &ea.p_cov, ma, &sok, ds, ids);
         ok = ok && sok;
       } else {
         nan = true;
@@ -545,7 +639,7 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
         double zz[2] = {z[0], z[1]}, R[4] = {ea.adcp_cov[0], ea.adcp_cov[1], ea.adcp_cov[2], ea.adcp_cov[3]};
         PWater<DOF> h;
         h.cw = ea.cw[c];
-        cnt[2] += psp_update<DOF, SR>(sm, zz, R, 1, h, &sok, ds, ids);
+        cnt[2] += psp_update<DOF, SR, PWater<DOF>, NW>(sm, zz, R, 1, h, &sok, ds, ids);
         ok = ok && sok;
       }
     }
@@ -563,13 +657,29 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     // prefetched), so they are dead through the next unit's epochs
     using G = PG<DOF>;
     const int l = olane();
-    const double* gs = b.sigma + (pre->have ? tn.inst : 0) * (int64_t)G::NP;
+    if constexpr (PD) {  // through the 26-DOF layout (load_psp_pd)
+      const int64_t in = pre->have ? tn.inst : 0;
+      const double* gs = b.sigma + in * (int64_t)PG<53>::NP;
+      const double* gm = b.mu + in * (int64_t)Lay<53>::store;
 #pragma unroll
-    for (int t = 0; t < G::NSLOT; t++) {
-      const int e = l + 64 * t;
-      pre->v[t] = (pre->have && e < G::NP) ? gs[e] : 0.0;
+      for (int t = 0; t < G::NSLOT; t++) {
+        const int e = l + 64 * t;
+        pre->v[t] = (pre->have && e < G::NP) ? gs[pd_pidx(e)] : 0.0;
+      }
+      pre->m = (pre->have && l < Lay<DOF>::store) ? gm[pd_store(l)] : 0.0;
+      const bool pl = pre->have && l >= kPdLane0 && l < kPdLane0 + kPdN;
+      const int tp = pl ? l - kPdLane0 : 0;
+      pre->ps = pl ? gs[pd_diag53(tp)] : 0.0;
+      pre->pm = pl ? gm[20 + tp] : 0.0;
+    } else {
+      const double* gs = b.sigma + (pre->have ? tn.inst : 0) * (int64_t)G::NP;
+#pragma unroll
+      for (int t = 0; t < G::NSLOT; t++) {
+        const int e = l + 64 * t;
+        pre->v[t] = (pre->have && e < G::NP) ? gs[e] : 0.0;
+      }
+      pre->m = (pre->have && l < Lay<DOF>::store) ? b.mu[(pre->have ? tn.inst : 0) * Lay<DOF>::store + l] : 0.0;
     }
-    pre->m = (pre->have && l < Lay<DOF>::store) ? b.mu[(pre->have ? tn.inst : 0) * Lay<DOF>::store + l] : 0.0;
   }
   if (lane_id() == 0) {
     // atomic: a later chunk that timed out flags the same word
@@ -592,9 +702,10 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
     c[1] = ids;
     psync();
   } else {
-    psp_fold<DOF>(sm, ds, ids);
+    psp_fold<DOF, PD>(sm, ds, ids, px);
   }
-  store_psp<DOF>(sm, b, inst, PERSIST ? olane() : lane_id());
+  if constexpr (PD) store_psp_pd(sm, px, b, inst, PERSIST ? olane() : lane_id());
+  else store_psp<DOF>(sm, b, inst, PERSIST ? olane() : lane_id());
   if (hand) tail_signal(ea, tu.tslot, tu.chunk);
 #ifdef UWVK_TIMELINE
   __builtin_amdgcn_s_waitcnt(0);
@@ -607,9 +718,11 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, const PoseBufs& b, const EpochArgs& ea,
 #ifndef PSP_EPOCH_ATTR
 #define PSP_EPOCH_ATTR
 #endif
-template <int DOF, int QM, int EVS, int SR>
+template <int DOF, int QM, int EVS, int SR, int PD = 0>
 __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
-  __shared__ PspSmem<DOF> sm;
+  __shared__ typename SmemT<DOF, PD>::type smx;
+  PspSmem<DOF>& sm = smx;
+  double* const px = pd_ptr<DOF>(smx);
   const int64_t B = b.batch;
   const TailUnit tu = tail_unit(ea, B);
   if (tu.chunk > 0 && !tail_wait(ea.tail_flag + tu.tslot, ea.tag * 16u + (uint32_t)tu.chunk, ea.wait_bound)) {
@@ -619,8 +732,9 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
     }
     return;
   }
-  const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
-  psp_unit<DOF, false, QM, EVS, SR>(sm, b, ea, tu, lq, [&] { return tail_unit(ea, B); }, blockIdx.x, lane_id());
+  const LaneQ lq = lane_q<DOF, PD>(b.Qp, lane_id());
+  psp_unit<DOF, false, QM, EVS, SR, PD>(sm, px, b, ea, tu, lq, [&] { return tail_unit(ea, B); }, blockIdx.x,
+                                        lane_id());
 }
 
 // Persistent form (UWVK_OPT_PERSIST): as many blocks as are resident, each
@@ -631,10 +745,12 @@ __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, Pos
 // dispatch-order assumption.  Faster XCDs / CUs take more units, and a slot
 // moves to its next unit without a new workgroup dispatch.  The next ticket is
 // taken while the current unit runs (its atomic latency hidden).
-template <int DOF, int QM, int EVS, int SR>
-__global__ __launch_bounds__(64) void k_psp_epoch_p(PoseBufs b, PoseShared sh0, EpochArgs ea) {
-  __shared__ PspSmem<DOF> sm;
-  const LaneQ lq = lane_q<DOF>(b.Qp, lane_id());
+template <int DOF, int QM, int EVS, int SR, int PD = 0>
+__global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch_p(PoseBufs b, PoseShared sh0, EpochArgs ea) {
+  __shared__ typename SmemT<DOF, PD>::type smx;
+  PspSmem<DOF>& sm = smx;
+  double* const px = pd_ptr<DOF>(smx);
+  const LaneQ lq = lane_q<DOF, PD>(b.Qp, lane_id());
   // the first unit is the block's own index (no atomic: 3,072 blocks claiming
   // one counter at once queue for ~50 us); tickets number the units from the grid on
   const uint32_t grid = gridDim.x;
@@ -644,6 +760,8 @@ __global__ __launch_bounds__(64) void k_psp_epoch_p(PoseBufs b, PoseShared sh0, 
 #pragma unroll
   for (int t = 0; t < PG<DOF>::NSLOT; t++) pre.v[t] = 0.0;
   pre.m = 0.0;
+  pre.ps = 0.0;
+  pre.pm = 0.0;
 #pragma unroll 1
   while (u < ea.units) {
     const TailUnit tu = ticket_unit(ea, u);
@@ -658,10 +776,13 @@ __global__ __launch_bounds__(64) void k_psp_epoch_p(PoseBufs b, PoseShared sh0, 
 #pragma unroll
       for (int t = 0; t < PG<DOF>::NSLOT; t++) pre.v[t] = 0.0;
       pre.m = 0.0;
+      pre.ps = 0.0;
+      pre.pm = 0.0;
     } else {
       // a laundered lane id: the unit's per-lane constants are recomputed per
       // unit, not hoisted out of the unit loop (held live across it)
-      psp_unit<DOF, true, QM, EVS, SR>(sm, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(), &vn, &pre);
+      psp_unit<DOF, true, QM, EVS, SR, PD>(sm, px, b, ea, tu, lq, [&] { return ticket_unit(ea, u); }, u, olane(),
+                                           &vn, &pre);
       u = vn;  // resolved by psp_unit
     }
     psync();  // the next unit's LDS writes after this unit's reads
@@ -750,13 +871,13 @@ hipError_t launch_psp_efforts_sr(int dof, int vo, hipStream_t st, const PoseBufs
   return hipGetLastError();
 }
 
-template <int DOF, int QM, int EVS, int SR>
+template <int DOF, int QM, int EVS, int SR, int PD = 0>
 static void launch_epoch_q(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea, dim3 g,
                            uint32_t pad) {
   if (ea.ticket)
-    hipLaunchKernelGGL((psp::k_psp_epoch_p<DOF, QM, EVS, SR>), g, dim3(64), pad, st, b, sh, ea);
+    hipLaunchKernelGGL((psp::k_psp_epoch_p<DOF, QM, EVS, SR, PD>), g, dim3(64), pad, st, b, sh, ea);
   else
-    hipLaunchKernelGGL((psp::k_psp_epoch<DOF, QM, EVS, SR>), g, dim3(64), pad, st, b, sh, ea);
+    hipLaunchKernelGGL((psp::k_psp_epoch<DOF, QM, EVS, SR, PD>), g, dim3(64), pad, st, b, sh, ea);
 }
 
 template <int DOF, int SR>
@@ -773,12 +894,17 @@ static void launch_epoch_dof(hipStream_t st, const PoseBufs& b, const PoseShared
 
 template <int SR>
 hipError_t launch_psp_epoch_sr(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                               int64_t grid, uint32_t ev_any, uint32_t lds_pad) {
+                               int64_t grid, uint32_t ev_any, uint32_t lds_pad, int pd) {
   const dim3 g((unsigned)(grid > 0 ? grid : b.batch));
-  if (dof == 53)
+  if (dof == 53 && pd) {  // the parameter-decoupled kernel (b.Qp: the host's PD table; q_simple)
+    if (!sh.q_simple) return hipErrorInvalidValue;
+    if (ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP)) launch_epoch_q<26, 1, 0, SR, 1>(st, b, sh, ea, g, lds_pad);
+    else launch_epoch_q<26, 1, 1, SR, 1>(st, b, sh, ea, g, lds_pad);
+  } else if (dof == 53) {
     launch_epoch_dof<53, SR>(st, b, sh, ea, g, ev_any, lds_pad);
-  else
+  } else {
     launch_epoch_dof<26, SR>(st, b, sh, ea, g, ev_any, lds_pad);
+  }
   return hipGetLastError();
 }
 
@@ -787,7 +913,7 @@ template hipError_t launch_psp_predict_sr<PSP_SIDE>(int, hipStream_t, const Pose
 template hipError_t launch_psp_update_sr<PSP_SIDE>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
                                                    const MeasArgs&, int);
 template hipError_t launch_psp_epoch_sr<PSP_SIDE>(int, hipStream_t, const PoseBufs&, const PoseShared&,
-                                                  const EpochArgs&, int64_t, uint32_t, uint32_t);
+                                                  const EpochArgs&, int64_t, uint32_t, uint32_t, int);
 template hipError_t launch_psp_efforts_sr<PSP_SIDE>(int, int, hipStream_t, const PoseBufs&, const PoseShared&,
                                                     const EpochArgs&);
 
@@ -805,9 +931,9 @@ hipError_t launch_psp_update(int dof, int kind, hipStream_t st, const PoseBufs& 
 }
 
 hipError_t launch_psp_epoch(int dof, hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                            int64_t grid, uint32_t ev_any, uint32_t lds_pad) {
-  return sh.so3_right ? launch_psp_epoch_sr<1>(dof, st, b, sh, ea, grid, ev_any, lds_pad)
-                      : launch_psp_epoch_sr<0>(dof, st, b, sh, ea, grid, ev_any, lds_pad);
+                            int64_t grid, uint32_t ev_any, uint32_t lds_pad, int pd) {
+  return sh.so3_right ? launch_psp_epoch_sr<1>(dof, st, b, sh, ea, grid, ev_any, lds_pad, pd)
+                      : launch_psp_epoch_sr<0>(dof, st, b, sh, ea, grid, ev_any, lds_pad, pd);
 }
 
 hipError_t launch_psp_efforts(int dof, int vo, hipStream_t st, const PoseBufs& b, const PoseShared& sh,
@@ -866,15 +992,19 @@ int xcd_round_robin(int device) {
 
 size_t psp_epoch_lds_bytes(int dof) { return dof == 53 ? sizeof(psp::PspSmem<53>) : sizeof(psp::PspSmem<26>); }
 
-int64_t psp_epoch_slots_per_xcd(int dof, int device) { return psp_epoch_slots(dof, device, false) / 8; }
+int64_t psp_epoch_slots_per_xcd(int dof, int device, int pd) { return psp_epoch_slots(dof, device, false, pd) / 8; }
 
-int64_t psp_epoch_slots(int dof, int device, bool persist) {
+int64_t psp_epoch_slots(int dof, int device, bool persist, int pd) {
   int per_cu = 0, cus = 0;
   // (the other instantiations have the same LDS and no more registers)
   // (every instantiation, both SO3 sides, is held to the same budget by
   // tests/test_kernel_resources.py: <= 168 registers, no scratch, 3 waves/SIMD)
-  const void* k = persist ? (dof == 53 ? (const void*)psp::k_psp_epoch_p<53, 1, 0, 0> : (const void*)psp::k_psp_epoch_p<26, 1, 0, 0>)
-                          : (dof == 53 ? (const void*)psp::k_psp_epoch<53, 1, 0, 0> : (const void*)psp::k_psp_epoch<26, 1, 0, 0>);
+  const void* k;
+  if (dof == 53 && pd)
+    k = persist ? (const void*)psp::k_psp_epoch_p<26, 1, 0, 0, 1> : (const void*)psp::k_psp_epoch<26, 1, 0, 0, 1>;
+  else
+    k = persist ? (dof == 53 ? (const void*)psp::k_psp_epoch_p<53, 1, 0, 0> : (const void*)psp::k_psp_epoch_p<26, 1, 0, 0>)
+                : (dof == 53 ? (const void*)psp::k_psp_epoch<53, 1, 0, 0> : (const void*)psp::k_psp_epoch<26, 1, 0, 0>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return 0;

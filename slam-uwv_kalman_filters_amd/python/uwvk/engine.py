@@ -43,7 +43,7 @@ SYMBOLS = [
     "uwvk_ipose_create", "uwvk_ipose_destroy", "uwvk_ipose_stream", "uwvk_ipose_init", "uwvk_ipose_set_option",
     "uwvk_ipose_set_pose_reference", "uwvk_ipose_predict", "uwvk_ipose_update_visual",
     "uwvk_ipose_get_corrected_pose", "uwvk_ipose_get_state", "uwvk_ipose_get_status",
-    "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots", "uwvk_pose_epoch_qshape", "uwvk_pose_timer_mark", "uwvk_pose_timer_elapsed",
+    "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots", "uwvk_pose_epoch_qshape", "uwvk_pose_param_block", "uwvk_pose_timer_mark", "uwvk_pose_timer_elapsed",
     "uwvk_xcd_round_robin", "uwvk_synth_normal", "uwvk_synth_normal_at",
 ]
 
@@ -88,6 +88,8 @@ def lib(path=None):
         L.uwvk_pose_tail_chunks.argtypes = [C.c_int64, C.c_int64, C.c_int64]
         L.uwvk_pose_epoch_qshape.argtypes = [C.c_void_p]
         L.uwvk_pose_epoch_qshape.restype = C.c_int
+        L.uwvk_pose_param_block.argtypes = [C.c_void_p]
+        L.uwvk_pose_param_block.restype = C.c_int
         L.uwvk_pose_resident_slots.argtypes = [C.c_int, C.c_int]
         L.uwvk_pose_resident_slots.restype = C.c_int64
         L.uwvk_memcpy_h2d.argtypes = [VP, VP, C.c_size_t]
@@ -207,6 +209,15 @@ class PoseUKFBatch:
         """UWVK_OPT_WAIT_BOUND (tests): < 0 the planner's hand-off wait bound, else
         that many ~1.7 us sleeps; 0 makes every hand-off of a spread launch time out."""
         _chk(self.L.uwvk_pose_set_option(self.h, 8, int(sleeps)), "set_option")
+
+    def set_param_block(self, on=True):
+        """UWVK_OPT_PARAM_BLOCK: run_log's launches on the parameter-decoupled
+        kernel while the model-parameter block is uncoupled (default on)."""
+        _chk(self.L.uwvk_pose_set_option(self.h, 9, int(bool(on))), "set_option")
+
+    def param_block(self):
+        """1 when the next run_log launch runs the parameter-decoupled kernel."""
+        return int(self.L.uwvk_pose_param_block(self.h))
 
     def set_literal_apply_delta(self, on=True):
         """ukfom's literal apply_delta re-spread instead of the exact T Sigma T^T form."""

@@ -47,9 +47,15 @@ static void compare(PoseUKF& f, or_pose* o, const char* where) {
     const int d = i < 3 ? i : i - 1;
     w = std::fmax(w, std::fabs(x[i] - xo[i]) / std::sqrt(Po[d * 53 + d]));
   }
-  // orientation: the angle between the quaternions, in the orientation std-dev
-  const double dot = std::fabs(x[3] * xo[3] + x[4] * xo[4] + x[5] * xo[5] + x[6] * xo[6]);
-  const double ang = 2 * std::acos(std::fmin(1.0, dot));
+  // orientation: the angle between the quaternions, 2 |vec(conj(q_o) q)|
+  // (well conditioned near 0, unlike acos of the dot product), in the
+  // orientation std-dev
+  const double* q = x + 3;
+  const double* r = xo + 3;
+  const double vx = r[0] * q[1] - r[1] * q[0] - r[2] * q[3] + r[3] * q[2];
+  const double vy = r[0] * q[2] + r[1] * q[3] - r[2] * q[0] - r[3] * q[1];
+  const double vz = r[0] * q[3] - r[1] * q[2] + r[2] * q[1] - r[3] * q[0];
+  const double ang = 2 * std::sqrt(vx * vx + vy * vy + vz * vz);
   w = std::fmax(w, ang / std::sqrt(std::fmin(Po[3 * 53 + 3], std::fmin(Po[4 * 53 + 4], Po[5 * 53 + 5]))));
   std::printf("%-28s worst %.3e\n", where, w);
   worst = std::fmax(worst, w);
