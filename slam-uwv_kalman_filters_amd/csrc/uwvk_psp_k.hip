@@ -713,10 +713,20 @@ UWVK_DEV void psp_unit(PspSmem<DOF>& sm, double* px, const PoseBufs& b, const Ep
 #endif
 }
 
-// PSP_EPOCH_ATTR: an attribute hook for occupancy A/Bs (make variant VFLAGS=...),
-// empty in the product build
+// Occupancy of the epoch kernels.  The 53-DOF layout is LDS-bound at 12
+// instances per CU (3 waves per SIMD, PspSmem<53> = 12.8 KB) and keeps the
+// compiler's own register allocation (<= 168 VGPRs; an explicit
+// amdgpu_waves_per_eu(3) scheduled its epoch loop worse, r02).  The 26-DOF
+// layout (the kinematic handles and the parameter-decoupled kernel of 53-DOF
+// handles) needs ~4.4 KB of LDS: it is capped at 4 waves per SIMD (16
+// instances per CU, <= 128 VGPRs) at the cost of ~80-130 B/lane of scratch,
+// ~17 reloads per epoch (r06 interleaved A/B, profiles/r06/r06d/: the PD
+// kernel 223.6 -> 233.9 M steps/s over 200 epochs, 206.3-207.9 -> 211.6-212.7
+// over 20; the plain 26-DOF kernel +5.4% / +4%, r06a).  The expression is
+// template-dependent: the 53-DOF instantiations' ISA is unchanged by it.
+// PSP_EPOCH_ATTR (make variant VFLAGS=...) overrides it for occupancy A/Bs.
 #ifndef PSP_EPOCH_ATTR
-#define PSP_EPOCH_ATTR
+#define PSP_EPOCH_ATTR __attribute__((amdgpu_waves_per_eu(DOF == 26 ? 4 : 1, DOF == 26 ? 4 : 8)))
 #endif
 template <int DOF, int QM, int EVS, int SR, int PD = 0>
 __global__ __launch_bounds__(64) PSP_EPOCH_ATTR void k_psp_epoch(PoseBufs b, PoseShared sh0, EpochArgs ea) {
@@ -996,9 +1006,9 @@ int64_t psp_epoch_slots_per_xcd(int dof, int device, int pd) { return psp_epoch_
 
 int64_t psp_epoch_slots(int dof, int device, bool persist, int pd) {
   int per_cu = 0, cus = 0;
-  // (the other instantiations have the same LDS and no more registers)
-  // (every instantiation, both SO3 sides, is held to the same budget by
-  // tests/test_kernel_resources.py: <= 168 registers, no scratch, 3 waves/SIMD)
+  // (the other instantiations of a layout have the same LDS and occupancy:
+  // tests/test_kernel_resources.py holds every 53-DOF one to 3 waves per SIMD
+  // and every 26-DOF-layout one to 4)
   const void* k;
   if (dof == 53 && pd)
     k = persist ? (const void*)psp::k_psp_epoch_p<26, 1, 0, 0, 1> : (const void*)psp::k_psp_epoch<26, 1, 0, 0, 1>;
