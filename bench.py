@@ -159,6 +159,9 @@ def parse():
     ap.add_argument("--param-block", type=int, default=-1,
                     help="UWVK_OPT_PARAM_BLOCK: -1 the engine's default (on), 0 always the general 53-DOF kernel, "
                          "1 the parameter-decoupled kernel while the model-parameter block is uncoupled")
+    ap.add_argument("--pair", type=int, default=-1,
+                    help="UWVK_OPT_PAIR: -1 the engine's default, 1 the parameter-decoupled kernel with two "
+                         "instances per wave, 0 one per wave")
     ap.add_argument("--tail-slots", type=int, default=0,
                     help="UWVK_OPT_TAIL_SLOTS: 0 runtime occupancy, > 0 blocks per XCD, < 0 no tail spreading")
     ap.add_argument("--lds-pad", type=int, default=0,
@@ -545,6 +548,8 @@ def main():
         f.set_persist(a.persist)
     if a.param_block >= 0:
         f.set_param_block(a.param_block)
+    if a.pair >= 0:
+        f.set_pair(a.pair)
     if a.tail_chunks:
         f.set_tail_chunks(a.tail_chunks)
     if a.dense:
@@ -658,16 +663,19 @@ def main():
     evs = 0 if (f.epoch_qshape() != 1 or bool(((window & 0xC) != 0).any())) else 1
     sr = 0 if a.so3_left else 1
     persist = a.persist if a.persist >= 0 else 1  # the engine's default scheduler (UWVK_OPT_PERSIST)
+    pair_window = bool(f.pair_active()) if pd_window else False
     kfam = "k_psp_epoch_p" if persist else "k_psp_epoch"
     if a.dense:
         kname = "k_pose_epoch<%d>" % a.dof
+    elif pd_window and pair_window:  # two instances per wave (uwvk_psp_pair.hip)
+        kname = "k_psp_epoch_pair<%d, %d> (53-DOF state, parameter-decoupled, 2 instances per wave)" % (evs, sr)
     elif pd_window:  # 53-DOF state on the 26-DOF layout (the parameter-decoupled kernel)
         kname = "%s<26, %d, %d, %d, 1> (53-DOF state, parameter-decoupled)" % (kfam, f.epoch_qshape(), evs, sr)
     else:
         kname = "%s<%d, %d, %d, %d>" % (kfam, a.dof, f.epoch_qshape(), evs, sr)
     workload = "%s-dof%d-b%d%s%s%s%s" % (log_mode, a.dof, B, "-dense" if a.dense else "",
                                          "-lad" if getattr(a, "literal_apply_delta", False) else "", "" if sr else "-left",
-                                         "-pd" if pd_window else "")
+                                         ("-pair" if pair_window else "-pd") if pd_window else "")
     pmc = pmc_entry(workload, a.steps)
     cr = None if a.dense or launches != 1 else counter_roofline(pmc, B, a.steps, kernel_ms)
     traffic = pmc.get("bytes_per_launch") if pmc.get("epochs_per_launch") == a.steps and launches == 1 else None

@@ -72,6 +72,7 @@ struct uwvk_pose {
   // (checked on the host at init; cleared by the full BodyEfforts update and by
   // any literal-kernel step, which do not keep those zeros exact)
   int pd_opt = 1;  // UWVK_OPT_PARAM_BLOCK
+  int pair_opt = 0;  // UWVK_OPT_PAIR: the PD kernel with two instances per wave (uwvk_psp_pair.hip)
   bool pdec = false;
   double* d_Qp_pd = nullptr;  // the PD table: the 26-DOF subset's {A A, dt^2 Q}, then the parameters' diagonal
   int wait_bound = -1;   // UWVK_OPT_WAIT_BOUND: < 0 the planner's bound, else that many sleeps (tests)
@@ -719,10 +720,11 @@ static int tail_plan(uwvk_pose* h, int64_t n, int64_t s, int64_t count) {
 // units); the last r = chunks x slots instances run as epoch chunks, claimed
 // in chunk order (uwvk_psp_k.hip, k_psp_epoch_p).  UWVK_OPT_TAIL_SLOTS < 0
 // turns the chunks off, > 0 plans for that many slots per XCD.
-static hipError_t prepare_persist(uwvk_pose* h, EpochArgs& ea, int64_t& grid, int pd) {
-  const int64_t B = h->batch;
-  const int64_t s = h->tail_slots > 0 ? 8 * h->tail_slots : psp_epoch_slots(h->dof, h->device, true, pd);
-  const int64_t slots = psp_epoch_slots(h->dof, h->device, true, pd);
+// pair: the two-instances-per-wave kernel, whose units are pairs of instances
+static hipError_t prepare_persist(uwvk_pose* h, EpochArgs& ea, int64_t& grid, int pd, int pair = 0) {
+  const int64_t B = pair ? h->batch / 2 : h->batch;
+  const int64_t slots = pair ? psp_pair_slots(h->device) : psp_epoch_slots(h->dof, h->device, true, pd);
+  const int64_t s = h->tail_slots > 0 ? 8 * h->tail_slots : slots;
   if (slots <= 0) return hipErrorInvalidValue;
   ea.chunks = 1;
   ea.tail0 = B;
@@ -856,12 +858,22 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     // the parameter-decoupled kernel while the parameter block is decoupled
     // (every launch before the first full BodyEfforts epoch of an init's life)
     const int pd = use_pd(h) ? 1 : 0;
+    // the two-instances-per-wave form of it (UWVK_OPT_PAIR; persistent, even batch)
+    const int pair = pd && h->pair_opt && h->persist && h->batch % 2 == 0 && h->lds_pad == 0;
     PoseBufs bl = b;
     if (pd) bl.Qp = h->d_Qp_pd;
-    HIPCHK(prepare_tail(h, ea, grid, pd));
-    const hipError_t le = launch_psp_epoch(h->dof, h->stream, bl, sh, ea, grid, ev_any, h->lds_pad, pd);
+    hipError_t le;
+    if (pair) {
+      ea.chunks = 1;
+      ea.ticket = nullptr;
+      HIPCHK(prepare_persist(h, ea, grid, pd, 1));
+      le = launch_psp_epoch_pair(h->stream, bl, sh, ea, grid, ev_any);
+    } else {
+      HIPCHK(prepare_tail(h, ea, grid, pd));
+      le = launch_psp_epoch(h->dof, h->stream, bl, sh, ea, grid, ev_any, h->lds_pad, pd);
+    }
     if (le != hipSuccess) {
-      ::uwvk::note_hip_error((int)le, "launch_psp_epoch");
+      ::uwvk::note_hip_error((int)le, pair ? "launch_psp_epoch_pair" : "launch_psp_epoch");
       // a persistent launch that did not run took no tickets: restart the
       // counter from zero (stream-ordered, before any later launch)
       if (ea.ticket) {
@@ -954,6 +966,10 @@ uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value) {
     h->pd_opt = value ? 1 : 0;
     return UWVK_OK;
   }
+  if (option == UWVK_OPT_PAIR) {
+    h->pair_opt = value ? 1 : 0;
+    return UWVK_OK;
+  }
   return UWVK_EINVAL;
 }
 
@@ -966,6 +982,10 @@ int uwvk_pose_param_block(uwvk_pose* h) {
   if (!h) return 0;
   // q_simple is refreshed by upload_shared; evaluate it on the current Q
   return (h->pd_opt && h->pdec && h->dof == 53 && q_is_simple(h) && q_params_diag(h)) ? 1 : 0;
+}
+
+int uwvk_pose_pair_active(uwvk_pose* h) {
+  return (uwvk_pose_param_block(h) && h->pair_opt && h->persist && h->batch % 2 == 0 && h->lds_pad == 0) ? 1 : 0;
 }
 
 int uwvk_xcd_round_robin(int device) { return xcd_round_robin(device); }

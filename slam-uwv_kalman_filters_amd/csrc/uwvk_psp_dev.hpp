@@ -46,8 +46,27 @@
 // arms, their measurements and the last commit that still builds them are
 // listed in profiles/EXPERIMENTS.md ("r05: knob pruning").
 
+// PSP_PAIR (r06, the pair translation unit uwvk_psp_pair.hip): TWO instances
+// per wave, instance h = lane >> 5 on the 32 lanes [32 h, 32 h + 32), each with
+// its own PspSmem; every routine below then works on the instance-local lane
+// l & 31 (olane), builds its lane masks for the 32 local lanes of both halves
+// (lane_mask / LANE_IN), reads a value of local lane j of its own half with
+// hread (two readlanes and a select instead of one readlane), sums within a
+// half (wave_sum_dpp), and runs Sigma~ -= C~ K~^T as a lane-per-row FMA sweep
+// (rankm_rows: one MFMA tile spans all 64 lanes).  The code is compiled there
+// under PSP_NS = psp2; the single-instance kernels (uwvk_psp_k.hip) are
+// PSP_PAIR 0, namespace psp.
+#ifndef PSP_PAIR
+#define PSP_PAIR 0
+#endif
+#ifndef PSP_NS
+#define PSP_NS psp
+#endif
+
 namespace uwvk {
-namespace psp {
+namespace PSP_NS {
+
+constexpr int kLanes = PSP_PAIR ? 32 : 64;  // lanes per instance
 
 // (r05) a partial Cholesky is one serial chain (pivot readlane -> rsqrt ->
 // scale -> column broadcast -> update, per column): the wave in it runs at
@@ -65,7 +84,7 @@ UWVK_DEV void chain_prio_lo() { __builtin_amdgcn_s_setprio(0); }
 template <int DOF>
 struct PG {
   static constexpr int NP = DOF * (DOF + 1) / 2;     // packed entries
-  static constexpr int NSLOT = (NP + 63) / 64;       // flat slots per lane
+  static constexpr int NSLOT = (NP + kLanes - 1) / kLanes;  // flat slots per lane
   static constexpr int N = 2 * DOF + 1;              // ukfom sigma points
   static constexpr int KP = 15;                      // predict: nonlinear prefix (pos.x .. gyro bias)
   // staging area (L_a rows for the point lanes, the Cholesky column, C~ halves,
@@ -149,7 +168,7 @@ constexpr int kFlatMu = PG<DOF>::NP;  // mu's offset in flat()
 // multi-epoch loop recompute their lane-derived addresses instead of having
 // LICM hoist hundreds of them out of the epoch loop (register blow-up)
 UWVK_DEV int olane() {
-  int l = (int)threadIdx.x;
+  int l = PSP_PAIR ? ((int)threadIdx.x & 31) : (int)threadIdx.x;
   asm volatile("" : "+v"(l));
   return l;  // (restoring the range with l & 63 measured 1% slower)
 }
@@ -164,8 +183,13 @@ template <class F>
 UWVK_DEV constexpr unsigned long long lane_mask(F f) {
   unsigned long long m = 0;
   for (int i = 0; i < 64; i++)
-    if (f(i)) m |= 1ull << i;
+    if (f(PSP_PAIR ? (i & 31) : i)) m |= 1ull << i;  // pair: the local lane of either half
   return m;
+}
+// a mask built for local lanes 0..63 as the mask of both halves' local lanes
+// 0..31 (PSP_PAIR; the identity otherwise)
+UWVK_DEV constexpr unsigned long long rep_mask(unsigned long long m) {
+  return PSP_PAIR ? ((m & 0xFFFFFFFFull) | ((m & 0xFFFFFFFFull) << 32)) : m;
 }
 // A 64-bit mask whose value is a sign-extended 32-bit number but not an
 // inline constant (e.g. lanes >= 5: 0xffffffffffffffe0) was emitted by the
@@ -186,13 +210,29 @@ UWVK_DEV bool lane_const() {
   if constexpr (mask_needs_split(M)) return lane_in_split(M);
   else return __builtin_amdgcn_inverse_ballot_w64(M);
 }
-#define LANE_IF(l, expr)                                                                                     \
-  ({                                                                                                         \
-    constexpr unsigned long long m_ = ::uwvk::psp::lane_mask([](int l) constexpr { return (bool)(expr); }); \
-    ::uwvk::psp::lane_const<m_>();                                                                           \
+#define LANE_IF(l, expr)                                                                                        \
+  ({                                                                                                            \
+    constexpr unsigned long long m_ = ::uwvk::PSP_NS::lane_mask([](int l) constexpr { return (bool)(expr); }); \
+    ::uwvk::PSP_NS::lane_const<m_>();                                                                           \
   })
-#define LANE_IN(m) \
-  (::uwvk::psp::mask_needs_split(m) ? ::uwvk::psp::lane_in_split(m) : __builtin_amdgcn_inverse_ballot_w64(m))
+#define LANE_IN(m)                                                                     \
+  (::uwvk::PSP_NS::mask_needs_split(::uwvk::PSP_NS::rep_mask(m))                       \
+       ? ::uwvk::PSP_NS::lane_in_split(::uwvk::PSP_NS::rep_mask(m))                    \
+       : __builtin_amdgcn_inverse_ballot_w64(::uwvk::PSP_NS::rep_mask(m)))
+// the upper half of the wave (PSP_PAIR: instance 1)
+UWVK_DEV bool upper_half() { return lane_const<0xFFFFFFFF00000000ull>(); }
+// local lane j's value of the lane's own instance: readlane (a uniform SGPR
+// pair) with one instance per wave; PSP_PAIR: lane j or 32 + j by half
+UWVK_DEV double hread(double v, int j) {
+#if PSP_PAIR
+  const double a = readlane_d(v, j), b = readlane_d(v, 32 + j);
+  return upper_half() ? b : a;
+#else
+  return readlane_d(v, j);
+#endif
+}
+// global lane of local lane j of the lane's own instance (shuffles)
+UWVK_DEV int hlane(int j) { return PSP_PAIR ? j + ((int)threadIdx.x & 32) : j; }
 // lanes whose column j >= p, with j the lane clamped to the last DOF (jl) or its
 // A-coupled column (jcc: pos -> vel, vel -> acc, else jl), for pidx_sel_b
 UWVK_DEV constexpr int couple_c(int d) { return d < 3 ? d + 6 : (d >= 6 && d < 9 ? d + 3 : -1); }
@@ -250,11 +290,19 @@ UWVK_DEV double wave_sum_dpp(double v) {
   s = s + dpp_d<0x113, 0xf, 0xf>(v);          // row_shr:3
   s = s + dpp_d<0x114, 0xf, 0xe>(s);          // row_shr:4, banks 1-3
   s = s + dpp_d<0x118, 0xf, 0xc>(s);          // row_shr:8, banks 2-3
+#if PSP_PAIR
+  // within each 32-lane half: rows 0 / 2 end in lanes 15 / 47, rows 0+1 / 2+3 in 31 / 63
+  static_assert(NL <= 32, "pair: one instance per 32-lane half");
+  if constexpr (NL <= 16) return upper_half() ? readlane_d(s, 47) : readlane_d(s, 15);
+  s = s + dpp_d<0x142, 0xa, 0xf>(s);          // row_bcast:15, rows 1,3
+  return upper_half() ? readlane_d(s, 63) : readlane_d(s, 31);
+#else
   if constexpr (NL <= 16) return readlane_d(s, 15);
   s = s + dpp_d<0x142, 0xa, 0xf>(s);          // row_bcast:15, rows 1,3
   if constexpr (NL <= 32) return readlane_d(s, 31);
   s = s + dpp_d<0x143, 0xc, 0xf>(s);          // row_bcast:31, rows 2,3
   return readlane_d(s, 63);
+#endif
 }
 // ---------------------------------------------------------------------------
 // Small-angle SO3 exp / log (the same maps as so3_exp / so3_log, evaluated by
@@ -377,7 +425,7 @@ UWVK_DEV void lds_sums(const double (&v)[R], double* buf, int l, double (&out)[R
 #pragma unroll
     for (int k = 0; k + w < NL / 2; k += 2 * w) p[k] += p[k + w];
 #pragma unroll
-  for (int i = 0; i < R; i++) out[i] = readlane_d(p[0], i);
+  for (int i = 0; i < R; i++) out[i] = hread(p[0], i);
 }
 
 // phase boundary: the stamp of the diagnostic build, and (PSP_FAST & 4096) a
@@ -436,7 +484,7 @@ UWVK_DEV void pchol_step_lds(double (&a)[K], int r, bool& ok, double* col, doubl
     // registers), so its rsqrt need not wait for the column broadcast
     double pnext = 0.0, invn = 0.0;
     if constexpr (J + 1 < K) {
-      pnext = readlane_d(a[J + 1] - a[J] * a[J], J + 1);
+      pnext = hread(a[J + 1] - a[J] * a[J], J + 1);
     }
     if constexpr (J + 1 < K) {
       // col aliases the LAST staged row's not-yet-written slots J+1 .. K-1:
@@ -482,16 +530,17 @@ UWVK_DEV bool pchol(const double* S, int r, double (&a)[K], double dl, double* s
   // zero L[r][c] for r < c before it is read)
   const double* Sr = S + rr * (rr + 1) / 2;
 #pragma unroll
-  for (int c = 0; c < K; c++) a[c] = Sr[c] * (scaled_dof(c) ? dl * readlane_d(dl, c) : dl);
+  for (int c = 0; c < K; c++) a[c] = Sr[c] * (scaled_dof(c) ? dl * hread(dl, c) : dl);
   bool ok = true;
   // the staged-row slot of lane r is its rank among the staged rows (the row
   // list is ascending): the set bits of the constant row mask below the lane,
   // two v_mbcnt instead of a select per staged row
   static_assert(rows_ascending<RL>(), "RL::rows ascending");
-  constexpr unsigned long long rm = rows_mask<RL>();
-  const int q = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(rm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)rm, 0u));
+  constexpr unsigned long long rm = rep_mask(rows_mask<RL>());
+  int q = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(rm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)rm, 0u));
+  if constexpr (PSP_PAIR) q -= upper_half() ? __builtin_popcount((unsigned)rm) : 0;  // the lower half's rows
   static_assert(RL::NR >= 1 && STG_ROWS + RL::NR * K <= 115, "staging area (PG::STG)");
-  const double p0 = readlane_d(a[0], 0);
+  const double p0 = hread(a[0], 0);
   const double inv0 = rsqrt_f64(p0);
   double chk = fma(inv0, 0.0, 0.0);
   // the column buffer anywhere in the (not yet written) rows area; the rows are
@@ -645,7 +694,7 @@ UWVK_DEV LaneQ lane_q(const double* fq, int l) {
     if (l >= 1) q.q1 = f2[pidx(l, l - 1)].y;
     if (l >= 2) q.q2 = f2[pidx(l, l - 2)].y;
   }
-  if constexpr (PD) {
+  if constexpr (PD && !PSP_PAIR) {
     if (l >= kPdLane0 && l < kPdLane0 + kPdN) q.q0 = f2[PG<DOF>::NP + (l - kPdLane0)].y;
   }
   return q;
@@ -713,7 +762,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   constexpr double wc = 1.0 + 2.0 * (NW - K);
   double mq[4];
 #pragma unroll
-  for (int i = 0; i < 4; i++) mq[i] = readlane_d(o[i], 2 * K);
+  for (int i = 0; i < 4; i++) mq[i] = hread(o[i], 2 * K);
   {
     int it = 0;
     double nrm;
@@ -802,7 +851,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
     const double ar = 1.0 + dt * pc.nt_tan;  // proc_diag_sel's value (nt_tan = 0 off the scaled DOFs)
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-      const double yc = shfl_d(Y[i], src);
+      const double yc = shfl_d(Y[i], hlane(src));
       X[i] = 0.5 * (LANE_IF(l, proc_couple(l) >= 0) ? (ar * Y[i] + dt * yc) : ar * Y[i]);
     }
   }
@@ -850,7 +899,9 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   }
   // new time scale d' = A_ll d (A_ll = 1 on the unscaled DOFs)
   // (PD: the parameters' lanes too; pc.nt_tan holds their decay rate)
-  if (LANE_IF(l, (l < DOF && scaled_dof(l)) || (PD && l >= kPdLane0 && l < kPdLane0 + kPdN))) {
+  // (PSP_PAIR: the parameters are the pair kernel's own, uwvk_psp_pair.hip)
+  constexpr bool kPL = PD && !PSP_PAIR;
+  if (LANE_IF(l, (l < DOF && scaled_dof(l)) || (kPL && l >= kPdLane0 && l < kPdLane0 + kPdN))) {
     ds = aj * ds;
     double rc = __builtin_amdgcn_rcp(ds);  // d in (0, 1]: two Newton steps
     rc = fma(rc, fma(-ds, rc, 1.0), rc);
@@ -983,7 +1034,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       band(std::true_type{});
     else
       band(std::false_type{});
-    if constexpr (PD) {  // the parameters' diagonal: the band's k = 0 entry, as above
+    if constexpr (PD && !PSP_PAIR) {  // the parameters' diagonal: the band's k = 0 entry, as above
       if (LANE_IF(l, l >= kPdLane0 && l < kPdLane0 + kPdN)) {
         const int t = (l - kPdLane0) & 31;
         const double v = px[t];
@@ -992,7 +1043,7 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       }
     }
     for (int k = 3; k <= (QM == 1 ? 0 : bw); k++) {  // uniform bound: wide Q bands only
-      const double idj = shfl_d(ids, l - k >= 0 ? l - k : 0);
+      const double idj = shfl_d(ids, hlane(l - k >= 0 ? l - k : 0));
       const int j = l - k;
       if (l >= R0 && l < DOF && j >= R0) {
         const int e = pidx(l, j);
@@ -1009,14 +1060,14 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   double mv = proc_vect_lane(l & 63, flat(sm) + kFlatMu<DOF>, pc);
   asm volatile("" : "+v"(mv));
   [[maybe_unused]] double mvp = 0.0;  // PD: the parameters' means (lane 27 + t, px + 32)
-  if constexpr (PD) {
+  if constexpr (PD && !PSP_PAIR) {
     mvp = proc_vect_lane((l - kPdLane0) & 31, px + 32, pc);
     asm volatile("" : "+v"(mvp));
   }
   psync();
   if (LANE_IF(l, l < L::store && !(l >= 3 && l < 7))) sm.mu[l] = mv;
   if (LANE_IF(l, l < 4)) sm.mu[3 + l] = mq[l];
-  if constexpr (PD) {
+  if constexpr (PD && !PSP_PAIR) {
     if (LANE_IF(l, l >= kPdLane0 && l < kPdLane0 + kPdN)) px[32 + ((l - kPdLane0) & 31)] = mvp;
   }
   psync();
@@ -1050,12 +1101,12 @@ UWVK_DEV void psp_fold(PspSmem<DOF>& sm, double& ds, double& ids, double* px = n
 #pragma unroll
     for (int r = 0; r < FB; r++) {
       const int i = i0 + r;
-      const double di = readlane_d(ds, i < DOF ? i : DOF - 1);
+      const double di = hread(ds, i < DOF ? i : DOF - 1);
       double* dst = (i < DOF && l <= i) ? sm.S + e[r] : sm.stg + (l & 63);
       *dst = v[r] * (di * dl);
     }
   }
-  if constexpr (PD) {  // the parameters' diagonal: d_i d_i as for any (i, i)
+  if constexpr (PD && !PSP_PAIR) {  // the parameters' diagonal: d_i d_i as for any (i, i)
     if (LANE_IF(l, l >= kPdLane0 && l < kPdLane0 + kPdN)) {
       const int t = (l - kPdLane0) & 31;
       px[t] = px[t] * (ds * ds);
@@ -1202,6 +1253,7 @@ UWVK_DEV void lds_sums_chunked(const double (&v)[R], double* buf, int l, double 
   }
 }
 
+#if !PSP_PAIR
 // one row block I of rankm_mfma_o (tiles (I, J), J <= I), then block I + 1
 template <int DOF, int I, int NT>
 UWVK_DEV void rankm_block(double* S, const double (&Aop)[NT], const double (&Bop)[NT], int q, int c, int tq) {
@@ -1342,6 +1394,46 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
   rankm_block<DOF, 0, NT>(S, Aop, Bop, q, c, ((q * (q + 1)) >> 1) + O + c);
 }
 
+#else
+// PSP_PAIR: Sigma~ -= C~ K~^T as a lane-per-row sweep (one v_mfma_f64_16x16x4
+// tile spans all 64 lanes, i.e. both instances): lane r holds C~_r and K~_r;
+// K~ of every row is staged in the instance's stg and read back as broadcasts;
+// row r's entries go in blocks of RB columns, each block's loads (clamped to
+// the diagonal) before its stores; an entry past the diagonal is stored to a
+// throw-away staging slot (stg[80 + r]), so the diagonal is written once, by
+// its own column
+template <int DOF, int M>
+UWVK_DEV void rankm_rows(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
+  static_assert(DOF * M <= 80 && 80 + 32 <= PG<DOF>::STG, "K~ rows and the throw-away slots (PG::STG)");
+  constexpr int RB = 4;
+  if (l < DOF) {
+#pragma unroll
+    for (int k = 0; k < M; k++) stg[l * M + k] = Kt[k];
+  }
+  wsync();
+  const int lc = l < DOF ? l : DOF - 1;
+  const int b0 = (lc * (lc + 1)) >> 1;
+  double* const junk = stg + 80 + (l & 31);
+#pragma unroll
+  for (int j0 = 0; j0 < DOF; j0 += RB) {
+    double sv[RB];
+#pragma unroll
+    for (int u = 0; u < RB; u++)
+      if (j0 + u < DOF) sv[u] = S[b0 + (j0 + u <= lc ? j0 + u : lc)];
+#pragma unroll
+    for (int u = 0; u < RB; u++) {
+      if (j0 + u >= DOF) continue;
+      double s2 = sv[u];
+#pragma unroll
+      for (int k = 0; k < M; k++) s2 = fma(-Ct[k], stg[(j0 + u) * M + k], s2);
+      double* dst = (l < DOF && j0 + u <= l) ? S + b0 + j0 + u : junk;
+      *dst = s2;
+    }
+  }
+  wsync();  // stg is rewritten next
+}
+#endif  // !PSP_PAIR
+
 // acc + h x for an entry h of a measurement Jacobian: the structural zeros of
 // H (e.g. the identity block of the acceleration model's bias columns) are
 // compile-time constants after inlining, and their terms are dropped.  For
@@ -1366,7 +1458,7 @@ UWVK_DEV double hfma(double h, double x, double acc) {
 template <int DOF, int SR>
 UWVK_DEV void psp_apply_delta(PspSmem<DOF>& sm, double dl, int l) {
   using L = Lay<DOF>;
-  const double dv[3] = {readlane_d(dl, 3), readlane_d(dl, 4), readlane_d(dl, 5)};
+  const double dv[3] = {hread(dl, 3), hread(dl, 4), hread(dl, 5)};
   double R[9], eq[4];  // exp(delta_ori) once: T's rotation and the mean's [+]
   so3_exp_psp(dv, eq);
   {
@@ -1434,7 +1526,6 @@ template <int DOF, int SR, class HM, int NW = DOF>
 UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const double (&Rm)[HM::M * HM::M], int gate,
                          const HM& hm, bool* ok, double ds, double ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
-  using G = PG<DOF>;
   constexpr int M = HM::M, K = HM::K, NC = HM::NC, KA = K > 0 ? K : 1, NCA = NC > 0 ? NC : 1;
   int l = olane();  // re-laundered per phase (PSP_PHASE)
   double a[KA];
@@ -1454,7 +1545,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   }
   double zc[M], zb[M], e[M];
 #pragma unroll
-  for (int i = 0; i < M; i++) zc[i] = readlane_d(zp[i], 2 * K);
+  for (int i = 0; i < M; i++) zc[i] = hread(zp[i], 2 * K);
   constexpr double wc = 1.0 + 2.0 * (NW - K);
   double S[M * M];
   // H and P first: P reads the staged rows, after which stg holds the
@@ -1531,7 +1622,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
 #pragma unroll
   for (int t = 0; t < NC; t++) {
     double s = sm.S[pidx_sel_b(HM::cols[t], rl, Trl, LANE_IN(col_ge_mask<DOF>(HM::cols[t], false)))];
-    if (scaled_dof(HM::cols[t])) s = s * readlane_d(ds, HM::cols[t]);
+    if (scaled_dof(HM::cols[t])) s = s * hread(ds, HM::cols[t]);
 #pragma unroll
     for (int i = 0; i < M; i++) Gr[i] = hfma(Hs[i][t], s, Gr[i]);
   }
@@ -1595,7 +1686,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     for (int j = 0; j <= i; j++) {
       double hg = 0.0;
 #pragma unroll
-      for (int t = 0; t < NC; t++) hg = hfma(Hs[i][t], readlane_d(Gl[j], HM::cols[t]), hg);
+      for (int t = 0; t < NC; t++) hg = hfma(Hs[i][t], hread(Gl[j], HM::cols[t]), hg);
       const double s = S[i * M + j] + hg;
       S[i * M + j] = s + Rm[i * M + j];
       if (j != i) S[j * M + i] = s + Rm[j * M + i];
@@ -1639,6 +1730,9 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     Kt[i] = Kg[i] * ids;
   }
   psync();
+#if PSP_PAIR
+  rankm_rows<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
+#else
   if constexpr (M <= 3) {
     rankm_mfma_o<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
   } else {  // rank M > 3 (constrainVelocity, M = 6): two passes of rank 3 and M - 3
@@ -1651,6 +1745,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     psync();
     rankm_mfma_o<DOF, M - 3>(sm.S, sm.stg, c1, k1, l);
   }
+#endif
   psync();
   PSP_PHASE(34);
   psp_apply_delta<DOF, SR>(sm, dl, l);
@@ -1659,6 +1754,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
 }
 
 
+#if !PSP_PAIR  // (the pair kernel runs no BodyEfforts update)
 // ---------------------------------------------------------------------------
 // measurementEfforts (PoseUKF.cpp:153-196), the full BodyEfforts update, in PSP
 // form on one wave per instance (r05; the literal two-wave kernel stays on
@@ -2046,5 +2142,7 @@ UWVK_DEV bool psp_update_eff(PspSmem<DOF>& sm, const double* sig_hbm, const HM& 
   return true;
 }
 
-}  // namespace psp
+#endif  // !PSP_PAIR
+
+}  // namespace PSP_NS
 }  // namespace uwvk

@@ -43,7 +43,7 @@ SYMBOLS = [
     "uwvk_ipose_create", "uwvk_ipose_destroy", "uwvk_ipose_stream", "uwvk_ipose_init", "uwvk_ipose_set_option",
     "uwvk_ipose_set_pose_reference", "uwvk_ipose_predict", "uwvk_ipose_update_visual",
     "uwvk_ipose_get_corrected_pose", "uwvk_ipose_get_state", "uwvk_ipose_get_status",
-    "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots", "uwvk_pose_epoch_qshape", "uwvk_pose_param_block", "uwvk_pose_timer_mark", "uwvk_pose_timer_elapsed",
+    "uwvk_pose_tail_chunks", "uwvk_pose_resident_slots", "uwvk_pose_epoch_qshape", "uwvk_pose_param_block", "uwvk_pose_pair_active", "uwvk_pose_timer_mark", "uwvk_pose_timer_elapsed",
     "uwvk_xcd_round_robin", "uwvk_synth_normal", "uwvk_synth_normal_at",
 ]
 
@@ -90,6 +90,8 @@ def lib(path=None):
         L.uwvk_pose_epoch_qshape.restype = C.c_int
         L.uwvk_pose_param_block.argtypes = [C.c_void_p]
         L.uwvk_pose_param_block.restype = C.c_int
+        L.uwvk_pose_pair_active.argtypes = [C.c_void_p]
+        L.uwvk_pose_pair_active.restype = C.c_int
         L.uwvk_pose_resident_slots.argtypes = [C.c_int, C.c_int]
         L.uwvk_pose_resident_slots.restype = C.c_int64
         L.uwvk_memcpy_h2d.argtypes = [VP, VP, C.c_size_t]
@@ -214,6 +216,15 @@ class PoseUKFBatch:
         """UWVK_OPT_PARAM_BLOCK: run_log's launches on the parameter-decoupled
         kernel while the model-parameter block is uncoupled (default on)."""
         _chk(self.L.uwvk_pose_set_option(self.h, 9, int(bool(on))), "set_option")
+
+    def set_pair(self, on=True):
+        """UWVK_OPT_PAIR: the parameter-decoupled kernel with two instances per
+        wave (persistent scheduler, even batch)."""
+        _chk(self.L.uwvk_pose_set_option(self.h, 10, int(bool(on))), "set_option")
+
+    def pair_active(self):
+        """1 when the next run_log launch runs the two-instances-per-wave kernel."""
+        return int(self.L.uwvk_pose_pair_active(self.h))
 
     def param_block(self):
         """1 when the next run_log launch runs the parameter-decoupled kernel."""

@@ -140,3 +140,80 @@ def test_pd_eligibility(eng):
     l26 = synth.make_pose_log(B, 10, "C3", dof=26)
     g26.init_from_config(l26["pos0"], l26["pos_cov"], l26["rot0"], l26["rot_cov"], cfg, uwv)
     assert g26.param_block() == 0
+
+
+# ---- the two-instances-per-wave form (UWVK_OPT_PAIR, csrc/uwvk_psp_pair.hip) ----
+def _run_pair(eng, log, cfg, uwv, pair, pieces, slots=-1, chunks=0, pd=True):
+    from uwvk import abi
+    B = log["gyro"].shape[1]
+    g = eng.PoseUKFBatch(B, 53)
+    g.set_param_block(pd)
+    g.set_pair(pair)
+    g.set_tail_slots(slots)
+    if chunks:
+        g.set_tail_chunks(chunks)
+    g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+    g.set_process_noise_from_config(cfg, 1e-3)
+    dlog = g.upload_log(log)
+    acc = eng.DeviceBuffer(np.zeros((B, 4), np.uint32))
+    for a, n in pieces:
+        g.run_log(dlog, a, n, accept_counts=acc)
+    x, P = g.get_state()
+    return x, P, acc.read(np.uint32, (B, 4)), g.get_status(), g.get_rotation_rate()
+
+
+@pytest.mark.parametrize("mode,E,pieces", [("C3", 300, [(0, 300)]), ("C3", 1100, [(0, 600), (600, 500)]),
+                                           ("C4", 800, [(0, 450), (450, 350)])])
+def test_pair_matches_single(eng, mode, E, pieces):
+    """The pair kernel against the one-instance PD kernel (C4: pressure, ADCP
+    and the efforts epochs, after which both run the general kernel): the same
+    filter to rounding (the rank-M update's order), gate decisions bitwise."""
+    from helpers import cov_err, state_err
+    from uwvk import synth
+    B = 96
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    extra = dict(dropout_on=0.3, dropout_off=0.1, adcp_every=100) if mode == "C4" else {}
+    log = synth.make_pose_log(B, E, mode, **extra)
+    ref = _run_pair(eng, log, cfg, uwv, False, pieces)
+    got = _run_pair(eng, log, cfg, uwv, True, pieces)
+    np.testing.assert_array_equal(got[2], ref[2])
+    np.testing.assert_array_equal(got[3], ref[3])
+    np.testing.assert_array_equal(got[4], ref[4])
+    assert state_err(got[0], ref[0], ref[1], 53).max() < 1e-9
+    assert cov_err(got[1], ref[1]).max() < 1e-9
+
+
+@pytest.mark.parametrize("chunks", [2, 5])
+def test_pair_tail_chunks_bitwise(eng, chunks):
+    """Tail chunks of pair units handed on (Sigma~ and the time scale unfolded):
+    bitwise the unchunked pair run."""
+    from uwvk import synth
+    B, E = 96, 120
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(B, E, "C3")
+    ref = _run_pair(eng, log, cfg, uwv, True, [(0, 70), (70, 50)])
+    got = _run_pair(eng, log, cfg, uwv, True, [(0, 70), (70, 50)], slots=1, chunks=chunks)
+    for name, a, b in zip(NAMES, got, ref):
+        np.testing.assert_array_equal(a, b, err_msg=name)
+    assert not got[3].any()
+
+
+def test_pair_matches_oracle(eng):
+    from helpers import cov_err, init_both, state_err
+    import oracle_ctypes as orc
+    from uwvk import synth
+    B, E = 6, 400
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+    log = synth.make_pose_log(B, E, "C3")
+    o = orc.OraclePoseBatch(B, 53)
+    g = eng.PoseUKFBatch(B, 53)
+    g.set_pair(True)
+    init_both(o, g, cfg, uwv, log)
+    co = o.run_log(log)
+    dlog = g.upload_log(log)
+    acc = eng.DeviceBuffer(np.zeros((B, 4), np.uint32))
+    g.run_log(dlog, accept_counts=acc)
+    np.testing.assert_array_equal(co, acc.read(np.uint32, (B, 4)))
+    xo, Po = o.get_state()
+    xg, Pg = g.get_state()
+    assert state_err(xg, xo, Po, 53).max() < 1e-7 and cov_err(Pg, Po).max() < 1e-7
