@@ -493,7 +493,9 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
 #define UWVK_OPT_PARAM_BLOCK 9
 /* UWVK_OPT_PAIR (r06): 1 runs the parameter-decoupled kernel with two
  *   instances per wave (each on 32 lanes; uwvk_psp_pair.hip), when that kernel
- *   applies, the scheduler is persistent and the batch is even.  The results
+ *   applies, the scheduler is persistent, the batch is even and the launch's
+ *   epochs hold IMU and DVL updates only (the pressure update's 39 sigma points
+ *   do not fit a half-wave).  The results
  *   agree with the one-instance kernel to rounding (the rank-M update sums in
  *   another order).  0: one instance per wave. */
 #define UWVK_OPT_PAIR 10
@@ -514,8 +516,8 @@ int uwvk_pose_epoch_qshape(const uwvk_pose* h);
 /* Host-only query: 1 when the next run_log PSP launch runs the
  * parameter-decoupled kernel (UWVK_OPT_PARAM_BLOCK), else 0. */
 int uwvk_pose_param_block(uwvk_pose* h);
-/* Host-only query: 1 when that launch runs the two-instances-per-wave form
- * (UWVK_OPT_PAIR). */
+/* Host-only query: 1 when that launch, if its epochs hold no pressure / ADCP
+ * update, runs the two-instances-per-wave form (UWVK_OPT_PAIR). */
 int uwvk_pose_pair_active(uwvk_pose* h);
 /* 1 when a probe grid on device showed round-robin workgroup placement over 8
  * XCCs (block b on the XCC of block b % 8, read from the hardware XCC_ID

@@ -72,7 +72,7 @@ struct uwvk_pose {
   // (checked on the host at init; cleared by the full BodyEfforts update and by
   // any literal-kernel step, which do not keep those zeros exact)
   int pd_opt = 1;  // UWVK_OPT_PARAM_BLOCK
-  int pair_opt = 0;  // UWVK_OPT_PAIR: the PD kernel with two instances per wave (uwvk_psp_pair.hip)
+  int pair_opt = 1;  // UWVK_OPT_PAIR (default on): the PD kernel with two instances per wave (uwvk_psp_pair.hip)
   bool pdec = false;
   double* d_Qp_pd = nullptr;  // the PD table: the 26-DOF subset's {A A, dt^2 Q}, then the parameters' diagonal
   int wait_bound = -1;   // UWVK_OPT_WAIT_BOUND: < 0 the planner's bound, else that many sleeps (tests)
@@ -859,7 +859,9 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     // (every launch before the first full BodyEfforts epoch of an init's life)
     const int pd = use_pd(h) ? 1 : 0;
     // the two-instances-per-wave form of it (UWVK_OPT_PAIR; persistent, even batch)
-    const int pair = pd && h->pair_opt && h->persist && h->batch % 2 == 0 && h->lds_pad == 0;
+    // (IMU + DVL launches: the pressure update's 39 sigma points do not fit a half-wave)
+    const int pair = pd && h->pair_opt && h->persist && h->batch % 2 == 0 && h->lds_pad == 0 &&
+                     !(ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP));
     PoseBufs bl = b;
     if (pd) bl.Qp = h->d_Qp_pd;
     hipError_t le;

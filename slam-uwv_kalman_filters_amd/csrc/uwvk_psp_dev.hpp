@@ -1527,6 +1527,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
                          const HM& hm, bool* ok, double ds, double ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   constexpr int M = HM::M, K = HM::K, NC = HM::NC, KA = K > 0 ? K : 1, NCA = NC > 0 ? NC : 1;
+  static_assert(!PSP_PAIR || 2 * K + 1 <= 32, "pair: the 2k + 1 sigma points of an update fit 32 lanes");
   int l = olane();  // re-laundered per phase (PSP_PHASE)
   double a[KA];
   bool cok = true;

@@ -18,7 +18,7 @@
 #define PSP_NS psp2
 // waves per SIMD of the pair kernel (PSP_PAIR_WAVES=... for occupancy A/Bs)
 #ifndef PSP_PAIR_WAVES
-#define PSP_PAIR_WAVES 4
+#define PSP_PAIR_WAVES 3
 #endif
 #include <algorithm>
 #include <atomic>
@@ -210,7 +210,11 @@ UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
 // The pair kernel's persistent work loop: block b runs pair unit b first, then
 // takes units from the ticket counter (k_psp_epoch_p's scheme); unit u is
 // instances 2u (lanes 0..31) and 2u + 1 (lanes 32..63).
-template <int EVS, int SR>
+// IMU + DVL launches only (EpochArgs flags host-checked): the pressure update's
+// nonlinear prefix is k = 19 (pos .. gravity; PoseUKF.cpp:107-115), 39 sigma
+// points, more than a half-wave holds; a launch with pressure or ADCP epochs
+// runs the one-instance PD kernel
+template <int SR>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PSP_PAIR_WAVES, PSP_PAIR_WAVES)))
 void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmemPD<26> smx[2];
@@ -238,8 +242,6 @@ void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
     const int64_t e_begin = tu.e0, e_end = tu.e1;
     bool ok = true, nan = false;
     uint32_t cnt[4] = {0, 0, 0, 0};
-    MeasArgs ma{};
-    ma.v3[0] = ea.p_sens[0]; ma.v3[1] = ea.p_sens[1]; ma.v3[2] = ea.p_sens[2];
     ProcCtx pc;
     for (int k = 0; k < 3; k++) pc.w[k] = b.rot[inst * 3 + k];
     {
@@ -306,33 +308,6 @@ void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
           nan = true;
         }
       }
-      if constexpr (EVS == 0) {
-        if (fl & UWVK_EV_PRESSURE) {
-          const double* zp = ea.pressure + (int64_t)ea.p_index[e] * B + inst;
-          if (finite_n(zp, 1)) {
-            double z[1], R[1];
-            copy_zr<1>(zp, &ea.p_cov, z, R);
-            PPressure<26> hp;
-            hp.h.s[0] = ma.v3[0]; hp.h.s[1] = ma.v3[1]; hp.h.s[2] = ma.v3[2];
-            hp.h.patm = sh.p.atmospheric_pressure;
-            cnt[1] += psp_update<26, SR, PPressure<26>, NW>(sm, z, R, 0, hp, &sok, ds, ids);
-            ok = ok && sok;
-          } else {
-            nan = true;
-          }
-        }
-        if (fl & UWVK_EV_ADCP) {
-          for (int c = 0; c < ea.cells; c++) {
-            const double* zp = ea.adcp + (((int64_t)ea.a_index[e] * ea.cells + c) * B + inst) * 2;
-            if (!finite_n(zp, 2)) { nan = true; continue; }
-            double zz[2] = {zp[0], zp[1]}, R[4] = {ea.adcp_cov[0], ea.adcp_cov[1], ea.adcp_cov[2], ea.adcp_cov[3]};
-            PWater<26> hw;
-            hw.cw = ea.cw[c];
-            cnt[2] += psp_update<26, SR, PWater<26>, NW>(sm, zz, R, 1, hw, &sok, ds, ids);
-            ok = ok && sok;
-          }
-        }
-      }
     }
     if (l == 0) {  // local lane 0 of each half: its instance's bookkeeping
       const uint32_t bits = (ok ? 0u : UWVK_ST_NOTPD) | (nan ? UWVK_ST_NAN : 0u);
@@ -367,10 +342,8 @@ template <int SR>
 static hipError_t launch_pair_sr(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
                                  int64_t grid, uint32_t ev_any) {
   const dim3 g((unsigned)grid), t(64);
-  if (ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP))
-    hipLaunchKernelGGL((psp2::k_psp_epoch_pair<0, SR>), g, t, 0, st, b, sh, ea);
-  else
-    hipLaunchKernelGGL((psp2::k_psp_epoch_pair<1, SR>), g, t, 0, st, b, sh, ea);
+  if (ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP)) return hipErrorInvalidValue;  // (pair_ok excludes them)
+  hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR>), g, t, 0, st, b, sh, ea);
   return hipGetLastError();
 }
 
@@ -382,7 +355,7 @@ hipError_t launch_psp_epoch_pair(hipStream_t st, const PoseBufs& b, const PoseSh
 
 int64_t psp_pair_slots(int device) {
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)psp2::k_psp_epoch_pair<1, 1>, 64, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)psp2::k_psp_epoch_pair<1>, 64, 0) !=
           hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return 0;

@@ -28,6 +28,7 @@ def _run(eng, log, cfg, uwv, pd, pieces, slots=-1, persist=True, init="config", 
     B = log["gyro"].shape[1]
     g = eng.PoseUKFBatch(B, 53)
     g.set_param_block(pd)
+    g.set_pair(False)  # the one-instance PD kernel (the pair form is not bitwise)
     g.set_tail_slots(slots)
     g.set_persist(persist)
     if init == "config":

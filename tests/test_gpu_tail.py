@@ -24,10 +24,11 @@ def eng():
     return engine
 
 
-def _run(eng, B, dof, log, cfg, uwv, slots, pieces, persist=False, force=0):
+def _run(eng, B, dof, log, cfg, uwv, slots, pieces, persist=False, force=0, pair=False):
     g = eng.PoseUKFBatch(B, dof)
     g.set_tail_slots(slots)
     g.set_persist(persist)
+    g.set_pair(pair)  # the pair form (default on, persistent only) is not bitwise the one-instance kernel
     if force:
         g.set_tail_chunks(force)
     g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
@@ -127,18 +128,21 @@ def test_every_chunk_count_at_full_batch(eng, B):
 # Persistent scheduling (UWVK_OPT_PERSIST): resident workgroups take units from
 # a ticket counter; chunk k of a tail instance may run on any XCD after chunk
 # k - 1.  Bitwise the one-workgroup-per-instance run, with and without chunks,
-# on every chunk count the planner can be forced to.
+# on every chunk count the planner can be forced to.  pair=True: the
+# two-instances-per-wave form (persistent only), its chunked runs bitwise its
+# unchunked one (the C4 and 26-DOF cases run no pair launch: the selection).
+@pytest.mark.parametrize("pair", [False, True])
 @pytest.mark.parametrize("dof,mode,E,slots,n,pieces", CASES)
-def test_persist_bitwise(eng, dof, mode, E, slots, n, pieces):
+def test_persist_bitwise(eng, dof, mode, E, slots, n, pieces, pair):
     from uwvk import synth
     B = 8 * n
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     extra = dict(dropout_on=0.1, dropout_off=0.05) if mode == "C4" else {}
     log = synth.make_pose_log(B, E, mode, dof=dof, **extra)
-    ref = _run(eng, B, dof, log, cfg, uwv, -1, pieces)
+    ref = _run(eng, B, dof, log, cfg, uwv, -1, pieces, persist=pair, pair=pair)
     names = ("state", "covariance", "accept counts", "status", "rotation rate")
     for sl in (-1, slots):  # no chunks; the planner's chunks for `slots` per XCD
-        got = _run(eng, B, dof, log, cfg, uwv, sl, pieces, persist=True)
+        got = _run(eng, B, dof, log, cfg, uwv, sl, pieces, persist=True, pair=pair)
         for name, a, b in zip(names, got, ref):
             np.testing.assert_array_equal(a, b, err_msg="%s (slots %d)" % (name, sl))
 
@@ -169,8 +173,8 @@ def test_persist_default_plan_repeat(eng):
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("persist", [False, True])
-def test_handoff_timeout_is_an_error(eng, persist):
+@pytest.mark.parametrize("persist,pair", [(False, False), (True, False), (True, True)])
+def test_handoff_timeout_is_an_error(eng, persist, pair):
     """ABI 3: a timed-out tail-chunk hand-off makes
     uwvk_pose_run_log return UWVK_ESCHEDULE (not only a status bit), the
     chunks after it flag their instances UWVK_ST_SCHEDULE, every other instance
@@ -183,10 +187,11 @@ def test_handoff_timeout_is_an_error(eng, persist):
     assert eng.lib().uwvk_pose_tail_chunks(B, 8 * slots, E) > 1  # the persistent plan
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     log = synth.make_pose_log(B, E, "C3")
-    ref = _run(eng, B, 53, log, cfg, uwv, -1, [(0, E)])
+    ref = _run(eng, B, 53, log, cfg, uwv, -1, [(0, E)], persist=pair, pair=pair)
     g = eng.PoseUKFBatch(B, 53)
     g.set_tail_slots(slots)
     g.set_persist(persist)
+    g.set_pair(pair)
     g.set_wait_bound(0)  # every chunk k > 0 gives up at once
     g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
     g.set_process_noise_from_config(cfg, 1e-3)
