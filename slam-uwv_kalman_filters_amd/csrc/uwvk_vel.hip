@@ -768,8 +768,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(VG / 16, VG 
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + i) * 3;
       const double zz[3] = {z[0], z[1], z[2]};
+#ifndef VEL_KARG_IDX
+#define VEL_KARG_IDX 1
+#endif
+#if VEL_KARG_IDX
+      // R by scalar loads in the branch, not held in SGPRs across the loop: a
+      // laundered zero index keeps the loads here (r06: the address of the
+      // by-value argument, laundered instead, made a private copy of the whole
+      // VelEpochArgs, 168 B/lane of scratch read in the loop)
+      int z0 = 0;
+      asm volatile("" : "+s"(z0));
+      double Rd[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) Rd[k] = ea.dvl_cov[k + z0];
+#else
       const double* Rd = ea.dvl_cov;
       asm volatile("" : "+s"(Rd));  // R loaded in the branch, not held in SGPRs across the loop
+#endif
       ok = vg_update<3, 0>(mu, S, zz, Rd, g) && ok;
     }
     if (fl & UWVK_EV_PRESSURE) {

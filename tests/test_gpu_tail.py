@@ -181,10 +181,11 @@ def test_handoff_timeout_is_an_error(eng, persist, pair):
     is bitwise the unspread run, and the handle's fault word is cleared: the
     next launch without forced timeouts returns OK again."""
     from uwvk import synth
-    n, slots, E = 12, 3, 20
+    n, slots, E = 12, (2 if pair else 3), 20
     B = 8 * n
     assert eng.lib().uwvk_pose_tail_chunks(n, slots, E) > 1
     assert eng.lib().uwvk_pose_tail_chunks(B, 8 * slots, E) > 1  # the persistent plan
+    assert not pair or eng.lib().uwvk_pose_tail_chunks(B // 2, 8 * slots, E) > 1  # the pair units' plan
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     log = synth.make_pose_log(B, E, "C3")
     ref = _run(eng, B, 53, log, cfg, uwv, -1, [(0, E)], persist=pair, pair=pair)
