@@ -1402,63 +1402,10 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
 // the diagonal) before its stores; an entry past the diagonal is stored to a
 // throw-away staging slot (stg[80 + r]), so the diagonal is written once, by
 // its own column
-// PSP_FUSE_AD (r06): the rows >= 6 of apply_delta's T
-// Sigma T^T (their columns 3..5 times R^T) applied in the same sweep, on the
-// updated values before their store: the columns go in blocks {0..2}, {3..5},
-// then RB from 6.  The arithmetic is the unfused pair's (the same values and
-// products), so the result is bitwise the same; psp_apply_delta<.., AD = 1>
-// then handles only the entries (3..5, 0..2) and the ori x ori block.
-#ifndef PSP_FUSE_AD
-#define PSP_FUSE_AD 1
-#endif
-template <int DOF, int M, int J0, int W, bool AD>
-UWVK_DEV void rankm_rows_blk(double* S, const double* stg, const double (&Ct)[M], int l, int lc, int b0,
-                             double* junk, const double* R) {
-  double sv[W];
-#pragma unroll
-  for (int u = 0; u < W; u++)
-    if (J0 + u < DOF) sv[u] = S[b0 + (J0 + u <= lc ? J0 + u : lc)];
-  double nv[W];
-#pragma unroll
-  for (int u = 0; u < W; u++) {
-    if (J0 + u >= DOF) continue;
-    double s2 = sv[u];
-#pragma unroll
-    for (int k = 0; k < M; k++) s2 = fma(-Ct[k], stg[(J0 + u) * M + k], s2);
-    nv[u] = s2;
-  }
-  if constexpr (AD && J0 == 3) {
-    static_assert(W == 3, "the orientation block");
-    // row r >= 6: T's columns (psp_apply_delta's n3), stored instead
-    const bool mix = LANE_IF(l, l >= 6);
-    double n3[3];
-#pragma unroll
-    for (int i = 0; i < 3; i++) n3[i] = R[i * 3] * nv[0] + R[i * 3 + 1] * nv[1] + R[i * 3 + 2] * nv[2];
-#pragma unroll
-    for (int i = 0; i < 3; i++) nv[i] = mix ? n3[i] : nv[i];
-  }
-#pragma unroll
-  for (int u = 0; u < W; u++) {
-    if (J0 + u >= DOF) continue;
-    double* dst = (l < DOF && J0 + u <= l) ? S + b0 + J0 + u : junk;
-    *dst = nv[u];
-  }
-}
-
-template <int DOF, int M, int J0, bool AD>
-UWVK_DEV void rankm_rows_from(double* S, const double* stg, const double (&Ct)[M], int l, int lc, int b0,
-                              double* junk, const double* R) {
-  if constexpr (J0 < DOF) {
-    constexpr int W = AD ? (J0 < 6 ? 3 : 4) : 4;
-    rankm_rows_blk<DOF, M, J0, W, AD>(S, stg, Ct, l, lc, b0, junk, R);
-    rankm_rows_from<DOF, M, J0 + W, AD>(S, stg, Ct, l, lc, b0, junk, R);
-  }
-}
-
-template <int DOF, int M, bool AD = false>
-UWVK_DEV void rankm_rows(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l,
-                         const double* R = nullptr) {
+template <int DOF, int M>
+UWVK_DEV void rankm_rows(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
   static_assert(DOF * M <= 80 && 80 + 32 <= PG<DOF>::STG, "K~ rows and the throw-away slots (PG::STG)");
+  constexpr int RB = 4;
   if (l < DOF) {
 #pragma unroll
     for (int k = 0; k < M; k++) stg[l * M + k] = Kt[k];
@@ -1467,7 +1414,22 @@ UWVK_DEV void rankm_rows(double* S, double* stg, const double (&Ct)[M], const do
   const int lc = l < DOF ? l : DOF - 1;
   const int b0 = (lc * (lc + 1)) >> 1;
   double* const junk = stg + 80 + (l & 31);
-  rankm_rows_from<DOF, M, 0, AD>(S, stg, Ct, l, lc, b0, junk, R);
+#pragma unroll
+  for (int j0 = 0; j0 < DOF; j0 += RB) {
+    double sv[RB];
+#pragma unroll
+    for (int u = 0; u < RB; u++)
+      if (j0 + u < DOF) sv[u] = S[b0 + (j0 + u <= lc ? j0 + u : lc)];
+#pragma unroll
+    for (int u = 0; u < RB; u++) {
+      if (j0 + u >= DOF) continue;
+      double s2 = sv[u];
+#pragma unroll
+      for (int k = 0; k < M; k++) s2 = fma(-Ct[k], stg[(j0 + u) * M + k], s2);
+      double* dst = (l < DOF && j0 + u <= l) ? S + b0 + j0 + u : junk;
+      *dst = s2;
+    }
+  }
   wsync();  // stg is rewritten next
 }
 #endif  // !PSP_PAIR
@@ -1493,30 +1455,15 @@ UWVK_DEV double hfma(double h, double x, double acc) {
 // T = R(exp d) (SR = 0) or R(exp d)^T = R(exp(d)^-1) (SR = 1); the vector
 // deviations are L_j unchanged.  The weights (1/2 over the 2n points) give
 // T L L^T T^T exactly.
-// exp(delta_ori) once: T's rotation R and the mean's [+] quaternion eq
-template <int SR>
-UWVK_DEV void apply_delta_rot(double dl, double (&R)[9], double (&eq)[4]) {
-  const double dv[3] = {hread(dl, 3), hread(dl, 4), hread(dl, 5)};
-  so3_exp_psp(dv, eq);
-  const double tq[4] = {eq[0], SR ? -eq[1] : eq[1], SR ? -eq[2] : eq[2], SR ? -eq[3] : eq[3]};
-  qmatrix(tq, R);
-}
-
-// AD = 1: the rows >= 6 were transformed by the fused rank-M sweep
-// (rankm_rows<.., AD>, R and eq from apply_delta_rot before it); only the
-// entries (3..5, 0..2) (lanes 0..2) and the block remain
-template <int DOF, int SR, bool AD = false>
-UWVK_DEV void psp_apply_delta(PspSmem<DOF>& sm, double dl, int l, const double* Rin = nullptr,
-                              const double* eqin = nullptr) {
+template <int DOF, int SR>
+UWVK_DEV void psp_apply_delta(PspSmem<DOF>& sm, double dl, int l) {
   using L = Lay<DOF>;
-  double R[9], eq[4];
-  if constexpr (AD) {
-#pragma unroll
-    for (int i = 0; i < 9; i++) R[i] = Rin[i];
-#pragma unroll
-    for (int i = 0; i < 4; i++) eq[i] = eqin[i];
-  } else {
-    apply_delta_rot<SR>(dl, R, eq);
+  const double dv[3] = {hread(dl, 3), hread(dl, 4), hread(dl, 5)};
+  double R[9], eq[4];  // exp(delta_ori) once: T's rotation and the mean's [+]
+  so3_exp_psp(dv, eq);
+  {
+    const double tq[4] = {eq[0], SR ? -eq[1] : eq[1], SR ? -eq[2] : eq[2], SR ? -eq[3] : eq[3]};
+    qmatrix(tq, R);
   }
   // (r04) rows 3..5 of every column j outside the block, and the ori x ori
   // block R B R^T: every lane loads and computes (its column clamped into
@@ -1527,10 +1474,9 @@ UWVK_DEV void psp_apply_delta(PspSmem<DOF>& sm, double dl, int l, const double* 
   {
     const int lc = l < DOF ? l : DOF - 1;
     const int Tl = (lc * (lc + 1)) >> 1;
-    // (AD: only lanes 0..2 store, their entries (3 + i, l) at T(3 + i) + l)
-    const int e0 = AD ? 6 + (l & 3) : pidx_sel_b(3, lc, Tl, LANE_IN(col_ge_mask<DOF>(3, false))),
-              e1 = AD ? 10 + (l & 3) : pidx_sel_b(4, lc, Tl, LANE_IN(col_ge_mask<DOF>(4, false))),
-              e2 = AD ? 15 + (l & 3) : pidx_sel_b(5, lc, Tl, LANE_IN(col_ge_mask<DOF>(5, false)));
+    const int e0 = pidx_sel_b(3, lc, Tl, LANE_IN(col_ge_mask<DOF>(3, false))),
+              e1 = pidx_sel_b(4, lc, Tl, LANE_IN(col_ge_mask<DOF>(4, false))),
+              e2 = pidx_sel_b(5, lc, Tl, LANE_IN(col_ge_mask<DOF>(5, false)));
     double s0 = sm.S[e0], s1 = sm.S[e1], s2 = sm.S[e2];
     asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2));  // loaded here, not sunk into the store branch
     double B[9];
@@ -1551,7 +1497,7 @@ UWVK_DEV void psp_apply_delta(PspSmem<DOF>& sm, double dl, int l, const double* 
     double n3[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) n3[i] = R[i * 3] * s0 + R[i * 3 + 1] * s1 + R[i * 3 + 2] * s2;
-    if (LANE_IF(l, AD ? l < 3 : (l < DOF && !(l >= 3 && l < 6)))) {
+    if (LANE_IF(l, l < DOF && !(l >= 3 && l < 6))) {
       sm.S[e0] = n3[0];
       sm.S[e1] = n3[1];
       sm.S[e2] = n3[2];
@@ -1786,18 +1732,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   }
   psync();
 #if PSP_PAIR
-#if PSP_FUSE_AD
-  double Rad[9], eqad[4];
-  apply_delta_rot<SR>(dl, Rad, eqad);
-  rankm_rows<DOF, M, true>(sm.S, sm.stg, Ct, Kt, l, Rad);
-  psync();
-  PSP_PHASE(34);
-  psp_apply_delta<DOF, SR, true>(sm, dl, l, Rad, eqad);
-  PSP_PHASE(35);
-  return true;
-#else
   rankm_rows<DOF, M>(sm.S, sm.stg, Ct, Kt, l);
-#endif
 #else
   if constexpr (M <= 3) {
     rankm_mfma_o<DOF, M>(sm.S, sm.stg, Ct, Kt, l);

@@ -405,10 +405,12 @@ def test_headline_shape_sampled(eng, orc, persist):
     batch 65,536, the Monte-Carlo start through the second constructor
     (bench.initialise "mc", PoseUKF.cpp:374-391), the DVL-aligned log
     (bench.window_shift) with its 5-epoch warm-up launch, then the 20-epoch
-    window in ONE run_log launch on k_psp_epoch<53, 1, 1, 1> (right SO3 side,
-    no pressure / ADCP events) with the default scheduler (persistent, tail
-    chunks spread over the ticket counter) and, persist=0, the static
-    tail-spread launch.  16+ XCD-spread instances (tail instances included)
+    window in ONE run_log launch (right SO3 side, no pressure / ADCP events):
+    since r06 the default is the two-instances-per-wave parameter-decoupled
+    kernel k_psp_epoch_pair<1> on the persistent scheduler (pair units, tail
+    chunks spread over the ticket counter); persist=0 runs the one-instance
+    PD kernel k_psp_epoch_p<26, 1, 1, 1, 1> in the static tail-spread launch.
+    16+ XCD-spread instances (tail instances included)
     against the oracle, each run alone on its own one-instance log (the
     Philox streams are keyed by the global instance id)."""
     import os
@@ -426,6 +428,7 @@ def test_headline_shape_sampled(eng, orc, persist):
         g.set_persist(persist)
     bench.initialise(g, log, cfg, uwv, "mc")
     g.set_process_noise_from_config(cfg, log["dt"])
+    assert g.param_block() == 1 and g.pair_active() == (1 if persist is None else 0)
     dlog = g.upload_log(log)
     acc = eng.DeviceBuffer(np.zeros((B, 4), np.uint32))
     g.run_log(dlog, 0, e0, accept_counts=acc)

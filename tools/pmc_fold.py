@@ -7,7 +7,8 @@ the bench (the alignment shift and the warm-up launches come first).
 usage: tools/pmc_fold.py TAG STEPS [WORKLOAD] [ROUND_DIR (default r05)] [KERNEL]
 An optional "mfma" pass (tools/pmc_r03.sh) adds the f64 MFMA counters.
 KERNEL: a substring of the timed kernel's name (default from WORKLOAD: the
-parameter-decoupled k_psp_epoch_p<26, 1, 1, 1, 1> for "-pd", else k_psp_epoch<53,
+parameter-decoupled k_psp_epoch_p<26, 1, 1, 1, 1> for "-pd", k_psp_epoch_pair<1 for
+"-pdpair", else k_psp_epoch<53,
 which also matches the persistent k_psp_epoch_p<53)."""
 import csv
 import json
@@ -24,6 +25,8 @@ base = os.path.join(ROOT, "gpurun_out", tag, "s%d" % steps)
 # k_psp_epoch<53, QM, ...> (r03: instantiated per process-noise shape); a
 # WORKLOAD ending in "-pair" folds the two-instances-per-wave k_psp2_epoch<53, SR>
 KERNEL = "k_psp2_epoch<53" if workload.endswith("-pair") else "k_psp_epoch<53"
+if workload.endswith("-pdpair"):  # r06: the two-instances-per-wave PD kernel (the default since r06)
+    KERNEL = "k_psp_epoch_pair<%d" % (0 if "-left" in workload else 1)
 if workload.endswith("-pd"):
     KERNEL = "k_psp_epoch_p<26, 1, 1, %d, 1>" % (0 if "-left" in workload else 1)
 if len(sys.argv) > 5:
@@ -56,8 +59,10 @@ instances = int(re.search(r"-b(\d+)", workload).group(1))
 we = instances * steps
 e = {
     "kernel": "k_psp2_epoch<53, 1>" if workload.endswith("-pair") else (
+              KERNEL + "> (53-DOF state, parameter-decoupled, two instances per wave)"
+              if workload.endswith("-pdpair") else (
               KERNEL + " (53-DOF state, parameter-decoupled)" if workload.endswith("-pd") else
-              "k_psp_epoch<53, 1, 1, %d>" % (0 if workload.endswith("-left") else 1)),
+              "k_psp_epoch<53, 1, 1, %d>" % (0 if workload.endswith("-left") else 1))),
     "epochs_per_launch": steps, "waves": waves, "instances": instances,
     "fetch_size_kib_raw": fetch["FETCH_SIZE"], "write_size_kib_raw": write["WRITE_SIZE"],
     "fetch_bytes": fetch["FETCH_SIZE"] * 1024 * 2, "write_bytes": write["WRITE_SIZE"] * 1024,
