@@ -675,7 +675,7 @@ def main():
         kname = "%s<%d, %d, %d, %d>" % (kfam, a.dof, f.epoch_qshape(), evs, sr)
     workload = "%s-dof%d-b%d%s%s%s%s" % (log_mode, a.dof, B, "-dense" if a.dense else "",
                                          "-lad" if getattr(a, "literal_apply_delta", False) else "", "" if sr else "-left",
-                                         ("-pair" if pair_window else "-pd") if pd_window else "")
+                                         ("-pdpair" if pair_window else "-pd") if pd_window else "")
     pmc = pmc_entry(workload, a.steps)
     cr = None if a.dense or launches != 1 else counter_roofline(pmc, B, a.steps, kernel_ms)
     traffic = pmc.get("bytes_per_launch") if pmc.get("epochs_per_launch") == a.steps and launches == 1 else None

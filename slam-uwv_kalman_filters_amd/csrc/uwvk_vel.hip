@@ -695,9 +695,6 @@ UWVK_DEV bool vg_update(double mu[4], double S[16], const double z[M], const dou
 // used: hoisted out of the epoch loop it held 50 SGPRs, which the register
 // allocator spilled to VGPR lanes and restored with v_readlane every epoch
 
-#ifndef VEL_EA_LDS
-#define VEL_EA_LDS 1
-#endif
 template <int VG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(VG / 16, VG / 16))) void k_vel_epoch_g(VelBufs b, VelShared P0, VelEpochArgs ea) {
   VEL_PARAMS(b, P0);
@@ -712,17 +709,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(VG / 16, VG 
   for (int k = 0; k < 13; k++) m[k] = b.model[i * 13 + k];
   double q[4] = {m[3], m[4], m[5], m[6]};
   bool ok = true;
-#if VEL_EA_LDS
-  // the low-rate sensors' arguments (DVL / pressure pointers, indices and
-  // covariances) staged in LDS and read in their branches through a laundered
-  // LDS pointer: nothing held in SGPRs across the loop, and no private copy of
-  // the by-value VelEpochArgs (r05: 168 B/lane of scratch read in the loop,
-  // made by laundering the address of ea.dvl_cov)
-  __shared__ VelEpochArgs sea;
-  if (threadIdx.x == 0) sea = ea;
-  __syncthreads();
-  using LEA = const __attribute__((address_space(3))) VelEpochArgs*;
-#endif
   // (r04) the next epoch's gyro / efforts / flag word issued one epoch ahead:
   // at one wave per SIMD the loads' latency was exposed at the top of every epoch
   double w_n[3] = {0, 0, 0}, tau_n[6] = {0, 0, 0, 0, 0, 0};
@@ -779,25 +765,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(VG / 16, VG 
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) q[k] = row_bcast_c<9>(side ? m[3 + k] : 0.0);
-#if VEL_EA_LDS
-    if (fl & UWVK_EV_DVL) {
-      LEA pe = (LEA)&sea;
-      asm volatile("" : "+v"(pe));
-      const double* z = pe->dvl + ((int64_t)pe->dvl_index[e] * B + i) * 3;
-      const double zz[3] = {z[0], z[1], z[2]};
-      double Rd[9];
-#pragma unroll
-      for (int k = 0; k < 9; k++) Rd[k] = pe->dvl_cov[k];
-      ok = vg_update<3, 0>(mu, S, zz, Rd, g) && ok;
-    }
-    if (fl & UWVK_EV_PRESSURE) {
-      LEA pe = (LEA)&sea;
-      asm volatile("" : "+v"(pe));
-      const double zz[1] = {pe->pressure[(int64_t)pe->p_index[e] * B + i]};
-      const double R[1] = {pe->p_cov};
-      ok = vg_update<1, 3>(mu, S, zz, R, g) && ok;
-    }
-#else
     if (fl & UWVK_EV_DVL) {
       const double* z = ea.dvl + ((int64_t)ea.dvl_index[e] * B + i) * 3;
       const double zz[3] = {z[0], z[1], z[2]};
@@ -810,7 +777,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(VG / 16, VG 
       const double R[1] = {ea.p_cov};
       ok = vg_update<1, 3>(mu, S, zz, R, g) && ok;
     }
-#endif
   }
   if (!live) return;
   if (VG == 32 && (threadIdx.x & 16)) return;  // the shadow row
