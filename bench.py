@@ -594,6 +594,7 @@ def main():
     wall, kernel_ms, stats, pieces, windows = 0.0, 0.0, None, 0, []
     truth = log["truth"]
     pd_window = None  # the parameter-decoupled kernel at the window's start (UWVK_OPT_PARAM_BLOCK)
+    pair_window = False  # ... in its two-instances-per-wave form (UWVK_OPT_PAIR)
     for si, (s0, s1) in enumerate(seg_bounds):
         if seg:
             print("segment %d/%d: epochs [%d, %d)" % (si + 1, len(seg_bounds), s0, s1), file=sys.stderr, flush=True)
@@ -613,6 +614,7 @@ def main():
         if lo < s1:
             if pd_window is None:
                 pd_window = bool(f.param_block()) and not a.dense
+                pair_window = bool(f.pair_active()) and pd_window
             windows.append(log["flags"][lo - s0:])
             w_s, k_ms, st, n = timed_run(f, dlog, s0, lo, s1, cut_abs, reduce_stats, truth, a.dof, barrier)
             wall, kernel_ms, pieces = wall + w_s, kernel_ms + k_ms, pieces + n
@@ -663,12 +665,16 @@ def main():
     evs = 0 if (f.epoch_qshape() != 1 or bool(((window & 0xC) != 0).any())) else 1
     sr = 0 if a.so3_left else 1
     persist = a.persist if a.persist >= 0 else 1  # the engine's default scheduler (UWVK_OPT_PERSIST)
-    pair_window = bool(f.pair_active()) if pd_window else False
     kfam = "k_psp_epoch_p" if persist else "k_psp_epoch"
     if a.dense:
         kname = "k_pose_epoch<%d>" % a.dof
     elif pd_window and pair_window:  # two instances per wave (uwvk_psp_pair.hip)
-        kname = "k_psp_epoch_pair<%d, %d> (53-DOF state, parameter-decoupled, 2 instances per wave)" % (evs, sr)
+        kname = "k_psp_epoch_pair<%d, %d> (53-DOF state, parameter-decoupled, 2 instances per wave)" % (
+            sr, 0 if bool(((window & 0x8) != 0).any()) else 1)
+        if bool(((window & 0x4) != 0).any()):  # run_log's split around the pressure epochs
+            kname += "; pressure epochs on %s<26, %d, 0, %d, 1>" % (kfam, f.epoch_qshape(), sr)
+        if bool(((window & 0x10) != 0).any()):
+            kname += "; after the first full BodyEfforts epoch the general 53-DOF kernel"
     elif pd_window:  # 53-DOF state on the 26-DOF layout (the parameter-decoupled kernel)
         kname = "%s<26, %d, %d, %d, 1> (53-DOF state, parameter-decoupled)" % (kfam, f.epoch_qshape(), evs, sr)
     else:

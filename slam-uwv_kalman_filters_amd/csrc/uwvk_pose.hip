@@ -844,28 +844,20 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   HIPCHK(upload_shared(h, log->dt));
   const PoseShared sh = h->sh;  // after upload_shared (it refreshes the Q shape)
   ea.fault = h->d_fault;
-  int64_t e = first;
-  while (e < first + count) {
-    int64_t r = e;
-    while (r < first + count && !(hf[r - first] & UWVK_EV_EFFORTS)) r++;
-    const int64_t last = r < first + count ? r + 1 : r;
-    ea.first = e;
-    ea.count = last - e;
+  // one epoch-kernel launch over [s0, s1): the pair kernel or the one-instance
+  // PSP kernel (parameter-decoupled while eligible)
+  auto launch_seg = [&](int64_t s0, int64_t s1, bool use_pair) -> uwvk_status {
+    ea.first = s0;
+    ea.count = s1 - s0;
     ea.efforts_only = 0;
     int64_t grid = 0;
     uint32_t ev_any = 0;  // the event kinds of this launch's epochs (kernel choice)
-    for (int64_t k = e; k < last; k++) ev_any |= hf[k - first];
-    // the parameter-decoupled kernel while the parameter block is decoupled
-    // (every launch before the first full BodyEfforts epoch of an init's life)
+    for (int64_t k = s0; k < s1; k++) ev_any |= hf[k - first];
     const int pd = use_pd(h) ? 1 : 0;
-    // the two-instances-per-wave form of it (UWVK_OPT_PAIR; persistent, even batch)
-    // (IMU + DVL launches: the pressure update's 39 sigma points do not fit a half-wave)
-    const int pair = pd && h->pair_opt && h->persist && h->batch % 2 == 0 && h->lds_pad == 0 &&
-                     !(ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP));
     PoseBufs bl = b;
     if (pd) bl.Qp = h->d_Qp_pd;
     hipError_t le;
-    if (pair) {
+    if (use_pair) {
       ea.chunks = 1;
       ea.ticket = nullptr;
       HIPCHK(prepare_persist(h, ea, grid, pd, 1));
@@ -875,7 +867,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
       le = launch_psp_epoch(h->dof, h->stream, bl, sh, ea, grid, ev_any, h->lds_pad, pd);
     }
     if (le != hipSuccess) {
-      ::uwvk::note_hip_error((int)le, pair ? "launch_psp_epoch_pair" : "launch_psp_epoch");
+      ::uwvk::note_hip_error((int)le, use_pair ? "launch_psp_epoch_pair" : "launch_psp_epoch");
       // a persistent launch that did not run took no tickets: restart the
       // counter from zero (stream-ordered, before any later launch)
       if (ea.ticket) {
@@ -885,9 +877,51 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
       return UWVK_EDEVICE;
     }
     if (ea.ticket) h->ticket_next += ea.units;  // the tickets the launch takes
+    return UWVK_OK;
+  };
+  int64_t e = first;
+  while (e < first + count) {
+    int64_t r = e;
+    while (r < first + count && !(hf[r - first] & UWVK_EV_EFFORTS)) r++;
+    const int64_t last = r < first + count ? r + 1 : r;
+    // the two-instances-per-wave form of the parameter-decoupled kernel
+    // (UWVK_OPT_PAIR; persistent, even batch) runs the epochs without a
+    // pressure update (its 39 sigma points do not fit a half-wave): a launch
+    // with pressure epochs is split around them when the runs between them are
+    // long (kPairMinRun epochs: each extra launch costs a Sigma round trip and
+    // a ramp), the pressure epochs and short runs on the one-instance kernel
+    const bool pair_ok = use_pd(h) && h->pair_opt && h->persist && h->batch % 2 == 0 && h->lds_pad == 0;
+    if (!pair_ok) {
+      const uwvk_status st = launch_seg(e, last, false);
+      if (st != UWVK_OK) return st;
+    } else {
+      constexpr int64_t kPairMinRun = 48;
+      int64_t s0 = e;  // start of the pending one-instance segment
+      int64_t k = e;
+      while (k < last) {
+        if (hf[k - first] & UWVK_EV_PRESSURE) { k++; continue; }
+        int64_t q = k;  // a run of epochs without pressure: [k, q)
+        while (q < last && !(hf[q - first] & UWVK_EV_PRESSURE)) q++;
+        if (q - k >= kPairMinRun || (k == e && q == last)) {
+          if (k > s0) {
+            const uwvk_status st = launch_seg(s0, k, false);
+            if (st != UWVK_OK) return st;
+          }
+          const uwvk_status st = launch_seg(k, q, true);
+          if (st != UWVK_OK) return st;
+          s0 = q;
+        }
+        k = q;
+      }
+      if (last > s0) {
+        const uwvk_status st = launch_seg(s0, last, false);
+        if (st != UWVK_OK) return st;
+      }
+    }
     if (r < first + count) {
       ea.first = r;
       ea.count = 1;
+      ea.efforts_only = 0;
       // constrainVelocity (PEffVO) or the full measurementEfforts (psp_update_eff)
       const int vo = (hf[r - first] & UWVK_EV_EFFORTS_VELOCITY_ONLY) ? 1 : 0;
       if (!vo) h->pdec = false;  // the full model couples the parameters (PD off from here)

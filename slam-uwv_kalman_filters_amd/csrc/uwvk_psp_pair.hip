@@ -210,11 +210,12 @@ UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
 // The pair kernel's persistent work loop: block b runs pair unit b first, then
 // takes units from the ticket counter (k_psp_epoch_p's scheme); unit u is
 // instances 2u (lanes 0..31) and 2u + 1 (lanes 32..63).
-// IMU + DVL launches only (EpochArgs flags host-checked): the pressure update's
-// nonlinear prefix is k = 19 (pos .. gravity; PoseUKF.cpp:107-115), 39 sigma
-// points, more than a half-wave holds; a launch with pressure or ADCP epochs
-// runs the one-instance PD kernel
-template <int SR>
+// Launches without pressure epochs only (EpochArgs flags host-checked): the
+// pressure update's nonlinear prefix is k = 19 (pos .. gravity;
+// PoseUKF.cpp:107-115), 39 sigma points, more than a half-wave holds; run_log
+// runs those epochs on the one-instance PD kernel.  EVS = 1: no ADCP epoch in
+// the launch either (the ADCP update, k = 6, not compiled in).
+template <int SR, int EVS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PSP_PAIR_WAVES, PSP_PAIR_WAVES)))
 void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmemPD<26> smx[2];
@@ -308,6 +309,22 @@ void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
           nan = true;
         }
       }
+      if constexpr (EVS == 0) {
+        if (fl & UWVK_EV_ADCP) {  // measurementWaterCurrents per cell (PoseUKF.cpp:133-151, :514-527)
+          for (int c = 0; c < ea.cells; c++) {
+            const double* zp = ea.adcp + (((int64_t)ea.a_index[e] * ea.cells + c) * B + inst) * 2;
+            if (!finite_n(zp, 2)) {
+              nan = true;
+              continue;
+            }
+            double z[2] = {zp[0], zp[1]}, R[4] = {ea.adcp_cov[0], ea.adcp_cov[1], ea.adcp_cov[2], ea.adcp_cov[3]};
+            PWater<26> hw;
+            hw.cw = ea.cw[c];
+            cnt[2] += psp_update<26, SR, PWater<26>, NW>(sm, z, R, 1, hw, &sok, ds, ids);
+            ok = ok && sok;
+          }
+        }
+      }
     }
     if (l == 0) {  // local lane 0 of each half: its instance's bookkeeping
       const uint32_t bits = (ok ? 0u : UWVK_ST_NOTPD) | (nan ? UWVK_ST_NAN : 0u);
@@ -342,8 +359,9 @@ template <int SR>
 static hipError_t launch_pair_sr(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
                                  int64_t grid, uint32_t ev_any) {
   const dim3 g((unsigned)grid), t(64);
-  if (ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP)) return hipErrorInvalidValue;  // (pair_ok excludes them)
-  hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR>), g, t, 0, st, b, sh, ea);
+  if (ev_any & UWVK_EV_PRESSURE) return hipErrorInvalidValue;  // (run_log splits those epochs off)
+  if (ev_any & UWVK_EV_ADCP) hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR, 0>), g, t, 0, st, b, sh, ea);
+  else hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR, 1>), g, t, 0, st, b, sh, ea);
   return hipGetLastError();
 }
 
@@ -355,7 +373,7 @@ hipError_t launch_psp_epoch_pair(hipStream_t st, const PoseBufs& b, const PoseSh
 
 int64_t psp_pair_slots(int device) {
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)psp2::k_psp_epoch_pair<1>, 64, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)psp2::k_psp_epoch_pair<1, 1>, 64, 0) !=
           hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return 0;

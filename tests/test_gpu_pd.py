@@ -166,14 +166,15 @@ def _run_pair(eng, log, cfg, uwv, pair, pieces, slots=-1, chunks=0, pd=True):
 @pytest.mark.parametrize("mode,E,pieces", [("C3", 300, [(0, 300)]), ("C3", 1100, [(0, 600), (600, 500)]),
                                            ("C4", 800, [(0, 450), (450, 350)])])
 def test_pair_matches_single(eng, mode, E, pieces):
-    """The pair kernel against the one-instance PD kernel (C4: pressure, ADCP
-    and the efforts epochs, after which both run the general kernel): the same
+    """The pair kernel against the one-instance PD kernel (C4: the launches
+    split around the pressure epochs, ADCP epochs inside the pair runs, then
+    the efforts epochs, after which both run the general kernel): the same
     filter to rounding (the rank-M update's order), gate decisions bitwise."""
     from helpers import cov_err, state_err
     from uwvk import synth
     B = 96
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
-    extra = dict(dropout_on=0.3, dropout_off=0.1, adcp_every=100) if mode == "C4" else {}
+    extra = dict(dropout_on=0.3, dropout_off=0.1, adcp_every=150) if mode == "C4" else {}
     log = synth.make_pose_log(B, E, mode, **extra)
     ref = _run_pair(eng, log, cfg, uwv, False, pieces)
     got = _run_pair(eng, log, cfg, uwv, True, pieces)
@@ -199,13 +200,25 @@ def test_pair_tail_chunks_bitwise(eng, chunks):
     assert not got[3].any()
 
 
-def test_pair_matches_oracle(eng):
+@pytest.mark.parametrize("mode", ["C3", "C4"])
+def test_pair_matches_oracle(eng, mode):
+    """Pair-default handles against the oracle; C4 (compressed drop-out cycle):
+    the launches split around the pressure epochs (those on the one-instance PD
+    kernel, the runs between them on the pair kernel with the ADCP update), then
+    the efforts epochs couple the parameters and the general kernel takes over."""
     from helpers import cov_err, init_both, state_err
     import oracle_ctypes as orc
-    from uwvk import synth
-    B, E = 6, 400
+    from uwvk import abi, synth
+    B, E = 6, 400 if mode == "C3" else 900
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
-    log = synth.make_pose_log(B, E, "C3")
+    # ADCP every 150 epochs: some on pressure epochs (one-instance kernel), some
+    # inside the pair runs (k_psp_epoch_pair<SR, 0>)
+    extra = dict(dropout_on=0.4, dropout_off=0.1, adcp_every=150) if mode == "C4" else {}
+    log = synth.make_pose_log(B, E, mode, **extra)
+    if mode == "C4":
+        fl = log["flags"]
+        assert ((fl & abi.EV_PRESSURE) != 0).any() and ((fl & abi.EV_ADCP) != 0).any()
+        assert ((fl & abi.EV_EFFORTS) != 0).any()
     o = orc.OraclePoseBatch(B, 53)
     g = eng.PoseUKFBatch(B, 53)
     g.set_pair(True)

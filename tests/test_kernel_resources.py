@@ -131,14 +131,15 @@ def test_psp_epoch_kernels_keep_their_occupancy(src, side):
 # The two-instances-per-wave PD kernel (k_psp_epoch_pair<SR, SCHED>, r06, the
 # default of 53-DOF handles' IMU + DVL launches): 3 waves per SIMD (<= 168
 # registers; the r06g A/B measured 3 > 2 > 4 waves: 347.6 / 299.6 / 278.8 M
-# steps/s at C3, 200 epochs) with a bounded spill area (172 B/lane at r06).
+# steps/s at C3, 200 epochs) with a bounded spill area (180 B/lane without the
+# ADCP update, 272 with it, at r06).
 @pytest.mark.skipif(not HAVE_HIPCC, reason="no hipcc")
 def test_pair_kernel_keeps_three_waves_per_simd():
     u = kernel_usage("csrc/uwvk_psp_pair.hip", ("_ZN4uwvk4psp216k_psp_epoch_pairILi",))
-    assert len(u) == 2, sorted(u)  # SR 0 / 1 (persistent)
+    assert len(u) == 4, sorted(u)  # SR 0 / 1 x EVS (ADCP compiled in or not), persistent
     for name, r in u.items():
         regs = r["vgpr"] + r.get("agpr", 0)
-        assert regs <= 168 and r["occupancy"] >= 3 and r["scratch"] <= 256, (name, r)
+        assert regs <= 168 and r["occupancy"] >= 3 and r["scratch"] <= (256 if "Li1EEEvNS" in name else 320), (name, r)
 
 
 # The BodyEfforts kernels (k_psp_efforts<DOF, VO, SR>, r05): no scratch, at
