@@ -180,7 +180,8 @@ def test_pair_matches_single(eng, mode, E, pieces):
     got = _run_pair(eng, log, cfg, uwv, True, pieces)
     np.testing.assert_array_equal(got[2], ref[2])
     np.testing.assert_array_equal(got[3], ref[3])
-    np.testing.assert_array_equal(got[4], ref[4])
+    # the rotation rate less the gyro-bias estimate (getRotationRate): to rounding
+    np.testing.assert_allclose(got[4], ref[4], rtol=1e-9, atol=1e-15)
     assert state_err(got[0], ref[0], ref[1], 53).max() < 1e-9
     assert cov_err(got[1], ref[1]).max() < 1e-9
 
