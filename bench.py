@@ -669,8 +669,10 @@ def main():
     if a.dense:
         kname = "k_pose_epoch<%d>" % a.dof
     elif pd_window and pair_window:  # two instances per wave (uwvk_psp_pair.hip)
+        # EVS 0 (the ADCP update compiled in) when an ADCP epoch falls outside the pressure epochs
+        adcp_in_pair = bool((((window & 0x8) != 0) & ((window & 0x4) == 0)).any())
         kname = "k_psp_epoch_pair<%d, %d> (53-DOF state, parameter-decoupled, 2 instances per wave)" % (
-            sr, 0 if bool(((window & 0x8) != 0).any()) else 1)
+            sr, 0 if adcp_in_pair else 1)
         if bool(((window & 0x4) != 0).any()):  # run_log's split around the pressure epochs
             kname += "; pressure epochs on %s<26, %d, 0, %d, 1>" % (kfam, f.epoch_qshape(), sr)
         if bool(((window & 0x10) != 0).any()):
