@@ -223,8 +223,48 @@ UWVK_DEV bool lane_const() {
 UWVK_DEV bool upper_half() { return lane_const<0xFFFFFFFF00000000ull>(); }
 // local lane j's value of the lane's own instance: readlane (a uniform SGPR
 // pair) with one instance per wave; PSP_PAIR: lane j or 32 + j by half
+#if PSP_PAIR
+#ifndef PSP_HREAD_DPP
+#define PSP_HREAD_DPP 1
+#endif
+// (r06) local lane J < 16 of each half by two DPP moves per dword:
+// row_newbcast:J (every 16-lane row takes its lane J), then row_bcast:15 into
+// rows 1 and 3 from rows 0 and 2 (row_mask 0xa; rows 0 and 2 keep their
+// value): 4 VALU per double instead of four v_readlane and two selects
+template <int J>
+UWVK_DEV double hbc(double v) {
+  static_assert(J >= 0 && J < 16, "row_newbcast lane");
+  int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x150 + J, 0xf, 0xf, false);
+  int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x150 + J, 0xf, 0xf, false);
+  lo = __builtin_amdgcn_update_dpp(lo, lo, 0x142, 0xa, 0xf, false);
+  hi = __builtin_amdgcn_update_dpp(hi, hi, 0x142, 0xa, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+#endif
 UWVK_DEV double hread(double v, int j) {
 #if PSP_PAIR
+#if PSP_HREAD_DPP
+  if (__builtin_constant_p(j) && j >= 0 && j < 16) {
+    switch (j) {
+      case 0: return hbc<0>(v);
+      case 1: return hbc<1>(v);
+      case 2: return hbc<2>(v);
+      case 3: return hbc<3>(v);
+      case 4: return hbc<4>(v);
+      case 5: return hbc<5>(v);
+      case 6: return hbc<6>(v);
+      case 7: return hbc<7>(v);
+      case 8: return hbc<8>(v);
+      case 9: return hbc<9>(v);
+      case 10: return hbc<10>(v);
+      case 11: return hbc<11>(v);
+      case 12: return hbc<12>(v);
+      case 13: return hbc<13>(v);
+      case 14: return hbc<14>(v);
+      default: return hbc<15>(v);
+    }
+  }
+#endif
   const double a = readlane_d(v, j), b = readlane_d(v, 32 + j);
   return upper_half() ? b : a;
 #else
@@ -293,7 +333,7 @@ UWVK_DEV double wave_sum_dpp(double v) {
 #if PSP_PAIR
   // within each 32-lane half: rows 0 / 2 end in lanes 15 / 47, rows 0+1 / 2+3 in 31 / 63
   static_assert(NL <= 32, "pair: one instance per 32-lane half");
-  if constexpr (NL <= 16) return upper_half() ? readlane_d(s, 47) : readlane_d(s, 15);
+  if constexpr (NL <= 16) return hread(s, 15);
   s = s + dpp_d<0x142, 0xa, 0xf>(s);          // row_bcast:15, rows 1,3
   return upper_half() ? readlane_d(s, 63) : readlane_d(s, 31);
 #else
