@@ -241,8 +241,50 @@ UWVK_DEV double hbc(double v) {
   return __hiloint2double(hi, lo);
 }
 #endif
+#if PSP_PAIR
+#ifndef PSP_HREAD_SWAP
+#define PSP_HREAD_SWAP 1
+#endif
+// local lane J in [16, 32) of each half: row_newbcast:(J - 16) leaves the right
+// value in rows 1 and 3; v_permlane16_swap moves rows 1 / 3 of one copy into
+// rows 0 / 2 of the other
+template <int J>
+UWVK_DEV unsigned hbc_hi_u(unsigned v) {
+  static_assert(J >= 16 && J < 32, "row_newbcast lane of rows 1 / 3");
+  const unsigned t = __builtin_amdgcn_update_dpp(0u, v, 0x150 + (J - 16), 0xf, 0xf, false);
+  const auto r = __builtin_amdgcn_permlane16_swap(t, t, false, false);
+  return r[1];
+}
+template <int J>
+UWVK_DEV double hbc_hi(double v) {
+  const unsigned lo = hbc_hi_u<J>((unsigned)__double2loint(v)), hi = hbc_hi_u<J>((unsigned)__double2hiint(v));
+  return __hiloint2double((int)hi, (int)lo);
+}
+#endif
 UWVK_DEV double hread(double v, int j) {
 #if PSP_PAIR
+#if PSP_HREAD_SWAP
+  if (__builtin_constant_p(j) && j >= 16 && j < 32) {
+    switch (j) {
+      case 16: return hbc_hi<16>(v);
+      case 17: return hbc_hi<17>(v);
+      case 18: return hbc_hi<18>(v);
+      case 19: return hbc_hi<19>(v);
+      case 20: return hbc_hi<20>(v);
+      case 21: return hbc_hi<21>(v);
+      case 22: return hbc_hi<22>(v);
+      case 23: return hbc_hi<23>(v);
+      case 24: return hbc_hi<24>(v);
+      case 25: return hbc_hi<25>(v);
+      case 26: return hbc_hi<26>(v);
+      case 27: return hbc_hi<27>(v);
+      case 28: return hbc_hi<28>(v);
+      case 29: return hbc_hi<29>(v);
+      case 30: return hbc_hi<30>(v);
+      default: return hbc_hi<31>(v);
+    }
+  }
+#endif
 #if PSP_HREAD_DPP
   if (__builtin_constant_p(j) && j >= 0 && j < 16) {
     switch (j) {
@@ -335,7 +377,7 @@ UWVK_DEV double wave_sum_dpp(double v) {
   static_assert(NL <= 32, "pair: one instance per 32-lane half");
   if constexpr (NL <= 16) return hread(s, 15);
   s = s + dpp_d<0x142, 0xa, 0xf>(s);          // row_bcast:15, rows 1,3
-  return upper_half() ? readlane_d(s, 63) : readlane_d(s, 31);
+  return hread(s, 31);
 #else
   if constexpr (NL <= 16) return readlane_d(s, 15);
   s = s + dpp_d<0x142, 0xa, 0xf>(s);          // row_bcast:15, rows 1,3
