@@ -224,9 +224,6 @@ UWVK_DEV bool upper_half() { return lane_const<0xFFFFFFFF00000000ull>(); }
 // local lane j's value of the lane's own instance: readlane (a uniform SGPR
 // pair) with one instance per wave; PSP_PAIR: lane j or 32 + j by half
 #if PSP_PAIR
-#ifndef PSP_HREAD_DPP
-#define PSP_HREAD_DPP 1
-#endif
 // (r06) local lane J < 16 of each half by two DPP moves per dword:
 // row_newbcast:J (every 16-lane row takes its lane J), then row_bcast:15 into
 // rows 1 and 3 from rows 0 and 2 (row_mask 0xa; rows 0 and 2 keep their
@@ -241,52 +238,9 @@ UWVK_DEV double hbc(double v) {
   return __hiloint2double(hi, lo);
 }
 #endif
-#if PSP_PAIR
-#ifndef PSP_HREAD_SWAP
-#define PSP_HREAD_SWAP 1
-#endif
-// local lane J in [16, 32) of each half: row_newbcast:(J - 16) leaves the right
-// value in rows 1 and 3; v_permlane16_swap moves rows 1 / 3 of one copy into
-// rows 0 / 2 of the other
-template <int J>
-UWVK_DEV unsigned hbc_hi_u(unsigned v) {
-  static_assert(J >= 16 && J < 32, "row_newbcast lane of rows 1 / 3");
-  const unsigned t = __builtin_amdgcn_update_dpp(0u, v, 0x150 + (J - 16), 0xf, 0xf, false);
-  const auto r = __builtin_amdgcn_permlane16_swap(t, t, false, false);
-  return r[1];
-}
-template <int J>
-UWVK_DEV double hbc_hi(double v) {
-  const unsigned lo = hbc_hi_u<J>((unsigned)__double2loint(v)), hi = hbc_hi_u<J>((unsigned)__double2hiint(v));
-  return __hiloint2double((int)hi, (int)lo);
-}
-#endif
 UWVK_DEV double hread(double v, int j) {
 #if PSP_PAIR
-#if PSP_HREAD_SWAP
-  if (__builtin_constant_p(j) && j >= 16 && j < 32) {
-    switch (j) {
-      case 16: return hbc_hi<16>(v);
-      case 17: return hbc_hi<17>(v);
-      case 18: return hbc_hi<18>(v);
-      case 19: return hbc_hi<19>(v);
-      case 20: return hbc_hi<20>(v);
-      case 21: return hbc_hi<21>(v);
-      case 22: return hbc_hi<22>(v);
-      case 23: return hbc_hi<23>(v);
-      case 24: return hbc_hi<24>(v);
-      case 25: return hbc_hi<25>(v);
-      case 26: return hbc_hi<26>(v);
-      case 27: return hbc_hi<27>(v);
-      case 28: return hbc_hi<28>(v);
-      case 29: return hbc_hi<29>(v);
-      case 30: return hbc_hi<30>(v);
-      default: return hbc_hi<31>(v);
-    }
-  }
-#endif
-#if PSP_HREAD_DPP
-  if (__builtin_constant_p(j) && j >= 0 && j < 16) {
+  if (__builtin_constant_p(j) && j >= 0 && j < 16) {  // (r06: +12% / +8% at 20 / 200 epochs, profiles/r06/r06o/)
     switch (j) {
       case 0: return hbc<0>(v);
       case 1: return hbc<1>(v);
@@ -306,7 +260,6 @@ UWVK_DEV double hread(double v, int j) {
       default: return hbc<15>(v);
     }
   }
-#endif
   const double a = readlane_d(v, j), b = readlane_d(v, 32 + j);
   return upper_half() ? b : a;
 #else
@@ -1484,6 +1437,17 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
 // the diagonal) before its stores; an entry past the diagonal is stored to a
 // throw-away staging slot (stg[80 + r]), so the diagonal is written once, by
 // its own column
+#ifndef PSP_RANKM_MASK
+#define PSP_RANKM_MASK 1
+#endif
+// the rows r of column j's entries: j <= r < DOF (local lanes of either half)
+template <int DOF>
+UWVK_DEV constexpr unsigned long long rankm_col_mask(int j) {
+  unsigned long long m = 0;
+  for (int l = 0; l < 64; l++)
+    if (l >= j && l < DOF) m |= 1ull << l;
+  return m;
+}
 template <int DOF, int M>
 UWVK_DEV void rankm_rows(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
   static_assert(DOF * M <= 80 && 80 + 32 <= PG<DOF>::STG, "K~ rows and the throw-away slots (PG::STG)");
@@ -1496,6 +1460,28 @@ UWVK_DEV void rankm_rows(double* S, double* stg, const double (&Ct)[M], const do
   const int lc = l < DOF ? l : DOF - 1;
   const int b0 = (lc * (lc + 1)) >> 1;
   double* const junk = stg + 80 + (l & 31);
+#if PSP_RANKM_MASK
+  // (r06) entry (r, j) loaded from S[T(r) + j] for every lane (j > r reads a
+  // later entry of the triangle: T(r) + j <= T(DOF - 1) + DOF - 1 < NP) and
+  // stored under the constant lane mask {l : j <= l < DOF} (an EXEC mask by
+  // scalar instructions), instead of two address selects per entry
+  (void)junk;
+#pragma unroll
+  for (int j0 = 0; j0 < DOF; j0 += RB) {
+    double sv[RB];
+#pragma unroll
+    for (int u = 0; u < RB; u++)
+      if (j0 + u < DOF) sv[u] = S[b0 + j0 + u];
+#pragma unroll
+    for (int u = 0; u < RB; u++) {
+      if (j0 + u >= DOF) continue;
+      double s2 = sv[u];
+#pragma unroll
+      for (int k = 0; k < M; k++) s2 = fma(-Ct[k], stg[(j0 + u) * M + k], s2);
+      if (LANE_IN(rankm_col_mask<DOF>(j0 + u))) S[b0 + j0 + u] = s2;
+    }
+  }
+#else
 #pragma unroll
   for (int j0 = 0; j0 < DOF; j0 += RB) {
     double sv[RB];
@@ -1512,6 +1498,7 @@ UWVK_DEV void rankm_rows(double* S, double* stg, const double (&Ct)[M], const do
       *dst = s2;
     }
   }
+#endif
   wsync();  // stg is rewritten next
 }
 #endif  // !PSP_PAIR
