@@ -1433,13 +1433,8 @@ UWVK_DEV void rankm_mfma_o(double* S, double* stg, const double (&Ct)[M], const 
 // PSP_PAIR: Sigma~ -= C~ K~^T as a lane-per-row sweep (one v_mfma_f64_16x16x4
 // tile spans all 64 lanes, i.e. both instances): lane r holds C~_r and K~_r;
 // K~ of every row is staged in the instance's stg and read back as broadcasts;
-// row r's entries go in blocks of RB columns, each block's loads (clamped to
-// the diagonal) before its stores; an entry past the diagonal is stored to a
-// throw-away staging slot (stg[80 + r]), so the diagonal is written once, by
-// its own column
-#ifndef PSP_RANKM_MASK
-#define PSP_RANKM_MASK 1
-#endif
+// row r's entries go in blocks of RB columns, each block's loads before its
+// stores; only the entries on or below the diagonal are stored (lane masks)
 // the rows r of column j's entries: j <= r < DOF (local lanes of either half)
 template <int DOF>
 UWVK_DEV constexpr unsigned long long rankm_col_mask(int j) {
@@ -1450,7 +1445,7 @@ UWVK_DEV constexpr unsigned long long rankm_col_mask(int j) {
 }
 template <int DOF, int M>
 UWVK_DEV void rankm_rows(double* S, double* stg, const double (&Ct)[M], const double (&Kt)[M], int l) {
-  static_assert(DOF * M <= 80 && 80 + 32 <= PG<DOF>::STG, "K~ rows and the throw-away slots (PG::STG)");
+  static_assert(DOF * M <= PG<DOF>::STG, "K~ rows (PG::STG)");
   constexpr int RB = 4;
   if (l < DOF) {
 #pragma unroll
@@ -1459,13 +1454,11 @@ UWVK_DEV void rankm_rows(double* S, double* stg, const double (&Ct)[M], const do
   wsync();
   const int lc = l < DOF ? l : DOF - 1;
   const int b0 = (lc * (lc + 1)) >> 1;
-  double* const junk = stg + 80 + (l & 31);
-#if PSP_RANKM_MASK
   // (r06) entry (r, j) loaded from S[T(r) + j] for every lane (j > r reads a
   // later entry of the triangle: T(r) + j <= T(DOF - 1) + DOF - 1 < NP) and
   // stored under the constant lane mask {l : j <= l < DOF} (an EXEC mask by
-  // scalar instructions), instead of two address selects per entry
-  (void)junk;
+  // scalar instructions), instead of two address selects per entry to a
+  // throw-away slot: +1.5% at 200 epochs (profiles/r06/r06q/)
 #pragma unroll
   for (int j0 = 0; j0 < DOF; j0 += RB) {
     double sv[RB];
@@ -1481,24 +1474,6 @@ UWVK_DEV void rankm_rows(double* S, double* stg, const double (&Ct)[M], const do
       if (LANE_IN(rankm_col_mask<DOF>(j0 + u))) S[b0 + j0 + u] = s2;
     }
   }
-#else
-#pragma unroll
-  for (int j0 = 0; j0 < DOF; j0 += RB) {
-    double sv[RB];
-#pragma unroll
-    for (int u = 0; u < RB; u++)
-      if (j0 + u < DOF) sv[u] = S[b0 + (j0 + u <= lc ? j0 + u : lc)];
-#pragma unroll
-    for (int u = 0; u < RB; u++) {
-      if (j0 + u >= DOF) continue;
-      double s2 = sv[u];
-#pragma unroll
-      for (int k = 0; k < M; k++) s2 = fma(-Ct[k], stg[(j0 + u) * M + k], s2);
-      double* dst = (l < DOF && j0 + u <= l) ? S + b0 + j0 + u : junk;
-      *dst = s2;
-    }
-  }
-#endif
   wsync();  // stg is rewritten next
 }
 #endif  // !PSP_PAIR
