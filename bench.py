@@ -614,7 +614,7 @@ def main():
         if lo < s1:
             if pd_window is None:
                 pd_window = bool(f.param_block()) and not a.dense
-                pair_window = bool(f.pair_active()) and pd_window
+                pair_window = bool(f.pair_active()) and not a.dense
             windows.append(log["flags"][lo - s0:])
             w_s, k_ms, st, n = timed_run(f, dlog, s0, lo, s1, cut_abs, reduce_stats, truth, a.dof, barrier)
             wall, kernel_ms, pieces = wall + w_s, kernel_ms + k_ms, pieces + n
@@ -668,14 +668,15 @@ def main():
     kfam = "k_psp_epoch_p" if persist else "k_psp_epoch"
     if a.dense:
         kname = "k_pose_epoch<%d>" % a.dof
-    elif pd_window and pair_window:  # two instances per wave (uwvk_psp_pair.hip)
+    elif pair_window:  # two instances per wave (uwvk_psp_pair.hip)
         # EVS 0 (the ADCP update compiled in) when an ADCP epoch falls outside the pressure epochs
         adcp_in_pair = bool((((window & 0x8) != 0) & ((window & 0x4) == 0)).any())
-        kname = "k_psp_epoch_pair<%d, %d> (53-DOF state, parameter-decoupled, 2 instances per wave)" % (
-            sr, 0 if adcp_in_pair else 1)
+        kname = "k_psp_epoch_pair<%d, %d, %d> (%s, 2 instances per wave)" % (
+            sr, 0 if adcp_in_pair else 1, 1 if pd_window else 0,
+            "53-DOF state, parameter-decoupled" if pd_window else "26-DOF state")
         if bool(((window & 0x4) != 0).any()):  # run_log's split around the pressure epochs
-            kname += "; pressure epochs on %s<26, %d, 0, %d, 1>" % (kfam, f.epoch_qshape(), sr)
-        if bool(((window & 0x10) != 0).any()):
+            kname += "; pressure epochs on %s<26, %d, 0, %d, %d>" % (kfam, f.epoch_qshape(), sr, 1 if pd_window else 0)
+        if pd_window and bool(((window & 0x10) != 0).any()):
             kname += "; after the first full BodyEfforts epoch the general 53-DOF kernel"
     elif pd_window:  # 53-DOF state on the 26-DOF layout (the parameter-decoupled kernel)
         kname = "%s<26, %d, %d, %d, 1> (53-DOF state, parameter-decoupled)" % (kfam, f.epoch_qshape(), evs, sr)
@@ -683,7 +684,8 @@ def main():
         kname = "%s<%d, %d, %d, %d>" % (kfam, a.dof, f.epoch_qshape(), evs, sr)
     workload = "%s-dof%d-b%d%s%s%s%s" % (log_mode, a.dof, B, "-dense" if a.dense else "",
                                          "-lad" if getattr(a, "literal_apply_delta", False) else "", "" if sr else "-left",
-                                         ("-pdpair" if pair_window else "-pd") if pd_window else "")
+                                         ("-pdpair" if pair_window else "-pd") if pd_window else
+                                         ("-pair" if pair_window else ""))
     pmc = pmc_entry(workload, a.steps)
     cr = None if a.dense or launches != 1 else counter_roofline(pmc, B, a.steps, kernel_ms)
     traffic = pmc.get("bytes_per_launch") if pmc.get("epochs_per_launch") == a.steps and launches == 1 else None

@@ -160,6 +160,15 @@ static bool use_pd(const uwvk_pose* h) {
   return h->pd_opt && h->pdec && h->dof == 53 && h->sh.q_simple && q_params_diag(h);
 }
 
+// the two-instances-per-wave kernel (UWVK_OPT_PAIR): the parameter-decoupled
+// state of a 53-DOF handle, or a 26-DOF handle's own state (r06), on the
+// persistent scheduler, an even batch, the lane-resident Q and no LDS pad
+static bool pair_eligible(uwvk_pose* h) {
+  if (!h->pair_opt || !h->persist || h->batch % 2 != 0 || h->lds_pad != 0 || use_dense(h)) return false;
+  if (h->dof == 26) return q_is_simple(h);
+  return h->pd_opt && h->pdec && h->dof == 53 && q_is_simple(h) && q_params_diag(h);  // (uwvk_pose_param_block)
+}
+
 static hipError_t upload_shared(uwvk_pose* h, double dt) {
   hipError_t e = hipSuccess;
   if (dt != h->qp_dt) {
@@ -846,7 +855,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
   ea.fault = h->d_fault;
   // one epoch-kernel launch over [s0, s1): the pair kernel or the one-instance
   // PSP kernel (parameter-decoupled while eligible)
-  auto launch_seg = [&](int64_t s0, int64_t s1, bool use_pair) -> uwvk_status {
+  auto launch_seg = [&](int64_t s0, int64_t s1, bool use_pair) -> uwvk_status {  // (pair or one-instance)
     ea.first = s0;
     ea.count = s1 - s0;
     ea.efforts_only = 0;
@@ -856,12 +865,13 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     const int pd = use_pd(h) ? 1 : 0;
     PoseBufs bl = b;
     if (pd) bl.Qp = h->d_Qp_pd;
+    if (h->dof == 53 && !pd) use_pair = false;  // (the pair kernel runs a 53-DOF state decoupled only)
     hipError_t le;
     if (use_pair) {
       ea.chunks = 1;
       ea.ticket = nullptr;
       HIPCHK(prepare_persist(h, ea, grid, pd, 1));
-      le = launch_psp_epoch_pair(h->stream, bl, sh, ea, grid, ev_any);
+      le = launch_psp_epoch_pair(h->stream, bl, sh, ea, grid, ev_any, pd);
     } else {
       HIPCHK(prepare_tail(h, ea, grid, pd));
       le = launch_psp_epoch(h->dof, h->stream, bl, sh, ea, grid, ev_any, h->lds_pad, pd);
@@ -890,7 +900,7 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     // with pressure epochs is split around them when the runs between them are
     // long (kPairMinRun epochs: each extra launch costs a Sigma round trip and
     // a ramp), the pressure epochs and short runs on the one-instance kernel
-    const bool pair_ok = use_pd(h) && h->pair_opt && h->persist && h->batch % 2 == 0 && h->lds_pad == 0;
+    const bool pair_ok = pair_eligible(h);
     if (!pair_ok) {
       const uwvk_status st = launch_seg(e, last, false);
       if (st != UWVK_OK) return st;
@@ -1020,9 +1030,7 @@ int uwvk_pose_param_block(uwvk_pose* h) {
   return (h->pd_opt && h->pdec && h->dof == 53 && q_is_simple(h) && q_params_diag(h)) ? 1 : 0;
 }
 
-int uwvk_pose_pair_active(uwvk_pose* h) {
-  return (uwvk_pose_param_block(h) && h->pair_opt && h->persist && h->batch % 2 == 0 && h->lds_pad == 0) ? 1 : 0;
-}
+int uwvk_pose_pair_active(uwvk_pose* h) { return (h && pair_eligible(h)) ? 1 : 0; }
 
 int uwvk_xcd_round_robin(int device) { return xcd_round_robin(device); }
 

@@ -62,7 +62,7 @@ int plan_tail(int64_t n, int64_t s, int64_t count);
 // persistent only (ea.ticket), pair units (EpochArgs units / tail0 / r_x count
 // pairs of instances 2u, 2u + 1), the PD table in b.Qp, sh.q_simple
 hipError_t launch_psp_epoch_pair(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                                 int64_t grid, uint32_t ev_any);
+                                 int64_t grid, uint32_t ev_any, int pd);
 // its resident blocks on the device (occupancy x CUs), 0 if unknown
 int64_t psp_pair_slots(int device);
 // 1 once a probe grid has shown round-robin block placement over 8 XCCs on

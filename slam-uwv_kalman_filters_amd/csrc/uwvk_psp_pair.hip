@@ -188,6 +188,43 @@ UWVK_DEV void store_pair(const PspSmem<26>& sm, const double* px, const PoseBufs
   }
 }
 
+// a 26-DOF handle's own state (PD = 0): the packed 26-DOF triangle and mean
+// (uwvk_psp_k.hip load_psp<26> / store_psp<26>, on 32 lanes per instance)
+UWVK_DEV void load_pair26(PspSmem<26>& sm, const PoseBufs& b, int64_t inst, int l) {
+  using G = PG<26>;
+  const double* gs = b.sigma + inst * (int64_t)G::NP;
+  const double* gm = b.mu + inst * (int64_t)Lay<26>::store;
+  double v[G::NSLOT];
+#pragma unroll
+  for (int t = 0; t < G::NSLOT; t++) {
+    const int e = l + kLanes * t;
+    v[t] = e < G::NP ? gs[e] : 0.0;
+  }
+  const double m = l < Lay<26>::store ? gm[l] : 0.0;
+#pragma unroll
+  for (int t = 0; t < G::NSLOT; t++) {
+    const int e = l + kLanes * t;
+    if (e < G::NP) sm.S[e] = v[t];
+  }
+  if (l < Lay<26>::store) sm.mu[l] = m;
+  psync();
+}
+UWVK_DEV void store_pair26(const PspSmem<26>& sm, const PoseBufs& b, int64_t inst, int l) {
+  using G = PG<26>;
+  double* gs = b.sigma + inst * (int64_t)G::NP;
+  double* gm = b.mu + inst * (int64_t)Lay<26>::store;
+  double v[G::NSLOT];
+#pragma unroll
+  for (int t = 0; t < G::NSLOT; t++) v[t] = flat(sm)[l + kLanes * t];
+  const double m = flat(sm)[kFlatMu<26> + l];
+#pragma unroll
+  for (int t = 0; t < G::NSLOT; t++) {
+    const int e = l + kLanes * t;
+    if (e < G::NP) gs[e] = v[t];
+  }
+  if (l < Lay<26>::store) gm[l] = m;
+}
+
 template <int M>
 UWVK_DEV void copy_zr(const double* zin, const double* Rin, double (&z)[M], double (&R)[M * M]) {
 #pragma unroll
@@ -215,14 +252,17 @@ UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
 // PoseUKF.cpp:107-115), 39 sigma points, more than a half-wave holds; run_log
 // runs those epochs on the one-instance PD kernel.  EVS = 1: no ADCP epoch in
 // the launch either (the ADCP update, k = 6, not compiled in).
-template <int SR, int EVS>
+// PD = 1: a 53-DOF handle's parameter-decoupled state (NW = 53, the 27
+// parameters in pS / pm); PD = 0 (r06): a 26-DOF kinematic handle's own state
+// (NW = 26, no parameter lanes).
+template <int SR, int EVS, int PD>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PSP_PAIR_WAVES, PSP_PAIR_WAVES)))
 void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
   __shared__ PspSmemPD<26> smx[2];
   const int h = half();
   PspSmem<26>& sm = smx[h];
   double* const px = smx[h].pS;
-  constexpr int NW = 53;
+  constexpr int NW = PD ? 53 : 26;
   const int64_t B = b.batch;
   const uint32_t grid = gridDim.x;
   uint32_t u = blockIdx.x;
@@ -252,7 +292,7 @@ void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
     }
     pc.off = nullptr;
     lane_proc(b, *b.shared, inst, l, pc);
-    const ParLane pl = par_lane(b, *b.shared, inst, l);
+    const ParLane pl = PD ? par_lane(b, *b.shared, inst, l) : ParLane{0.0, 0.0, 0.0};
     const LaneQ lq = lane_q<26, 0>(b.Qp, l);
     uint32_t fl_n = 0;
     double g_n[3] = {0, 0, 0}, a_n[3] = {0, 0, 0};
@@ -265,7 +305,8 @@ void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
       }
     };
     if (e_end > e_begin) fetch(e_begin);
-    load_pair(sm, px, b, inst, l);
+    if constexpr (PD) load_pair(sm, px, b, inst, l);
+    else load_pair26(sm, b, inst, l);
     double ds = 1.0, ids = 1.0;  // time scale of the 26-DOF layout's Markov DOFs
     if (tu.chunk > 0) {
       const double2 c = reinterpret_cast<const double2*>(ea.tail_carry)[tu.tslot * 64 + lane_id()];
@@ -285,8 +326,8 @@ void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
       }
       const PoseShared& sh = shared_for_epoch(b);
       if (((e - ea.first) & 1023) == 1023) psp_fold<26, 0>(sm, ds, ids);
-      bool sok = psp_predict<26, 1, SR, 1>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, nullptr, px);
-      par_epoch(px, l, pc.dt, pl);
+      bool sok = psp_predict<26, 1, SR, PD>(sm, sh, pc, b.Q, b.Qp, ds, ids, lq, nullptr, px);
+      if constexpr (PD) par_epoch(px, l, pc.dt, pl);
       ok = ok && sok;
       if (fl & UWVK_EV_ACC) {
         if (finite_n(za, 3)) {
@@ -346,7 +387,8 @@ void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
     } else {
       psp_fold<26, 0>(sm, ds, ids);
     }
-    store_pair(sm, px, b, inst, l);
+    if constexpr (PD) store_pair(sm, px, b, inst, l);
+    else store_pair26(sm, b, inst, l);
     if (hand) tail_signal(ea, tn.tslot, tn.chunk);
     u = un;
     psync();  // the next unit's LDS writes after this unit's reads
@@ -355,25 +397,28 @@ void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
 
 }  // namespace psp2
 
-template <int SR>
+template <int SR, int PD>
 static hipError_t launch_pair_sr(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
                                  int64_t grid, uint32_t ev_any) {
   const dim3 g((unsigned)grid), t(64);
   if (ev_any & UWVK_EV_PRESSURE) return hipErrorInvalidValue;  // (run_log splits those epochs off)
-  if (ev_any & UWVK_EV_ADCP) hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR, 0>), g, t, 0, st, b, sh, ea);
-  else hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR, 1>), g, t, 0, st, b, sh, ea);
+  if (ev_any & UWVK_EV_ADCP) hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR, 0, PD>), g, t, 0, st, b, sh, ea);
+  else hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR, 1, PD>), g, t, 0, st, b, sh, ea);
   return hipGetLastError();
 }
 
 hipError_t launch_psp_epoch_pair(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
-                                 int64_t grid, uint32_t ev_any) {
+                                 int64_t grid, uint32_t ev_any, int pd) {
   if (!sh.q_simple || !ea.ticket || grid <= 0) return hipErrorInvalidValue;
-  return sh.so3_right ? launch_pair_sr<1>(st, b, sh, ea, grid, ev_any) : launch_pair_sr<0>(st, b, sh, ea, grid, ev_any);
+  if (pd) return sh.so3_right ? launch_pair_sr<1, 1>(st, b, sh, ea, grid, ev_any)
+                              : launch_pair_sr<0, 1>(st, b, sh, ea, grid, ev_any);
+  return sh.so3_right ? launch_pair_sr<1, 0>(st, b, sh, ea, grid, ev_any)
+                      : launch_pair_sr<0, 0>(st, b, sh, ea, grid, ev_any);
 }
 
 int64_t psp_pair_slots(int device) {
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)psp2::k_psp_epoch_pair<1, 1>, 64, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)psp2::k_psp_epoch_pair<1, 1, 1>, 64, 0) !=
           hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return 0;

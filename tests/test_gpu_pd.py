@@ -144,10 +144,10 @@ def test_pd_eligibility(eng):
 
 
 # ---- the two-instances-per-wave form (UWVK_OPT_PAIR, csrc/uwvk_psp_pair.hip) ----
-def _run_pair(eng, log, cfg, uwv, pair, pieces, slots=-1, chunks=0, pd=True):
+def _run_pair(eng, log, cfg, uwv, pair, pieces, slots=-1, chunks=0, pd=True, dof=53):
     from uwvk import abi
     B = log["gyro"].shape[1]
-    g = eng.PoseUKFBatch(B, 53)
+    g = eng.PoseUKFBatch(B, dof)
     g.set_param_block(pd)
     g.set_pair(pair)
     g.set_tail_slots(slots)
@@ -155,6 +155,7 @@ def _run_pair(eng, log, cfg, uwv, pair, pieces, slots=-1, chunks=0, pd=True):
         g.set_tail_chunks(chunks)
     g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
     g.set_process_noise_from_config(cfg, 1e-3)
+    assert g.pair_active() == (1 if pair else 0)
     dlog = g.upload_log(log)
     acc = eng.DeviceBuffer(np.zeros((B, 4), np.uint32))
     for a, n in pieces:
@@ -163,9 +164,11 @@ def _run_pair(eng, log, cfg, uwv, pair, pieces, slots=-1, chunks=0, pd=True):
     return x, P, acc.read(np.uint32, (B, 4)), g.get_status(), g.get_rotation_rate()
 
 
-@pytest.mark.parametrize("mode,E,pieces", [("C3", 300, [(0, 300)]), ("C3", 1100, [(0, 600), (600, 500)]),
-                                           ("C4", 800, [(0, 450), (450, 350)])])
-def test_pair_matches_single(eng, mode, E, pieces):
+@pytest.mark.parametrize("mode,E,pieces,dof", [("C3", 300, [(0, 300)], 53), ("C3", 1100, [(0, 600), (600, 500)], 53),
+                                               ("C4", 800, [(0, 450), (450, 350)], 53),
+                                               ("C3", 600, [(0, 350), (350, 250)], 26),
+                                               ("C4", 800, [(0, 450), (450, 350)], 26)])
+def test_pair_matches_single(eng, mode, E, pieces, dof):
     """The pair kernel against the one-instance PD kernel (C4: the launches
     split around the pressure epochs, ADCP epochs inside the pair runs, then
     the efforts epochs, after which both run the general kernel): the same
@@ -175,14 +178,14 @@ def test_pair_matches_single(eng, mode, E, pieces):
     B = 96
     cfg, uwv = synth.default_pose_config(), synth.default_uwv()
     extra = dict(dropout_on=0.3, dropout_off=0.1, adcp_every=150) if mode == "C4" else {}
-    log = synth.make_pose_log(B, E, mode, **extra)
-    ref = _run_pair(eng, log, cfg, uwv, False, pieces)
-    got = _run_pair(eng, log, cfg, uwv, True, pieces)
+    log = synth.make_pose_log(B, E, mode, dof=dof, **extra)
+    ref = _run_pair(eng, log, cfg, uwv, False, pieces, dof=dof)
+    got = _run_pair(eng, log, cfg, uwv, True, pieces, dof=dof)
     np.testing.assert_array_equal(got[2], ref[2])
     np.testing.assert_array_equal(got[3], ref[3])
     # the rotation rate less the gyro-bias estimate (getRotationRate): to rounding
     np.testing.assert_allclose(got[4], ref[4], rtol=1e-9, atol=1e-15)
-    assert state_err(got[0], ref[0], ref[1], 53).max() < 1e-9
+    assert state_err(got[0], ref[0], ref[1], dof).max() < 1e-9
     assert cov_err(got[1], ref[1]).max() < 1e-9
 
 
@@ -201,9 +204,9 @@ def test_pair_tail_chunks_bitwise(eng, chunks):
     assert not got[3].any()
 
 
-@pytest.mark.parametrize("mode", ["C3", "C4"])
-def test_pair_matches_oracle(eng, mode):
-    """Pair-default handles against the oracle; C4 (compressed drop-out cycle):
+@pytest.mark.parametrize("mode,dof", [("C3", 53), ("C4", 53), ("C3", 26), ("C4", 26)])
+def test_pair_matches_oracle(eng, mode, dof):
+    """Pair-default handles (53-DOF decoupled, 26-DOF) against the oracle; C4 (compressed drop-out cycle):
     the launches split around the pressure epochs (those on the one-instance PD
     kernel, the runs between them on the pair kernel with the ADCP update), then
     the efforts epochs couple the parameters and the general kernel takes over."""
@@ -215,13 +218,13 @@ def test_pair_matches_oracle(eng, mode):
     # ADCP every 150 epochs: some on pressure epochs (one-instance kernel), some
     # inside the pair runs (k_psp_epoch_pair<SR, 0>)
     extra = dict(dropout_on=0.4, dropout_off=0.1, adcp_every=150) if mode == "C4" else {}
-    log = synth.make_pose_log(B, E, mode, **extra)
+    log = synth.make_pose_log(B, E, mode, dof=dof, **extra)
     if mode == "C4":
         fl = log["flags"]
         assert ((fl & abi.EV_PRESSURE) != 0).any() and ((fl & abi.EV_ADCP) != 0).any()
         assert ((fl & abi.EV_EFFORTS) != 0).any()
-    o = orc.OraclePoseBatch(B, 53)
-    g = eng.PoseUKFBatch(B, 53)
+    o = orc.OraclePoseBatch(B, dof)
+    g = eng.PoseUKFBatch(B, dof)
     g.set_pair(True)
     init_both(o, g, cfg, uwv, log)
     co = o.run_log(log)
@@ -231,4 +234,4 @@ def test_pair_matches_oracle(eng, mode):
     np.testing.assert_array_equal(co, acc.read(np.uint32, (B, 4)))
     xo, Po = o.get_state()
     xg, Pg = g.get_state()
-    assert state_err(xg, xo, Po, 53).max() < 1e-7 and cov_err(Pg, Po).max() < 1e-7
+    assert state_err(xg, xo, Po, dof).max() < 1e-7 and cov_err(Pg, Po).max() < 1e-7
