@@ -25,6 +25,19 @@ namespace uwvk {
 // public entry point starts with a DeviceGuard, so the text always belongs to
 // the current call's UWVK_EDEVICE, never an earlier, unrelated failure
 void clear_hip_error();
+void note_hip_error(int err, const char* where);
+// UWVK_EDEVICE with the text of the first failing HIP call (uwvk_last_device_error)
+inline int edevice_status(hipError_t e, const char* where) {
+  note_hip_error((int)e, where);
+  return 5;  // UWVK_EDEVICE (include/uwvk.h; static_assert in uwvk_rt.hip)
+}
+// a launch's error, else its stream synchronisation's; 0 when both succeeded
+inline int launch_sync_status(hipError_t launch, hipStream_t st, const char* where) {
+  const hipError_t s = hipStreamSynchronize(st);
+  if (launch != hipSuccess) return edevice_status(launch, where);
+  if (s != hipSuccess) return edevice_status(s, where);
+  return 0;
+}
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int device) {

@@ -351,7 +351,8 @@ static bool take_fault(uwvk_pose* h) {
 uwvk_status uwvk_pose_synchronize(uwvk_pose* h) {
   UWVK_DEVICE_GUARD(h);
   if (!h) return UWVK_EINVAL;
-  if (hipStreamSynchronize(h->stream) != hipSuccess) return UWVK_EDEVICE;
+  const hipError_t e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) return (uwvk_status)::uwvk::edevice_status(e, "uwvk_pose_synchronize");
   return take_fault(h) ? UWVK_ESCHEDULE : UWVK_OK;
 }
 
@@ -615,8 +616,7 @@ uwvk_status uwvk_pose_update_visual_landmark(uwvk_pose* h, int32_t n_features, c
   }
   h->pdec = false;  // the literal augmented update (all sigma points)
   const hipError_t e = launch_pose_visual(h->dof, h->sh.so3_right, h->stream, bufs(h), va);
-  if (hipStreamSynchronize(h->stream) != hipSuccess || e != hipSuccess) return UWVK_EDEVICE;
-  return UWVK_OK;
+  return (uwvk_status)::uwvk::launch_sync_status(e, h->stream, "launch_pose_visual");
 }
 
 uwvk_status uwvk_pose_update_delayed_xy(uwvk_pose* h, const double* mu, const double* cov, const double* sc,

@@ -9,6 +9,7 @@
 #include "../../include/uwvk.h"
 #include "uwvk_dev.hpp"
 
+static_assert(UWVK_EDEVICE == 5, "uwvk_dev.hpp edevice_status");
 namespace uwvk {
 // uwvk_last_device_error: the HIP error behind the thread's last UWVK_EDEVICE
 thread_local char g_last_hip_error[160] = "";
@@ -99,14 +100,14 @@ uwvk_status uwvk_memcpy_d2h(void* dst, const void* src, size_t bytes) {
 uwvk_status uwvk_memcpy_h2d_on(void* dst, const void* src, size_t bytes, void* stream) {
   uwvk::clear_hip_error();
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st) != hipSuccess) return UWVK_EDEVICE;
-  return hipStreamSynchronize(st) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
+  const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+  return (uwvk_status)uwvk::launch_sync_status(e, st, "uwvk_memcpy_h2d_on");
 }
 uwvk_status uwvk_memcpy_d2h_on(void* dst, const void* src, size_t bytes, void* stream) {
   uwvk::clear_hip_error();
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) return UWVK_EDEVICE;
-  return hipStreamSynchronize(st) == hipSuccess ? UWVK_OK : UWVK_EDEVICE;
+  const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+  return (uwvk_status)uwvk::launch_sync_status(e, st, "uwvk_memcpy_d2h_on");
 }
 
 }  // extern "C"

@@ -595,8 +595,7 @@ uwvk_status uwvk_ipose_update_visual(uwvk_ipose* h, int32_t n_features, const do
     hipLaunchKernelGGL(k_ipose_visual<0>, dim3(grid_of(h->batch, IAE<0>::IPB)), dim3(IAE<0>::BLOCK), 0, h->stream,
                        h->bufs(), va);
   const hipError_t e = hipGetLastError();
-  if (hipStreamSynchronize(h->stream) != hipSuccess || e != hipSuccess) return UWVK_EDEVICE;
-  return UWVK_OK;
+  return (uwvk_status)::uwvk::launch_sync_status(e, h->stream, "k_ipose_visual");
 }
 
 // getCorrectedPose (IndirectPoseUKF.cpp:137-142): pose_ref * pose_error, t(3) q(4)
