@@ -238,49 +238,8 @@ UWVK_DEV double hbc(double v) {
   return __hiloint2double(hi, lo);
 }
 #endif
-#if PSP_PAIR
-// local lane J in [16, 32): row_newbcast:(J - 16) fills rows 1 / 3, wave_shl:1
-// hands lane 16 (48) to lane 15 (47), row_newbcast:15 fills rows 0 / 2 from it
-// (3 DPP moves per dword, no v_readlane)
-template <int J>
-UWVK_DEV int hbc_hi_i(int v) {
-  static_assert(J >= 16 && J < 32, "rows 1 / 3");
-  int t = __builtin_amdgcn_update_dpp(0, v, 0x150 + (J - 16), 0xf, 0xf, false);
-  int w = __builtin_amdgcn_update_dpp(t, t, 0x130, 0x5, 0xf, false);  // wave_shl:1, rows 0,2
-  return __builtin_amdgcn_update_dpp(w, w, 0x15F, 0x5, 0xf, false);  // row_newbcast:15, rows 0,2
-}
-template <int J>
-UWVK_DEV double hbc_hi(double v) {
-  return __hiloint2double(hbc_hi_i<J>(__double2hiint(v)), hbc_hi_i<J>(__double2loint(v)));
-}
-#ifndef PSP_HREAD_HI
-#define PSP_HREAD_HI 1
-#endif
-#endif
 UWVK_DEV double hread(double v, int j) {
 #if PSP_PAIR
-#if PSP_HREAD_HI
-  if (__builtin_constant_p(j) && j >= 16 && j < 32) {
-    switch (j) {
-      case 16: return hbc_hi<16>(v);
-      case 17: return hbc_hi<17>(v);
-      case 18: return hbc_hi<18>(v);
-      case 19: return hbc_hi<19>(v);
-      case 20: return hbc_hi<20>(v);
-      case 21: return hbc_hi<21>(v);
-      case 22: return hbc_hi<22>(v);
-      case 23: return hbc_hi<23>(v);
-      case 24: return hbc_hi<24>(v);
-      case 25: return hbc_hi<25>(v);
-      case 26: return hbc_hi<26>(v);
-      case 27: return hbc_hi<27>(v);
-      case 28: return hbc_hi<28>(v);
-      case 29: return hbc_hi<29>(v);
-      case 30: return hbc_hi<30>(v);
-      default: return hbc_hi<31>(v);
-    }
-  }
-#endif
   if (__builtin_constant_p(j) && j >= 0 && j < 16) {  // (r06: +12% / +8% at 20 / 200 epochs, profiles/r06/r06o/)
     switch (j) {
       case 0: return hbc<0>(v);
@@ -351,16 +310,6 @@ UWVK_DEV constexpr bool rows_ascending() {
 // row_shr 4/8 with bank masks -> row sums in lane 15 of each row, row_bcast
 // 15/31 -> the total in lane 63, read back as a uniform (SGPR) value.
 // ---------------------------------------------------------------------------
-#ifndef PSP_WSUM_MIRROR
-#define PSP_WSUM_MIRROR 1
-#endif
-// the same with the rows / banks outside the masks keeping `old`
-template <int CTRL, int ROW, int BANK>
-UWVK_DEV double dpp_d_old(double old, double v) {
-  const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), CTRL, ROW, BANK, false);
-  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), CTRL, ROW, BANK, false);
-  return __hiloint2double(hi, lo);
-}
 template <int CTRL, int ROW, int BANK>
 UWVK_DEV double dpp_d(double v) {
   const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW, BANK, true);
@@ -380,18 +329,8 @@ UWVK_DEV double wave_sum_dpp(double v) {
   // within each 32-lane half: rows 0 / 2 end in lanes 15 / 47, rows 0+1 / 2+3 in 31 / 63
   static_assert(NL <= 32, "pair: one instance per 32-lane half");
   if constexpr (NL <= 16) return hread(s, 15);
-#if PSP_WSUM_MIRROR
-  // (r06) rows 1 / 3 mirrored (their sum moves from lane 15 to their first
-  // lane), then wave_shl:1 into rows 0 / 2: lane 15 (47) adds its neighbour
-  // row's sum, and the DPP broadcast of lane 15 spreads the half's total
-  // (no v_readlane)
-  const double m = dpp_d_old<0x140, 0xa, 0xf>(s, s);  // row_mirror, rows 1,3
-  s = s + dpp_d<0x130, 0x5, 0xf>(m);                  // wave_shl:1, rows 0,2
-  return hread(s, 15);
-#else
   s = s + dpp_d<0x142, 0xa, 0xf>(s);          // row_bcast:15, rows 1,3
   return hread(s, 31);
-#endif
 #else
   if constexpr (NL <= 16) return readlane_d(s, 15);
   s = s + dpp_d<0x142, 0xa, 0xf>(s);          // row_bcast:15, rows 1,3
