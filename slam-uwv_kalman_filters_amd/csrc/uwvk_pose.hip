@@ -739,6 +739,10 @@ static hipError_t prepare_persist(uwvk_pose* h, EpochArgs& ea, int64_t& grid, in
   ea.tail0 = B;
   ea.r_x = 0;
   int c = h->tail_slots < 0 || h->lds_pad > 0 || s <= 0 ? 1 : tail_plan(h, B, s, ea.count);
+  // the pair kernel's default: no spreading (r06v, interleaved: off +2.4% at 20
+  // epochs, a tie at 200; forced 3 / 4 chunks -6% / -18% at 20); an explicit
+  // UWVK_OPT_TAIL_SLOTS > 0 or UWVK_OPT_TAIL_CHUNKS still spreads (tests)
+  if (pair && h->tail_slots == 0 && h->tail_force < 2) c = 1;
   if (c > 1) {
     const int64_t r = c * s;
     hipError_t e = tail_buffers(h, r, 8 * s);

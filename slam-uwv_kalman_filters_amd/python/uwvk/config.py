@@ -20,7 +20,7 @@ A file holds up to four top-level sections:
                   (inertia_matrix, damping_matrices: 6x6 nested lists or 36
                   values row-major; weight, buoyancy, distance_body2center*)
     engine:       handle options (so3_right, dense_sigma, literal_apply_delta,
-                  tail_slots, tail_chunks, persist), `apply_engine_options`
+                  tail_slots, tail_chunks, persist, param_block, pair), `apply_engine_options`
     visual_landmarks may also sit at top level instead of inside pose_config.
 
 `visual_landmarks` (VisualLandmarkConfiguration, PoseUKFConfig.hpp:111-143) is
@@ -43,7 +43,8 @@ import numpy as np
 
 from . import abi
 
-ENGINE_OPTIONS = ("so3_right", "dense_sigma", "literal_apply_delta", "tail_slots", "tail_chunks", "persist")
+ENGINE_OPTIONS = ("so3_right", "dense_sigma", "literal_apply_delta", "tail_slots", "tail_chunks", "persist",
+                  "param_block", "pair")
 
 
 class ConfigError(ValueError):
@@ -252,7 +253,7 @@ def from_dict(d, base_pose=None, base_uwv=None):
     for k, v in eng.items():
         if k not in ENGINE_OPTIONS:
             raise ConfigError("engine.%s: unknown option (known: %s)" % (k, ", ".join(ENGINE_OPTIONS)))
-        if k in ("so3_right", "dense_sigma", "literal_apply_delta"):
+        if k in ("so3_right", "dense_sigma", "literal_apply_delta", "param_block", "pair"):
             if not isinstance(v, bool):
                 raise ConfigError("engine.%s: expected true / false, got %r" % (k, v))
         elif k == "persist":
@@ -313,5 +314,9 @@ def apply_engine_options(batch, opts):
             batch.set_tail_chunks(v)
         elif k == "persist":
             batch.set_persist(int(v))
+        elif k == "param_block":
+            batch.set_param_block(bool(v))
+        elif k == "pair":
+            batch.set_pair(bool(v))
         else:
             raise ConfigError("engine.%s: unknown option" % k)

@@ -169,9 +169,17 @@ def test_apply_engine_options_calls():
         def __getattr__(self, n):
             return lambda *a: calls.append((n,) + a)
     config.apply_engine_options(Fake(), {"so3_right": True, "dense_sigma": False, "persist": 1, "tail_chunks": 2,
-                                         "tail_slots": -1})
+                                         "tail_slots": -1, "param_block": True, "pair": False})
     assert calls == [("set_so3_right", True), ("set_dense_sigma", False), ("set_persist", 1), ("set_tail_chunks", 2),
-                     ("set_tail_slots", -1)]
+                     ("set_tail_slots", -1), ("set_param_block", True), ("set_pair", False)]
+
+
+def test_engine_pair_options_parse():
+    """The r06 options (UWVK_OPT_PARAM_BLOCK, UWVK_OPT_PAIR) are booleans."""
+    c = config.loads("engine: {pair: false, param_block: true}\n")
+    assert c.engine == {"pair": False, "param_block": True}
+    with pytest.raises(config.ConfigError, match="engine.pair"):
+        config.loads("engine: {pair: 2}\n")
 
 
 @pytest.mark.gpu

@@ -407,8 +407,9 @@ def test_headline_shape_sampled(eng, orc, persist):
     (bench.window_shift) with its 5-epoch warm-up launch, then the 20-epoch
     window in ONE run_log launch (right SO3 side, no pressure / ADCP events):
     since r06 the default is the two-instances-per-wave parameter-decoupled
-    kernel k_psp_epoch_pair<1, 1, 1> on the persistent scheduler (pair units, tail
-    chunks spread over the ticket counter); persist=0 runs the one-instance
+    kernel k_psp_epoch_pair<1, 1, 1> on the persistent scheduler (pair units
+    from the ticket counter; no tail spreading for pair launches since r06v);
+    persist=0 runs the one-instance
     PD kernel k_psp_epoch_p<26, 1, 1, 1, 1> in the static tail-spread launch.
     16+ XCD-spread instances (tail instances included)
     against the oracle, each run alone on its own one-instance log (the
