@@ -605,7 +605,12 @@ def main():
             truth = log["truth"]
         dlog = f.upload_log(log)
         if s0 < e0:  # the alignment shift and the warm-up (untimed)
-            f.run_log(dlog, 0, min(s1, e0) - s0)
+            # in launches of the timed window's length, so that a kernel-trace
+            # summary of the command (rocprofv3 --stats) averages launches of
+            # the timed shape (the same epochs either way)
+            pre = min(s1, e0) - s0
+            for p0 in range(0, pre, max(1, a.steps)):
+                f.run_log(dlog, p0, min(max(1, a.steps), pre - p0))
         if si == 0:
             # warm the statistics kernels and the collective (module load, RCCL
             # channel set-up) outside the timed region
