@@ -604,17 +604,24 @@ def main():
                                      c4_cycle=cyc, cfg=cfg, epoch0=s0, epochs=s1 - s0)
             truth = log["truth"]
         dlog = f.upload_log(log)
-        if s0 < e0:  # the alignment shift and the warm-up (untimed)
-            # in launches of the timed window's length, so that a kernel-trace
-            # summary of the command (rocprofv3 --stats) averages launches of
-            # the timed shape (the same epochs either way)
-            pre = min(s1, e0) - s0
-            for p0 in range(0, pre, max(1, a.steps)):
-                f.run_log(dlog, p0, min(max(1, a.steps), pre - p0))
         if si == 0:
             # warm the statistics kernels and the collective (module load, RCCL
-            # channel set-up) outside the timed region
-            reduce_stats(truth.state(min(max(e0, s0), s1), a.dof))
+            # channel set-up) outside the timed region, ahead of the untimed
+            # epochs (its values are discarded)
+            reduce_stats(truth.state(s0, a.dof))
+        if s0 < e0:  # the alignment shift and the warm-up (untimed)
+            # in launches of the timed window's length, the remainder first, so
+            # that a kernel-trace summary of the command (rocprofv3 --stats)
+            # averages launches of the timed shape and the launch right before
+            # the window is one of them (the same epochs either way)
+            pre = min(s1, e0) - s0
+            n = max(1, a.steps)
+            p0 = 0
+            if pre % n:
+                f.run_log(dlog, 0, pre % n)
+                p0 = pre % n
+            for q in range(p0, pre, n):
+                f.run_log(dlog, q, min(n, pre - q))
         lo = max(s0, e0)
         if lo < s1:
             if pd_window is None:
