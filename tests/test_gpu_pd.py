@@ -206,10 +206,12 @@ def test_pair_tail_chunks_bitwise(eng, chunks):
 
 @pytest.mark.parametrize("mode,dof", [("C3", 53), ("C4", 53), ("C3", 26), ("C4", 26)])
 def test_pair_matches_oracle(eng, mode, dof):
-    """Pair-default handles (53-DOF decoupled, 26-DOF) against the oracle; C4 (compressed drop-out cycle):
-    the launches split around the pressure epochs (those on the one-instance PD
-    kernel, the runs between them on the pair kernel with the ADCP update), then
-    the efforts epochs couple the parameters and the general kernel takes over."""
+    """Pair-default handles (53-DOF decoupled, 26-DOF) against the oracle.  C4
+    (compressed drop-out cycle): the launches split around the pressure epochs
+    (those on the one-instance kernel, the runs between them on the pair kernel,
+    ADCP epochs 150 / 450 / 750 inside the runs); at 53 DOF the first full
+    efforts epoch (399) couples the parameters and the general kernel takes
+    over, at 26 DOF the pair kernel runs to the end."""
     from helpers import cov_err, init_both, state_err
     import oracle_ctypes as orc
     from uwvk import abi, synth
