@@ -169,10 +169,12 @@ def _run_pair(eng, log, cfg, uwv, pair, pieces, slots=-1, chunks=0, pd=True, dof
                                                ("C3", 600, [(0, 350), (350, 250)], 26),
                                                ("C4", 800, [(0, 450), (450, 350)], 26)])
 def test_pair_matches_single(eng, mode, E, pieces, dof):
-    """The pair kernel against the one-instance PD kernel (C4: the launches
-    split around the pressure epochs, ADCP epochs inside the pair runs, then
-    the efforts epochs, after which both run the general kernel): the same
-    filter to rounding (the rank-M update's order), gate decisions bitwise."""
+    """The pair kernel against the one-instance kernel (PD at 53 DOF, the
+    handle's own layout at 26).  C4: the launches split around the pressure
+    epochs, ADCP epochs inside the pair runs; at 53 DOF the first full efforts
+    epoch hands both handles to the general kernel, at 26 DOF the pair kernel
+    continues.  The same filter to rounding (the rank-M update's order), gate
+    decisions bitwise."""
     from helpers import cov_err, state_err
     from uwvk import synth
     B = 96
