@@ -491,13 +491,15 @@ uwvk_status uwvk_comm_allreduce_sum_device(void* comm, double* d_buf, int64_t n,
  *   general kernel until it is re-initialised.  0: always the general kernel.
  *   uwvk_pose_param_block says which the next launch runs. */
 #define UWVK_OPT_PARAM_BLOCK 9
-/* UWVK_OPT_PAIR (r06): 1 runs the parameter-decoupled kernel with two
- *   instances per wave (each on 32 lanes; uwvk_psp_pair.hip), when that kernel
- *   applies, the scheduler is persistent, the batch is even and the launch's
- *   epochs hold IMU and DVL updates only (the pressure update's 39 sigma points
- *   do not fit a half-wave).  The results
- *   agree with the one-instance kernel to rounding (the rank-M update sums in
- *   another order).  0: one instance per wave. */
+/* UWVK_OPT_PAIR (r06, default 1): run_log runs two instances per wave (each on
+ *   32 lanes; uwvk_psp_pair.hip) for 53-DOF handles while the parameter-
+ *   decoupled kernel applies and for 26-DOF handles, on the persistent
+ *   scheduler, an even batch and the lane-resident Q.  The pressure update's
+ *   39 sigma points do not fit a half-wave: a launch is split around its
+ *   pressure epochs (those run one instance per wave) when the runs between
+ *   them are at least 48 epochs long.  The results agree with the one-instance
+ *   kernel to rounding (the rank-M update sums in another order), gate
+ *   decisions bitwise.  0: one instance per wave. */
 #define UWVK_OPT_PAIR 10
 uwvk_status uwvk_pose_set_option(uwvk_pose* h, int option, int value);
 /* Host-only query (no device work): the chunks per tail instance the
@@ -516,8 +518,8 @@ int uwvk_pose_epoch_qshape(const uwvk_pose* h);
 /* Host-only query: 1 when the next run_log PSP launch runs the
  * parameter-decoupled kernel (UWVK_OPT_PARAM_BLOCK), else 0. */
 int uwvk_pose_param_block(uwvk_pose* h);
-/* Host-only query: 1 when that launch, if its epochs hold no pressure / ADCP
- * update, runs the two-instances-per-wave form (UWVK_OPT_PAIR). */
+/* Host-only query: 1 when run_log's launches (their epochs without a pressure
+ * update) run the two-instances-per-wave form (UWVK_OPT_PAIR). */
 int uwvk_pose_pair_active(uwvk_pose* h);
 /* 1 when a probe grid on device showed round-robin workgroup placement over 8
  * XCCs (block b on the XCC of block b % 8, read from the hardware XCC_ID
