@@ -78,8 +78,13 @@ constexpr int kLanes = PSP_PAIR ? 32 : 64;  // lanes per instance
 // within noise (profiles/r05/ab_prio/round3-4.txt).  Raising it over the
 // manifold mean, the update's points, the gain, apply_delta or the BodyEfforts
 // factor did not help (same runs).
+#if defined(PSP_NOPRIO)  // (A/B builds)
+UWVK_DEV void chain_prio_hi() {}
+UWVK_DEV void chain_prio_lo() {}
+#else
 UWVK_DEV void chain_prio_hi() { __builtin_amdgcn_s_setprio(1); }
 UWVK_DEV void chain_prio_lo() { __builtin_amdgcn_s_setprio(0); }
+#endif
 
 template <int DOF>
 struct PG {
