@@ -78,13 +78,8 @@ constexpr int kLanes = PSP_PAIR ? 32 : 64;  // lanes per instance
 // within noise (profiles/r05/ab_prio/round3-4.txt).  Raising it over the
 // manifold mean, the update's points, the gain, apply_delta or the BodyEfforts
 // factor did not help (same runs).
-#if defined(PSP_NOPRIO)  // (A/B builds)
-UWVK_DEV void chain_prio_hi() {}
-UWVK_DEV void chain_prio_lo() {}
-#else
 UWVK_DEV void chain_prio_hi() { __builtin_amdgcn_s_setprio(1); }
 UWVK_DEV void chain_prio_lo() { __builtin_amdgcn_s_setprio(0); }
-#endif
 
 template <int DOF>
 struct PG {
@@ -803,9 +798,6 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
   double mq[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) mq[i] = hread(o[i], 2 * K);
-#if PSP_PRIO_MORE && PSP_PAIR
-  chain_prio_hi();  // (A/B) the mean's Gauss-Newton iterations are a serial chain too
-#endif
   {
     int it = 0;
     double nrm;
@@ -826,9 +818,6 @@ UWVK_DEV bool psp_predict(PspSmem<DOF>& sm, const PoseShared& sh, const ProcCtx&
       for (int i = 0; i < 4; i++) mq[i] = q[i];
     } while (nrm > 1e-12 && ++it < 10000);  // |delta| > 1e-6
   }
-#if PSP_PRIO_MORE && PSP_PAIR
-  chain_prio_lo();
-#endif
   PSP_PHASE(22);
   // deviations; ori x ori block; Delta_j = d_{j+} - d_{j-}
   double d[3];
@@ -1748,9 +1737,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       if (j != i) S[j * M + i] = s + Rm[j * M + i];
     }
   double Si[M * M];
-#if PSP_PRIO_MORE && PSP_PAIR
-  chain_prio_hi();  // (A/B) S^-1, the gain, delta: a serial chain
-#endif
   small_inv<M>(S, Si);
   double Kg[M];
 #pragma unroll
@@ -1772,9 +1758,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     d2 += u * nu[j];
   }
   *ok = cok;
-#if PSP_PRIO_MORE && PSP_PAIR
-  chain_prio_lo();
-#endif
   const bool accept = gate == 0 ? true : !(d2 > kD2P95);
   if (!accept) return false;
   PSP_PHASE(33);
