@@ -163,9 +163,6 @@ static bool use_pd(const uwvk_pose* h) {
 // the two-instances-per-wave kernel (UWVK_OPT_PAIR): the parameter-decoupled
 // state of a 53-DOF handle, or a 26-DOF handle's own state (r06), on the
 // persistent scheduler, an even batch, the lane-resident Q and no LDS pad
-#ifndef UWVK_PAIR_SPLIT  // (A/B) 1: split launches around the pressure epochs (r06n)
-#define UWVK_PAIR_SPLIT 0
-#endif
 static bool pair_eligible(uwvk_pose* h) {
   if (!h->pair_opt || !h->persist || h->batch % 2 != 0 || h->lds_pad != 0 || use_dense(h)) return false;
   if (h->dof == 26) return q_is_simple(h);
@@ -910,9 +907,6 @@ uwvk_status uwvk_pose_run_log(uwvk_pose* h, const uwvk_pose_log* log, int64_t fi
     const bool pair_ok = pair_eligible(h);
     if (!pair_ok) {
       const uwvk_status st = launch_seg(e, last, false);
-      if (st != UWVK_OK) return st;
-    } else if (!UWVK_PAIR_SPLIT) {  // the pair kernel runs the pressure update too (two points per lane)
-      const uwvk_status st = launch_seg(e, last, true);
       if (st != UWVK_OK) return st;
     } else {
       constexpr int64_t kPairMinRun = 48;

@@ -463,32 +463,6 @@ UWVK_DEV void lds_sums(const double (&v)[R], double* buf, int l, double (&out)[R
   for (int i = 0; i < R; i++) out[i] = hread(p[0], i);
 }
 
-#if PSP_PAIR
-// lds_sums over NL > 32 contributors, two per lane (PSP_PAIR): contributor l
-// from v, contributor 32 + l (l < NL - 32) from v2
-template <int R, int NL>
-UWVK_DEV void lds_sums2(const double (&v)[R], const double (&v2)[R], double* buf, int l, double (&out)[R]) {
-  static_assert(NL % 2 == 0 && NL > 32 && NL <= 64 && R * NL <= 115, "transpose buffer (PG::STG)");
-#pragma unroll
-  for (int i = 0; i < R; i++) buf[i * NL + l] = v[i];
-  if (LANE_IF(l, l + 32 < NL)) {
-#pragma unroll
-    for (int i = 0; i < R; i++) buf[i * NL + 32 + l] = v2[i];
-  }
-  wsync();
-  const double* row = buf + (l < R ? l : 0) * NL;
-  double p[NL / 2];
-#pragma unroll
-  for (int k = 0; k < NL / 2; k++) p[k] = row[2 * k] + row[2 * k + 1];
-#pragma unroll
-  for (int w = 1; w < NL / 2; w *= 2)
-#pragma unroll
-    for (int k = 0; k + w < NL / 2; k += 2 * w) p[k] += p[k + w];
-#pragma unroll
-  for (int i = 0; i < R; i++) out[i] = hread(p[0], i);
-}
-#endif
-
 // phase boundary: the stamp of the diagnostic build, and (PSP_FAST & 4096) a
 // fresh laundered lane id, so that lane masks are recomputed per phase (one
 // v_cmp each) instead of being kept as SGPR pairs across the epoch, where they
@@ -647,28 +621,6 @@ UWVK_DEV constexpr bool has_rot() {
     if (RL::rows[q] >= 3 && RL::rows[q] < 6) return true;
   return false;
 }
-#if PSP_PAIR
-// the same for point OFF + p (PSP_PAIR, 2k + 1 > 32: the pressure update's 39
-// points, the second set in local lanes p < 2k + 1 - OFF; the others evaluate
-// the centre and are not used)
-template <class RL, int DOF, int K, int SR, int OFF>
-UWVK_DEV void gen_rows_off(const double* mu, const double* stg, int p, double x[Lay<DOF>::store]) {
-  using L = Lay<DOF>;
-  static_assert(OFF % 2 == 0, "point parity");
-#pragma unroll
-  for (int s = 0; s < L::store; s++) x[s] = mu[s];
-  const bool in = LANE_IF(p, p + OFF < 2 * K);
-  const int j = in ? ((p + OFF) >> 1) : 0;
-  const double sg = in ? (LANE_IF(p, (p & 1) != 0) ? -1.0 : 1.0) : 0.0;
-  double v[3] = {0.0, 0.0, 0.0};
-  gen_rows_q<RL, DOF, K, 0>(mu, stg, j, sg, v, x);
-  if constexpr (has_rot<RL>()) {
-    double e[4];
-    so3_exp_psp(v, e);
-    qplus_psp<SR>(e, mu + L::s_quat, x + L::s_quat);
-  }
-}
-#endif
 template <class RL, int DOF, int K, int SR>
 UWVK_DEV void gen_rows(const double* mu, const double* stg, int p, double x[Lay<DOF>::store]) {
   using L = Lay<DOF>;
@@ -1619,10 +1571,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
                          const HM& hm, bool* ok, double ds, double ids, Stamper* st = nullptr) {
   using L = Lay<DOF>;
   constexpr int M = HM::M, K = HM::K, NC = HM::NC, KA = K > 0 ? K : 1, NCA = NC > 0 ? NC : 1;
-  // pair: the 2k + 1 sigma points of an update in the half's 32 lanes, or (the
-  // pressure update, k = 19) two per lane, points 32 + l in the second set
-  constexpr bool kTwo = PSP_PAIR && 2 * K + 1 > 32;
-  static_assert(!PSP_PAIR || 2 * K + 1 <= 64, "pair: at most two sigma points per lane");
+  static_assert(!PSP_PAIR || 2 * K + 1 <= 32, "pair: the 2k + 1 sigma points of an update fit 32 lanes");
   int l = olane();  // re-laundered per phase (PSP_PHASE)
   double a[KA];
   bool cok = true;
@@ -1639,22 +1588,9 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     gen_rows<HM, DOF, K, SR>(sm.mu, sm.stg + STG_ROWS, l, x);
     hm.eval(x, zp);
   }
-  [[maybe_unused]] double zp2[M];
-#if PSP_PAIR
-  if constexpr (kTwo) {
-    double x[L::store];
-    gen_rows_off<HM, DOF, K, SR, 32>(sm.mu, sm.stg + STG_ROWS, l, x);
-    hm.eval(x, zp2);
-  }
-#endif
   double zc[M], zb[M], e[M];
-  if constexpr (kTwo) {  // the centre is point 2k: the second set's lane 2k - 32
 #pragma unroll
-    for (int i = 0; i < M; i++) zc[i] = hread(zp2[i], (2 * K - 32) & 31);
-  } else {
-#pragma unroll
-    for (int i = 0; i < M; i++) zc[i] = hread(zp[i], 2 * K);
-  }
+  for (int i = 0; i < M; i++) zc[i] = hread(zp[i], 2 * K);
   constexpr double wc = 1.0 + 2.0 * (NW - K);
   double S[M * M];
   // H and P first: P reads the staged rows, after which stg holds the
@@ -1693,19 +1629,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     for (int i2 = 0; i2 < M; i2++)
 #pragma unroll
       for (int j2 = 0; j2 <= i2; j2++) v[k++] = v[i2] * v[j2];
-#if PSP_PAIR
-    if constexpr (kTwo) {
-      double v2[R];
-#pragma unroll
-      for (int i2 = 0; i2 < M; i2++) v2[i2] = zp2[i2] - zc[i2];
-      int k2 = M;
-#pragma unroll
-      for (int i2 = 0; i2 < M; i2++)
-#pragma unroll
-        for (int j2 = 0; j2 <= i2; j2++) v2[k2++] = v2[i2] * v2[j2];
-      lds_sums2<R, 2 * K>(v, v2, sm.stg, l, sums);
-    } else
-#endif
     if constexpr (R * 2 * K <= 115) lds_sums<R, 2 * K, 1>(v, sm.stg, l, sums);
     else lds_sums_chunked<R, 2 * K, 1>(v, sm.stg, l, sums);  // M = 6 (constrainVelocity)
     double m[M];
@@ -1735,11 +1658,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
   double zd[M];
 #pragma unroll
   for (int i = 0; i < M; i++) zd[i] = K > 0 ? zp[i] - swap_pair_d(zp[i]) : 0.0;
-  [[maybe_unused]] double zd2[M];
-  if constexpr (kTwo) {
-#pragma unroll
-    for (int i = 0; i < M; i++) zd2[i] = zp2[i] - swap_pair_d(zp2[i]);
-  }
   PSP_PHASE(31);
   const int rl = l < DOF ? l : DOF - 1;
   const int Trl = (rl * (rl + 1)) >> 1;
@@ -1771,12 +1689,6 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     if (LANE_IF(l, (l & 1) == 0 && l < 2 * K)) {
 #pragma unroll
       for (int i = 0; i < M; i++) sm.stg[P0 + PS * K + (l >> 1) * PS + i] = zd[i];
-    }
-    if constexpr (kTwo) {  // Dz_j for j = 16 + l / 2 (the second point set)
-      if (LANE_IF(l, (l & 1) == 0 && l + 32 < 2 * K)) {
-#pragma unroll
-        for (int i = 0; i < M; i++) sm.stg[P0 + PS * K + ((l + 32) >> 1) * PS + i] = zd2[i];
-      }
     }
     wsync();
     double g[M], c[M];

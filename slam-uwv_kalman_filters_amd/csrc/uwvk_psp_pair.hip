@@ -247,10 +247,11 @@ UWVK_DEV const PoseShared& shared_for_epoch(const PoseBufs& b) {
 // The pair kernel's persistent work loop: block b runs pair unit b first, then
 // takes units from the ticket counter (k_psp_epoch_p's scheme); unit u is
 // instances 2u (lanes 0..31) and 2u + 1 (lanes 32..63).
-// EVS = 1: the launch's epochs hold no pressure or ADCP update (not compiled
-// in).  The pressure update's nonlinear prefix is k = 19 (pos .. gravity;
-// PoseUKF.cpp:107-115): 39 sigma points, two per lane (psp_update's second
-// point set).
+// Launches without pressure epochs only (EpochArgs flags host-checked): the
+// pressure update's nonlinear prefix is k = 19 (pos .. gravity;
+// PoseUKF.cpp:107-115), 39 sigma points, more than a half-wave holds; run_log
+// runs those epochs on the one-instance PD kernel.  EVS = 1: no ADCP epoch in
+// the launch either (the ADCP update, k = 6, not compiled in).
 // PD = 1: a 53-DOF handle's parameter-decoupled state (NW = 53, the 27
 // parameters in pS / pm); PD = 0 (r06): a 26-DOF kinematic handle's own state
 // (NW = 26, no parameter lanes).
@@ -350,19 +351,6 @@ void k_psp_epoch_pair(PoseBufs b, PoseShared sh0, EpochArgs ea) {
         }
       }
       if constexpr (EVS == 0) {
-        if (fl & UWVK_EV_PRESSURE) {  // measurementPressureSensor (PoseUKF.cpp:107-115): k = 19, two points per lane
-          const double* zp = ea.pressure + (int64_t)ea.p_index[e] * B + inst;
-          if (finite_n(zp, 1)) {
-            double z[1] = {zp[0]}, R[1] = {ea.p_cov};
-            PPressure<26> hp;
-            hp.h.s[0] = ea.p_sens[0]; hp.h.s[1] = ea.p_sens[1]; hp.h.s[2] = ea.p_sens[2];
-            hp.h.patm = sh.p.atmospheric_pressure;
-            cnt[1] += psp_update<26, SR, PPressure<26>, NW>(sm, z, R, 0, hp, &sok, ds, ids);
-            ok = ok && sok;
-          } else {
-            nan = true;
-          }
-        }
         if (fl & UWVK_EV_ADCP) {  // measurementWaterCurrents per cell (PoseUKF.cpp:133-151, :514-527)
           for (int c = 0; c < ea.cells; c++) {
             const double* zp = ea.adcp + (((int64_t)ea.a_index[e] * ea.cells + c) * B + inst) * 2;
@@ -413,7 +401,8 @@ template <int SR, int PD>
 static hipError_t launch_pair_sr(hipStream_t st, const PoseBufs& b, const PoseShared& sh, const EpochArgs& ea,
                                  int64_t grid, uint32_t ev_any) {
   const dim3 g((unsigned)grid), t(64);
-  if (ev_any & (UWVK_EV_PRESSURE | UWVK_EV_ADCP)) hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR, 0, PD>), g, t, 0, st, b, sh, ea);
+  if (ev_any & UWVK_EV_PRESSURE) return hipErrorInvalidValue;  // (run_log splits those epochs off)
+  if (ev_any & UWVK_EV_ADCP) hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR, 0, PD>), g, t, 0, st, b, sh, ea);
   else hipLaunchKernelGGL((psp2::k_psp_epoch_pair<SR, 1, PD>), g, t, 0, st, b, sh, ea);
   return hipGetLastError();
 }

@@ -133,7 +133,7 @@ def test_psp_epoch_kernels_keep_their_occupancy(src, side):
 # 26-DOF handles): 3 waves per SIMD (<= 168
 # registers; the r06g A/B measured 3 > 2 > 4 waves: 347.6 / 299.6 / 278.8 M
 # steps/s at C3, 200 epochs) with a bounded spill area (180 B/lane without the
-# ADCP and pressure updates, 420 with them, at r06).
+# ADCP update, 272 with it, at r06).
 @pytest.mark.skipif(not HAVE_HIPCC, reason="no hipcc")
 def test_pair_kernel_keeps_three_waves_per_simd():
     u = kernel_usage("csrc/uwvk_psp_pair.hip", ("_ZN4uwvk4psp216k_psp_epoch_pairILi",))
@@ -142,7 +142,7 @@ def test_pair_kernel_keeps_three_waves_per_simd():
     for name, r in u.items():
         sr, evs, pd = map(int, re.search(r"pairILi(\d)ELi(\d)ELi(\d)E", name).groups())
         regs = r["vgpr"] + r.get("agpr", 0)
-        assert regs <= 168 and r["occupancy"] >= 3 and r["scratch"] <= (256 if evs else 448), (name, r)
+        assert regs <= 168 and r["occupancy"] >= 3 and r["scratch"] <= (256 if evs else 320), (name, r)
 
 
 # The BodyEfforts kernels (k_psp_efforts<DOF, VO, SR>, r05): no scratch, at
