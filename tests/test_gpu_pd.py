@@ -239,3 +239,33 @@ def test_pair_matches_oracle(eng, mode, dof):
     xo, Po = o.get_state()
     xg, Pg = g.get_state()
     assert state_err(xg, xo, Po, dof).max() < 1e-7 and cov_err(Pg, Po).max() < 1e-7
+
+
+def test_pair_eligibility(eng):
+    """Where run_log takes the pair kernel (uwvk_pose_pair_active): 53-DOF
+    handles while decoupled and 26-DOF handles, on an even batch, the
+    persistent scheduler and the PSP path; otherwise one instance per wave."""
+    from uwvk import synth
+    cfg, uwv = synth.default_pose_config(), synth.default_uwv()
+
+    def mk(B, dof):
+        log = synth.make_pose_log(B, 4, "C3", dof=dof)
+        g = eng.PoseUKFBatch(B, dof)
+        g.init_from_config(log["pos0"], log["pos_cov"], log["rot0"], log["rot_cov"], cfg, uwv)
+        g.set_process_noise_from_config(cfg, 1e-3)
+        return g
+    assert mk(6, 53).pair_active() == 1
+    assert mk(6, 26).pair_active() == 1
+    assert mk(5, 53).pair_active() == 0  # odd batch
+    g = mk(6, 53)
+    g.set_persist(False)
+    assert g.pair_active() == 0
+    g.set_persist(True)
+    g.set_pair(False)
+    assert g.pair_active() == 0
+    g.set_pair(True)
+    g.set_param_block(False)  # the general 53-DOF kernel
+    assert g.pair_active() == 0
+    g = mk(6, 26)
+    g.set_dense_sigma(True)
+    assert g.pair_active() == 0
