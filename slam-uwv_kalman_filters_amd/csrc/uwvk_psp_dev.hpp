@@ -298,6 +298,15 @@ UWVK_DEV constexpr unsigned long long rows_mask() {
   for (int k = 0; k < RL::NR; k++) m |= 1ull << RL::rows[k];
   return m;
 }
+// lanes of a measurement model's affine Jacobian columns (HM::cols, ascending)
+template <class HM>
+UWVK_DEV constexpr unsigned long long cols_mask() {
+  unsigned long long m = 0;
+  for (int k = 0; k < HM::NC; k++) m |= 1ull << HM::cols[k];
+  for (int k = 1; k < HM::NC; k++)
+    if (HM::cols[k] <= HM::cols[k - 1]) return 0;  // (not ascending: unusable, see the static_assert)
+  return m;
+}
 template <class RL>
 UWVK_DEV constexpr bool rows_ascending() {
   for (int k = 1; k < RL::NR; k++)
@@ -1725,13 +1734,41 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       C[i] = Gr[i];
     }
   }
+#if PSP_PAIR && PSP_GL_LDS
+  // (A/B) Gl of the Jacobian's columns through the staging area: lane c of
+  // column rank t (HM::cols ascending) writes Gl[.] to stg[t M + .], every
+  // lane reads them back as broadcasts (instead of one hread per (t, j))
+  double glb[NCA][M];
+  {
+    static_assert(NC * M <= PG<DOF>::STG, "Gl staging (PG::STG)");
+    constexpr unsigned long long cm = cols_mask<HM>();
+    static_assert(NC == 0 || (cm != 0 && (cm >> 32) == 0), "HM::cols ascending, below 32");
+    const int t = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(rep_mask(cm) >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((unsigned)rep_mask(cm), 0u)) -
+                  (upper_half() ? __builtin_popcount((unsigned)cm) : 0);
+    if (LANE_IN(cm)) {
+#pragma unroll
+      for (int j = 0; j < M; j++) sm.stg[t * M + j] = Gl[j];
+    }
+    wsync();
+#pragma unroll
+    for (int tt = 0; tt < NC; tt++)
+#pragma unroll
+      for (int j = 0; j < M; j++) glb[tt][j] = sm.stg[tt * M + j];
+    wsync();  // stg is rewritten by the rank-M staging
+  }
+#endif
 #pragma unroll
   for (int i = 0; i < M; i++)
 #pragma unroll
     for (int j = 0; j <= i; j++) {
       double hg = 0.0;
 #pragma unroll
+#if PSP_PAIR && PSP_GL_LDS
+      for (int t = 0; t < NC; t++) hg = hfma(Hs[i][t], glb[t][j], hg);
+#else
       for (int t = 0; t < NC; t++) hg = hfma(Hs[i][t], hread(Gl[j], HM::cols[t]), hg);
+#endif
       const double s = S[i * M + j] + hg;
       S[i * M + j] = s + Rm[i * M + j];
       if (j != i) S[j * M + i] = s + Rm[j * M + i];
