@@ -1734,10 +1734,12 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
       C[i] = Gr[i];
     }
   }
-#if PSP_PAIR && PSP_GL_LDS
-  // (A/B) Gl of the Jacobian's columns through the staging area: lane c of
-  // column rank t (HM::cols ascending) writes Gl[.] to stg[t M + .], every
-  // lane reads them back as broadcasts (instead of one hread per (t, j))
+#if PSP_PAIR
+  // Gl of the Jacobian's columns through the staging area: lane c of column
+  // rank t (HM::cols ascending) writes Gl[.] to stg[t M + .], every lane reads
+  // them back as LDS broadcasts -- one hread per (t, j) costs a DPP pair or a
+  // readlane + select per half (r06zf: -0.5 % kernel time at 20 epochs,
+  // -0.8 % at 200)
   double glb[NCA][M];
   {
     static_assert(NC * M <= PG<DOF>::STG, "Gl staging (PG::STG)");
@@ -1764,7 +1766,7 @@ UWVK_DEV bool psp_update(PspSmem<DOF>& sm, const double (&z)[HM::M], const doubl
     for (int j = 0; j <= i; j++) {
       double hg = 0.0;
 #pragma unroll
-#if PSP_PAIR && PSP_GL_LDS
+#if PSP_PAIR
       for (int t = 0; t < NC; t++) hg = hfma(Hs[i][t], glb[t][j], hg);
 #else
       for (int t = 0; t < NC; t++) hg = hfma(Hs[i][t], hread(Gl[j], HM::cols[t]), hg);
