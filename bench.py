@@ -483,7 +483,11 @@ def make_rccl(dist, engine, world, rank, local):
 def collective_desc(dist, world, comm, comm_err, same_dev):
     """config.collective of the bench line: which all-reduce summed the
     ensemble statistics (None for a single-process run)."""
-    if dist is None or world == 1:
+    if world == 1:
+        c = os.environ.get("UWVK_BENCH_COLL", "")
+        return {"rccl1": "one-rank RCCL communicator through the timed region (N = 1 rehearsal)",
+                "scoped": "one-rank RCCL communicator made around each statistics all-reduce (N = 1 rehearsal)"}.get(c)
+    if dist is None:
         return None
     if comm is not None:
         return "RCCL all_reduce of the ensemble statistics on the handle's stream (uwvk_pose_ensemble_allreduce)"
@@ -567,12 +571,27 @@ def main():
     # DESIGN.md section 8), part of C5's cost.  RCCL refuses two ranks on one
     # GPU, so the one-GPU rehearsal (UWVK_BENCH_SAME_DEVICE) sums over gloo;
     # UWVK_BENCH_COLL=host does the same on purpose (A/B).
-    coll = "host" if (same_dev or os.environ.get("UWVK_BENCH_COLL") == "host") else "rccl"
+    # One-GPU measurements of the communicator's cost at
+    # N = 1: UWVK_BENCH_COLL=rccl1 makes a one-rank communicator before the
+    # timed region and sums through it (the N > 1 lifetime); =scoped makes it
+    # around each statistics all-reduce and destroys it after (its set-up
+    # inside the timed region).
+    coll_env = os.environ.get("UWVK_BENCH_COLL", "")
+    coll = "host" if (same_dev or coll_env == "host") else "rccl"
     comm, comm_err = None, None
     if dist is not None and world > 1 and coll == "rccl":
         comm, comm_err = make_rccl(dist, engine, world, rank, local)
+    if world == 1 and coll_env == "rccl1":
+        comm = engine.RcclComm(1, engine.RcclComm.unique_id(), 0, local)
+    scoped = world == 1 and coll_env == "scoped"
 
     def reduce_stats(truth):
+        if scoped:
+            c1 = engine.RcclComm(1, engine.RcclComm.unique_id(), 0, local)
+            try:
+                return f.ensemble_stats(truth, c1)
+            finally:
+                c1.close()
         st = f.ensemble_stats(truth, comm)
         if dist is not None and world > 1 and comm is None:
             st = ensemble.allreduce_stats(st, dist)

@@ -219,3 +219,15 @@ def test_eight_rank_spawn_and_collective_text(tmp_path, fail):
         assert all(t.startswith("RCCL all_reduce") for t in texts)
     else:
         assert all(t.startswith("gloo all_reduce") and "RCCL communicator failed" in t for t in texts)
+
+
+def test_collective_desc_one_gpu_rehearsals(monkeypatch):
+    """N = 1 names the communicator rehearsal UWVK_BENCH_COLL asks for (the
+    one-rank communicator through the window, or made around each all-reduce),
+    and no collective without one."""
+    monkeypatch.delenv("UWVK_BENCH_COLL", raising=False)
+    assert bench.collective_desc(None, 1, None, None, False) is None
+    monkeypatch.setenv("UWVK_BENCH_COLL", "rccl1")
+    assert "through the timed region" in bench.collective_desc(None, 1, None, None, False)
+    monkeypatch.setenv("UWVK_BENCH_COLL", "scoped")
+    assert "around each statistics all-reduce" in bench.collective_desc(None, 1, None, None, False)
