@@ -566,9 +566,10 @@ def main():
     # The collective (C5): the per-rank ensemble statistics summed over the
     # engine's RCCL communicator on the handle's stream (uwvk_pose_ensemble_
     # allreduce), every --stats-every epochs and at the end of the window.  The
-    # communicator is made before the timed region and lives through it: an
-    # RCCL communicator costs the running epoch kernel ~6% of its clock (DVFS,
-    # DESIGN.md section 8), part of C5's cost.  RCCL refuses two ranks on one
+    # communicator is made before the timed region and lives through it (made
+    # around each all-reduce, its set-up would be ~0.6 s of the window; a live
+    # one-rank communicator no longer slows the epoch kernel, r06zh, DESIGN.md
+    # section 8).  RCCL refuses two ranks on one
     # GPU, so the one-GPU rehearsal (UWVK_BENCH_SAME_DEVICE) sums over gloo;
     # UWVK_BENCH_COLL=host does the same on purpose (A/B).
     # One-GPU measurements of the communicator's cost at
